@@ -1,0 +1,186 @@
+/*
+ * rnsntt.h -- C-ABI of the MI355X-native RNS-NTT backend (librnsntt.so).
+ *
+ * Drop-in boundary for oiwn/toy-heaan-ckks's `RnsPoly<N>` / `RnsBasis<N>`
+ * (src/rings/backends/rns_ntt/) and the key-switch / rescale loops of
+ * `CkksEngine` (src/crypto/engine.rs).  Each entry point names the reference
+ * interface it replaces (paths relative to the reference repository root).
+ *
+ * Conventions
+ *  - Every function returns an `int` status: 0 = OK, otherwise one of
+ *    RNT_ERR_*.  No exception, abort or panic crosses this boundary.
+ *    `rnt_last_error()` returns a thread-local human-readable message for the
+ *    last failing call on the calling thread.
+ *  - Host polynomial data is exactly the reference's memory: a polynomial is
+ *    `Vec<[u64; N]>`, i.e. `uint64_t[L][N]` (limb-major, "channels"); a batch
+ *    of B polynomials is `uint64_t[B][L][N]`.  Rust passes
+ *    `channels.as_ptr() as *const u64`.
+ *  - NTT-domain data crossing the boundary is in the reference's natural
+ *    order: index k holds a(psi^(2k+1)) mod q_i (poly.rs:136-148).  The
+ *    device-internal order is private.
+ *  - Ops are asynchronous on the context's stream; `rnt_sync` waits.
+ *    Uploads and downloads are synchronous (they validate / return host
+ *    data).
+ *  - Threading: a context is immutable after creation and may be shared by
+ *    any number of host threads (it is the reference's `Arc<RnsBasis>`).  A
+ *    buffer must not be used by two threads at once (the reference's `&mut`).
+ */
+#ifndef RNSNTT_H
+#define RNSNTT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RNT_ABI_VERSION 1
+
+/* Status codes.  1..6 mirror RnsNttError in order
+ * (src/rings/backends/rns_ntt/errors.rs:4-20). */
+enum {
+  RNT_OK = 0,
+  RNT_ERR_INVALID_DEGREE = 1,      /* RnsNttError::InvalidDegree          */
+  RNT_ERR_EMPTY_BASIS = 2,         /* RnsNttError::EmptyBasis             */
+  RNT_ERR_NON_NTT_FRIENDLY = 3,    /* RnsNttError::NonNttFriendlyModulus  */
+  RNT_ERR_INVALID_MOD_DROP = 4,    /* RnsNttError::InvalidModDrop         */
+  RNT_ERR_CHANNEL_COUNT = 5,       /* RnsNttError::ChannelCountMismatch   */
+  RNT_ERR_NON_REDUCED = 6,         /* RnsNttError::NonReducedCoefficient  */
+  RNT_ERR_DOMAIN_MISMATCH = 7,     /* reference: debug_assert only (poly.rs:264-267, 292-295) */
+  RNT_ERR_BASIS_MISMATCH = 8,      /* reference: debug_assert Arc::ptr_eq (poly.rs:260-263, 288-291) */
+  RNT_ERR_DEVICE = 9,              /* HIP runtime error                   */
+  RNT_ERR_OUT_OF_MEMORY = 10,
+  RNT_ERR_BAD_ARGUMENT = 11
+};
+
+typedef struct rnt_ctx rnt_ctx; /* == Arc<RnsBasis<N>> (basis.rs:90-94) */
+typedef struct rnt_buf rnt_buf; /* == device storage of B RnsPoly (poly.rs:25-30) */
+
+/* ---- library / diagnostics ------------------------------------------- */
+int rnt_abi_version(void);
+const char* rnt_last_error(void);
+const char* rnt_status_string(int status);
+
+/* Number of visible HIP devices (0 without a GPU; never fails on CPU-only
+ * hosts). */
+int rnt_device_count(int* n);
+
+/* ---- per-kernel timing (diagnostics; not thread-safe) ------------------ */
+/* When enabled on a context, every kernel the library launches on that
+ * context's stream is bracketed by HIP events; rnt_profile_read syncs and
+ * returns, for one kernel name ("col_fwd", "row_fwd", "row_inv",
+ * "row_mul", "col_inv", "elementwise", "rescale", "automorphism",
+ * "ks_decompose", "ks_rows", "tensor_rows", "import", "export"), the
+ * launch count and summed device milliseconds since enabling. */
+int rnt_profile_enable(const rnt_ctx* ctx, int enable);
+int rnt_profile_read(const rnt_ctx* ctx, const char* kernel, uint64_t* launches,
+                     double* total_ms);
+
+/* ---- host-side number theory (no device needed) ----------------------- */
+/* is_ntt_friendly_prime (src/math/primes.rs:125-131); writes 0/1. */
+int rnt_is_ntt_friendly_prime(uint64_t p, uint64_t degree, int* out);
+/* generate_primes (src/math/utils.rs:47-80): `count` descending NTT-friendly
+ * primes of exactly `bit_size` bits for `degree`. */
+int rnt_generate_primes(uint32_t bit_size, size_t count, uint64_t degree,
+                        uint64_t* out);
+/* psi of NttTable::new (basis.rs:39-40, find_primitive_root :217-237). */
+int rnt_find_psi(uint64_t modulus, uint64_t degree, uint64_t* psi);
+
+/* ---- context == RnsBasis ---------------------------------------------- */
+/* RnsBasis::new (basis.rs:97-106) + NttTable::new per modulus (:20-84):
+ * validates like the reference, builds the device tables on `device`. */
+int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t count,
+                   int device, rnt_ctx** out);
+int rnt_ctx_destroy(rnt_ctx* ctx);
+/* RnsBasis::drop_last (basis.rs:121-134): a prefix view sharing the
+ * parent's device tables (no table copy). */
+int rnt_ctx_drop_last(const rnt_ctx* ctx, size_t drop_count, rnt_ctx** out);
+int rnt_ctx_degree(const rnt_ctx* ctx, size_t* n);
+int rnt_ctx_channel_count(const rnt_ctx* ctx, size_t* count); /* basis.rs:116-118 */
+int rnt_ctx_moduli(const rnt_ctx* ctx, uint64_t* out);       /* basis.rs:108-110 */
+int rnt_ctx_total_bits(const rnt_ctx* ctx, uint32_t* bits);  /* basis.rs:140-145 */
+int rnt_ctx_psi(const rnt_ctx* ctx, size_t limb, uint64_t* psi);
+/* The context's HIP stream (hipStream_t) for event timing / interop. */
+int rnt_ctx_stream(const rnt_ctx* ctx, void** stream);
+int rnt_sync(const rnt_ctx* ctx);
+
+/* ---- buffers == batches of RnsPoly ------------------------------------ */
+/* Allocates device storage for n_polys polynomials over ctx's basis, all
+ * zero, coefficient domain (RnsPoly::zero, poly.rs:36-43). */
+int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out);
+int rnt_buf_free(rnt_buf* buf);
+int rnt_buf_n_polys(const rnt_buf* buf, size_t* n);
+int rnt_buf_is_ntt(const rnt_buf* buf, int* in_ntt); /* is_ntt_domain, poly.rs:127-129 */
+/* RnsPoly::from_channels (poly.rs:73-99) for a batch: host
+ * uint64_t[n_polys][channels][N]; `channels` must equal the basis' channel
+ * count (else RNT_ERR_CHANNEL_COUNT); every residue must be < q_i (else
+ * RNT_ERR_NON_REDUCED).  `in_ntt` != 0: natural-order NTT-domain data. */
+int rnt_upload(rnt_buf* buf, const uint64_t* host, size_t n_polys,
+               size_t channels, int in_ntt);
+/* RnsPoly::from_coeffs (poly.rs:49-67) for a batch: host int64_t[n_polys][N]
+ * reduced by rem_euclid per channel; result in coefficient domain. */
+int rnt_upload_coeffs(rnt_buf* buf, const int64_t* coeffs, size_t n_polys);
+/* RnsPoly::channels (poly.rs:119-121): copies uint64_t[n_polys][L][N] out,
+ * in the buffer's current domain (natural order when NTT). */
+int rnt_download(const rnt_buf* buf, uint64_t* host, size_t n_polys);
+int rnt_copy(rnt_buf* dst, const rnt_buf* src); /* Clone */
+
+/* ---- ring ops (batched; every poly of the buffers participates) -------- */
+/* to_ntt_domain / to_coeff_domain (poly.rs:136-166); no-ops when already
+ * in the target domain. */
+int rnt_ntt_fwd(rnt_buf* buf);
+int rnt_ntt_inv(rnt_buf* buf);
+/* MulAssign (poly.rs:277-331) as out = a * b: both NTT -> pointwise, result
+ * NTT; both coefficient -> negacyclic product, result coefficient.  Mixed
+ * domains -> RNT_ERR_DOMAIN_MISMATCH.  out may alias a or b. */
+int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b);
+/* AddAssign (poly.rs:254-275) as out = a + b, either domain (must match). */
+int rnt_add(rnt_buf* out, const rnt_buf* a, const rnt_buf* b);
+int rnt_sub(rnt_buf* out, const rnt_buf* a, const rnt_buf* b);
+/* Neg (poly.rs:370-385), either domain. */
+int rnt_neg(rnt_buf* out, const rnt_buf* a);
+/* rescale_into (poly.rs:187-228): `out` belongs to a context equal to
+ * drop_last(1) of `in`'s; result coefficient domain, floor division by the
+ * last prime. */
+int rnt_rescale(rnt_buf* out, const rnt_buf* in);
+/* mod_drop_last (poly.rs:169-177): out (a context equal to drop_last(k) of
+ * in's) receives the first L-k channels; domain preserved. */
+int rnt_mod_drop_last(rnt_buf* out, const rnt_buf* in);
+/* automorphism X -> X^g (poly.rs:492-541). Output coefficient domain, except
+ * g mod 2N == 0 which copies `in` (domain preserved) like the reference. */
+int rnt_automorphism(rnt_buf* out, const rnt_buf* in, uint64_t g);
+/* rotate_slots (poly.rs:546-569): g = 5^k mod 2N (k >= 0); for k < 0 the
+ * reference's automorphism(5^|k|) then automorphism(2N-1). */
+int rnt_rotate_slots(rnt_buf* out, const rnt_buf* in, int32_t k);
+
+/* ---- engine-level fused ops (src/crypto/engine.rs) -------------------- */
+/* A gadget key (RnsGadgetRelinKey / RnsGadgetRotationKey, engine.rs:224-253):
+ * key_a and key_b are buffers of L polys each (poly i = a_i / b_i).  They
+ * are kept device-resident in the NTT domain; rnt_key_prepare transforms
+ * them once. */
+int rnt_key_prepare(rnt_buf* key_a, rnt_buf* key_b);
+/* Gadget key-switch sum (engine.rs:505-528 / :429-452): for every poly of d
+ * (coefficient domain): acc0 = sum_i alpha_i(d) * key_b[i],
+ * acc1 = sum_i alpha_i(d) * key_a[i]; outputs coefficient domain. */
+int rnt_keyswitch(rnt_buf* acc0, rnt_buf* acc1, const rnt_buf* d,
+                  const rnt_buf* key_a, const rnt_buf* key_b);
+/* mul_ciphertexts_gadget (engine.rs:473-539) for a batch of ciphertext
+ * pairs: tensor product + gadget relinearization.  Inputs coefficient
+ * domain; outputs coefficient domain. */
+int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
+                     const rnt_buf* c1, const rnt_buf* c0p, const rnt_buf* c1p,
+                     const rnt_buf* key_a, const rnt_buf* key_b);
+/* rotate_ciphertext (engine.rs:412-463). */
+int rnt_ct_rotate(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
+                  const rnt_buf* c1, int32_t k, const rnt_buf* key_a,
+                  const rnt_buf* key_b);
+/* rescale_ciphertext (engine.rs:263-282): both components onto the same
+ * dropped basis. */
+int rnt_ct_rescale(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
+                   const rnt_buf* c1);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RNSNTT_H */

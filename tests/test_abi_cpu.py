@@ -1,0 +1,106 @@
+"""C-ABI checks that need no GPU: the library loads, exports exactly what
+include/rnsntt.h declares, its host-side setup math matches the oracle and
+the reference KATs, and validation errors come back as the reference's
+RnsNttError variants."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import pyoracle as orc
+import rns_ntt
+from rns_ntt import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    text = open(os.path.join(REPO, "include", "rnsntt.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(rnt_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    lib = rns_ntt.load()
+    assert lib.rnt_abi_version() == 1
+    names = declared_functions()
+    assert len(names) >= 35
+    for n in names:
+        assert hasattr(lib, n), n
+    # the Python binding types every declared function
+    assert sorted(_lib.SIGNATURES) == names
+
+
+def test_status_strings_mirror_rnsntt_error():
+    lib = rns_ntt.load()
+    want = ["ok", "InvalidDegree", "EmptyBasis", "NonNttFriendlyModulus", "InvalidModDrop",
+            "ChannelCountMismatch", "NonReducedCoefficient"]
+    for code, name in enumerate(want):
+        assert lib.rnt_status_string(code).decode() == name
+
+
+def test_generate_primes_matches_oracle_and_configs(vectors, manifest):
+    for name, m in manifest.items():
+        mods = rns_ntt.generate_primes(m["bits"], m["L"], m["n"])
+        assert mods == [int(x) for x in vectors[f"{name}/moduli"]], name
+        assert mods == orc.generate_primes(m["bits"], m["L"], m["n"])
+        if f"{name}/psi" in vectors:
+            for q, psi in zip(mods, vectors[f"{name}/psi"]):
+                assert rns_ntt.find_psi(q, m["n"]) == int(psi)
+
+
+def test_prime_kats(kats):
+    k = kats["primes"]
+    f = k["ntt_friendly_condition"]
+    assert all(rns_ntt.is_ntt_friendly_prime(p, f["n"]) for p in f["friendly"])
+    assert not any(rns_ntt.is_ntt_friendly_prime(p, f["n"]) for p in f["not_friendly"])
+    g = k["generates_ntt_primes_in_range"]
+    ps = rns_ntt.generate_primes(g["bits"], g["count"], g["degree"])
+    assert all((1 << 19) <= q < (1 << 20) and rns_ntt.is_ntt_friendly_prime(q, 1024) for q in ps)
+    g = k["panics_when_not_enough_primes"]
+    with pytest.raises(rns_ntt.RnsNttError):
+        rns_ntt.generate_primes(g["bits"], g["count"], g["degree"])
+    # primality through the friendly test at degree 1 (p = 1 mod 2 <=> odd prime)
+    for p in k["is_prime_large"]["prime"] + k["near_u64_limit"]["prime"]:
+        assert rns_ntt.is_ntt_friendly_prime(p, 1)
+    for c in k["is_prime_large"]["composite"] + k["tricky_composites"]["composite"]:
+        assert not rns_ntt.is_ntt_friendly_prime(c, 1)
+    for lo, hi in k["miller_rabin_matches_reference_ranges"]["ranges"]:
+        for n in range(lo, hi + 1):
+            want = orc.lib().or_is_prime(n) and n % 2 == 1
+            assert rns_ntt.is_ntt_friendly_prime(n, 1) == bool(want), n
+
+
+def test_psi_matches_oracle_random_primes():
+    rng = np.random.default_rng(5)
+    for logn in (1, 3, 8, 12, 16, 17):
+        n = 1 << logn
+        for bits in (20, 31, 40, 62):
+            if bits <= logn + 8:
+                continue
+            for q in rns_ntt.generate_primes(bits, 2, n):
+                assert rns_ntt.find_psi(q, n) == orc.lib().or_find_primitive_root(q, 2 * n)
+
+
+def test_ctx_validation_errors_without_gpu(kats):
+    """RnsBasis::new error order (basis.rs:97-106) -- checked before any HIP call."""
+    lib = rns_ntt.load()
+    h = ctypes.c_void_p()
+    arr = np.zeros(1, dtype=np.uint64)
+    assert lib.rnt_ctx_create(3, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), 0, 0, ctypes.byref(h)) == 2
+    with pytest.raises(rns_ntt.RnsNttError) as e:
+        rns_ntt.RnsBasis([], 8)
+    assert e.value.kind == "EmptyBasis"
+    with pytest.raises(rns_ntt.RnsNttError) as e:
+        rns_ntt.RnsBasis([kats["basis_n8"]["rejects_non_friendly_modulus"]["modulus"]], 8)
+    assert e.value.kind == "NonNttFriendlyModulus"
+    with pytest.raises(rns_ntt.RnsNttError) as e:
+        rns_ntt.RnsBasis([17], 12)
+    assert e.value.kind == "InvalidDegree"
+    with pytest.raises(rns_ntt.RnsNttError) as e:
+        rns_ntt.RnsBasis([rns_ntt.generate_primes(31, 1, 1 << 18)[0]], 1 << 18)
+    assert e.value.kind == "InvalidDegree"  # beyond this backend's 2^17 limit

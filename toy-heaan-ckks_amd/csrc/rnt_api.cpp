@@ -1,0 +1,1024 @@
+// rnt_api.cpp -- the extern "C" boundary (include/rnsntt.h) over the HIP
+// kernels.  Every entry point validates like the reference (errors.rs:4-20
+// order), turns every failure into a status code, and never lets a C++
+// exception or HIP error escape.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cinttypes>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rnsntt.h"
+#include "rnt_hostmath.hpp"
+#include "rnt_internal.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
+    return fail(RNT_ERR_OUT_OF_MEMORY, "%s: %s", where, hipGetErrorString(e));
+  return fail(RNT_ERR_DEVICE, "%s: %s", where, hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, where)                  \
+  do {                                        \
+    hipError_t e_ = (expr);                   \
+    if (e_ != hipSuccess) return hip_fail(e_, where); \
+  } while (0)
+
+inline size_t word_bytes(const rnt::Tables* t) { return t->wide ? 8 : 4; }
+
+const char* const kKernelNames[rnt::K_COUNT] = {
+    "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
+    "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export"};
+
+hipEvent_t prof_event(rnt::Prof* p) {
+  if (!p->pool.empty()) {
+    hipEvent_t e = p->pool.back();
+    p->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Bracket one launch with events when profiling is on.
+template <class F>
+hipError_t prof_launch(const rnt::Tables* t, int id, F&& f) {
+  rnt::Prof* p = t->prof;
+  if (p == nullptr || !p->on) return f();
+  std::lock_guard<std::mutex> g(p->mu);
+  hipEvent_t a = prof_event(p), b = prof_event(p);
+  if (a) (void)hipEventRecord(a, t->stream);
+  hipError_t e = f();
+  if (b) (void)hipEventRecord(b, t->stream);
+  if (a && b) p->pending.push_back({id, a, b});
+  return e;
+}
+
+#define LAUNCH(T, ID, EXPR, WHERE) \
+  HIP_TRY(prof_launch((T), (ID), [&]() { return (EXPR); }), WHERE)
+
+
+
+inline rnt::Launch launch_for(const rnt_buf* b) {
+  rnt::Launch k;
+  k.t = b->ctx->t.get();
+  k.L = b->ctx->L;
+  k.B = b->n_polys;
+  k.s = k.t->stream;
+  return k;
+}
+
+inline size_t poly_words(const rnt_buf* b) { return b->ctx->L * b->n_polys * b->ctx->t->n; }
+inline uint64_t limb_stride(const rnt_buf* b) { return (uint64_t)b->n_polys * b->ctx->t->n; }
+
+int set_device(const rnt_ctx* ctx) {
+  HIP_TRY(hipSetDevice(ctx->t->device), "hipSetDevice");
+  return RNT_OK;
+}
+
+// Grow the buffer's private workspace to at least `bytes`.
+int ensure_ws(rnt_buf* b, size_t bytes) {
+  if (b->ws_bytes >= bytes) return RNT_OK;
+  if (b->ws) {
+    // the stream may still be using the old workspace
+    HIP_TRY(hipStreamSynchronize(b->ctx->t->stream), "hipStreamSynchronize");
+    HIP_TRY(hipFree(b->ws), "hipFree");
+    b->ws = nullptr;
+    b->ws_bytes = 0;
+  }
+  HIP_TRY(hipMalloc(&b->ws, bytes), "hipMalloc(workspace)");
+  b->ws_bytes = bytes;
+  return RNT_OK;
+}
+
+int ensure_stage(rnt_buf* b, size_t bytes) {
+  if (b->stage_bytes >= bytes) return RNT_OK;
+  if (b->stage) {
+    HIP_TRY(hipStreamSynchronize(b->ctx->t->stream), "hipStreamSynchronize");
+    HIP_TRY(hipFree(b->stage), "hipFree");
+    b->stage = nullptr;
+    b->stage_bytes = 0;
+  }
+  HIP_TRY(hipMalloc(&b->stage, bytes), "hipMalloc(stage)");
+  b->stage_bytes = bytes;
+  return RNT_OK;
+}
+
+// Staging for uploads/downloads is cached per buffer, except very large
+// ones (a 256-poly batch at N=2^16, L=16 stages 2 GiB of u64).
+void trim_stage(rnt_buf* b) {
+  if (b->stage_bytes > ((size_t)256 << 20)) {
+    (void)hipFree(b->stage);
+    b->stage = nullptr;
+    b->stage_bytes = 0;
+  }
+}
+
+int check_buf(const rnt_buf* b, const char* name) {
+  if (b == nullptr || b->ctx == nullptr) return fail(RNT_ERR_BAD_ARGUMENT, "%s: null buffer", name);
+  return RNT_OK;
+}
+
+// Same basis (Arc::ptr_eq on the basis in the reference) and batch size.
+int check_same(const rnt_buf* a, const rnt_buf* b, const char* what) {
+  if (a->ctx != b->ctx)
+    return fail(RNT_ERR_BASIS_MISMATCH, "%s: operands belong to different bases", what);
+  if (a->n_polys != b->n_polys)
+    return fail(RNT_ERR_BAD_ARGUMENT, "%s: batch sizes differ (%zu vs %zu)", what, a->n_polys,
+                b->n_polys);
+  return RNT_OK;
+}
+
+// Inverse-transform src (NTT domain) into dst (same layout): dst may equal src.
+int to_coeff_into(const rnt_buf* src, void* dst) {
+  rnt::Launch k = launch_for(src);
+  const uint64_t ls = limb_stride(src);
+  if (dst != src->data)
+    HIP_TRY(hipMemcpyAsync(dst, src->data, poly_words(src) * word_bytes(k.t),
+                           hipMemcpyDeviceToDevice, k.s),
+            "hipMemcpyAsync");
+  LAUNCH(k.t, rnt::K_ROW_INV, rnt::launch_row(k, 1, dst, nullptr, ls), "row inverse");
+  LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, dst, ls, dst, ls, 0, nullptr), "column inverse");
+  return RNT_OK;
+}
+
+}  // namespace
+
+rnt::Tables::~Tables() {
+  (void)hipSetDevice(device);
+  if (stream) {
+    (void)hipStreamSynchronize(stream);
+    (void)hipStreamDestroy(stream);
+  }
+  (void)hipFree(tw_fwd);
+  (void)hipFree(tw_fwd_p);
+  (void)hipFree(tw_inv);
+  (void)hipFree(tw_inv_p);
+  (void)hipFree(lconst);
+  (void)hipFree(resc);
+  (void)hipFree(resc_p);
+  if (prof) {
+    for (auto& r : prof->pending) {
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
+    for (hipEvent_t e : prof->pool) (void)hipEventDestroy(e);
+    delete prof;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// diagnostics
+// ---------------------------------------------------------------------------
+extern "C" int rnt_abi_version(void) { return RNT_ABI_VERSION; }
+extern "C" const char* rnt_last_error(void) { return g_last_error.c_str(); }
+extern "C" const char* rnt_status_string(int s) {
+  switch (s) {
+    case RNT_OK: return "ok";
+    case RNT_ERR_INVALID_DEGREE: return "InvalidDegree";
+    case RNT_ERR_EMPTY_BASIS: return "EmptyBasis";
+    case RNT_ERR_NON_NTT_FRIENDLY: return "NonNttFriendlyModulus";
+    case RNT_ERR_INVALID_MOD_DROP: return "InvalidModDrop";
+    case RNT_ERR_CHANNEL_COUNT: return "ChannelCountMismatch";
+    case RNT_ERR_NON_REDUCED: return "NonReducedCoefficient";
+    case RNT_ERR_DOMAIN_MISMATCH: return "DomainMismatch";
+    case RNT_ERR_BASIS_MISMATCH: return "BasisMismatch";
+    case RNT_ERR_DEVICE: return "DeviceError";
+    case RNT_ERR_OUT_OF_MEMORY: return "OutOfMemory";
+    case RNT_ERR_BAD_ARGUMENT: return "BadArgument";
+    default: return "unknown";
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side number theory
+// ---------------------------------------------------------------------------
+extern "C" int rnt_is_ntt_friendly_prime(uint64_t p, uint64_t degree, int* out) {
+  if (!out) return fail(RNT_ERR_BAD_ARGUMENT, "null out");
+  if (degree == 0 || degree > UINT64_MAX / 2)
+    return fail(RNT_ERR_BAD_ARGUMENT, "is_ntt_friendly_prime: degree must be in [1, 2^63)");
+  *out = rnt::host::is_ntt_friendly(p, degree) ? 1 : 0;
+  return RNT_OK;
+}
+
+extern "C" int rnt_generate_primes(uint32_t bit_size, size_t count, uint64_t degree,
+                                   uint64_t* out) {
+  if (!out && count) return fail(RNT_ERR_BAD_ARGUMENT, "null out");
+  if (rnt::host::generate_primes(bit_size, count, degree, out) != 0)
+    return fail(RNT_ERR_BAD_ARGUMENT,
+                "Unable to find %zu NTT primes with %u-bit ceiling for degree %" PRIu64, count,
+                bit_size, degree);
+  return RNT_OK;
+}
+
+extern "C" int rnt_find_psi(uint64_t modulus, uint64_t degree, uint64_t* psi) {
+  if (!psi) return fail(RNT_ERR_BAD_ARGUMENT, "null out");
+  if (degree == 0 || (degree & (degree - 1)))
+    return fail(RNT_ERR_INVALID_DEGREE, "ring degree must be a power of two, got %" PRIu64, degree);
+  if (!rnt::host::is_ntt_friendly(modulus, degree))
+    return fail(RNT_ERR_NON_NTT_FRIENDLY, "modulus %" PRIu64 " is not NTT-friendly for degree %" PRIu64,
+                modulus, degree);
+  *psi = rnt::host::find_psi(modulus, degree);
+  return RNT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+namespace {
+
+template <class W>
+int build_tables(rnt::Tables* t) {
+  using namespace rnt::host;
+  const size_t n = t->n, L = t->L;
+  const unsigned wbits = sizeof(W) * 8;
+  std::vector<W> tw(L * n), twp(L * n), itw(L * n), itwp(L * n);
+  std::vector<rnt::LimbConst<W>> lc(L);
+  std::vector<W> resc(L * L, 0), rescp(L * L, 0);
+  std::vector<uint64_t> pw(n), ipw(n);
+  for (size_t l = 0; l < L; ++l) {
+    const uint64_t q = t->moduli[l];
+    const uint64_t psi = find_psi(q, n);
+    if (psi == 0) return fail(RNT_ERR_NON_NTT_FRIENDLY, "no primitive 2N-th root mod %" PRIu64, q);
+    t->psi.push_back(psi);
+    const uint64_t psi_inv = invmod(psi, q);
+    uint64_t a = 1, b = 1;
+    for (size_t j = 0; j < n; ++j) {
+      pw[j] = a;
+      ipw[j] = b;
+      a = mulmod(a, psi, q);
+      b = mulmod(b, psi_inv, q);
+    }
+    W* T = tw.data() + l * n;
+    W* TP = twp.data() + l * n;
+    W* I = itw.data() + l * n;
+    W* IP = itwp.data() + l * n;
+    T[0] = 1;
+    I[0] = 1;
+    TP[0] = (W)shoup_companion(1, q, wbits);
+    IP[0] = TP[0];
+    for (size_t g = 1; g < n; ++g) {
+      const uint64_t e = brv(g, t->log_n);
+      T[g] = (W)pw[e];
+      I[g] = (W)ipw[e];
+      TP[g] = (W)shoup_companion(pw[e], q, wbits);
+      IP[g] = (W)shoup_companion(ipw[e], q, wbits);
+    }
+    rnt::LimbConst<W>& c = lc[l];
+    c.q = (W)q;
+    c.qinv = (W)neg_free_qinv(q, wbits);
+    c.one_p = (W)shoup_companion(1, q, wbits);
+    const uint64_t r = (uint64_t)((((u128)1) << wbits) % q);  // 2^w mod q
+    c.rmod = (W)r;
+    c.rmod_p = (W)shoup_companion(r, q, wbits);
+    const uint64_t ninv = invmod(n % q, q);
+    const uint64_t w1 = n > 1 ? (uint64_t)I[1] : 1;
+    c.c1 = (W)ninv;
+    c.c1_p = (W)shoup_companion(ninv, q, wbits);
+    c.c2 = (W)mulmod(w1, ninv, q);
+    c.c2_p = (W)shoup_companion(c.c2, q, wbits);
+    const uint64_t ninvr = mulmod(ninv, r, q);
+    c.c1r = (W)ninvr;
+    c.c1r_p = (W)shoup_companion(ninvr, q, wbits);
+    c.c2r = (W)mulmod(w1, ninvr, q);
+    c.c2r_p = (W)shoup_companion(c.c2r, q, wbits);
+    for (size_t i = 0; i < l; ++i) {
+      const uint64_t qi = t->moduli[i];
+      const uint64_t inv = invmod(q % qi, qi);
+      if (inv == 0)
+        return fail(RNT_ERR_BAD_ARGUMENT, "moduli %" PRIu64 " and %" PRIu64 " are not coprime", q, qi);
+      resc[l * L + i] = (W)inv;
+      rescp[l * L + i] = (W)shoup_companion(inv, qi, wbits);
+    }
+  }
+  const size_t tb = L * n * sizeof(W);
+  HIP_TRY(hipMalloc(&t->tw_fwd, tb), "hipMalloc(tables)");
+  HIP_TRY(hipMalloc(&t->tw_fwd_p, tb), "hipMalloc(tables)");
+  HIP_TRY(hipMalloc(&t->tw_inv, tb), "hipMalloc(tables)");
+  HIP_TRY(hipMalloc(&t->tw_inv_p, tb), "hipMalloc(tables)");
+  HIP_TRY(hipMalloc(&t->lconst, L * sizeof(rnt::LimbConst<W>)), "hipMalloc(tables)");
+  HIP_TRY(hipMalloc(&t->resc, L * L * sizeof(W)), "hipMalloc(tables)");
+  HIP_TRY(hipMalloc(&t->resc_p, L * L * sizeof(W)), "hipMalloc(tables)");
+  HIP_TRY(hipMemcpy(t->tw_fwd, tw.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
+  HIP_TRY(hipMemcpy(t->tw_fwd_p, twp.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
+  HIP_TRY(hipMemcpy(t->tw_inv, itw.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
+  HIP_TRY(hipMemcpy(t->tw_inv_p, itwp.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
+  HIP_TRY(hipMemcpy(t->lconst, lc.data(), L * sizeof(rnt::LimbConst<W>), hipMemcpyHostToDevice),
+          "hipMemcpy");
+  HIP_TRY(hipMemcpy(t->resc, resc.data(), L * L * sizeof(W), hipMemcpyHostToDevice), "hipMemcpy");
+  HIP_TRY(hipMemcpy(t->resc_p, rescp.data(), L * L * sizeof(W), hipMemcpyHostToDevice),
+          "hipMemcpy");
+  return RNT_OK;
+}
+
+}  // namespace
+
+extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t count, int device,
+                              rnt_ctx** out) {
+  if (!out) return fail(RNT_ERR_BAD_ARGUMENT, "null out");
+  *out = nullptr;
+  // RnsBasis::new order (basis.rs:97-106): empty basis first, then each
+  // NttTable::new (degree check, NTT-friendliness).
+  if (count == 0) return fail(RNT_ERR_EMPTY_BASIS, "RNS basis must contain at least one modulus");
+  if (!moduli) return fail(RNT_ERR_BAD_ARGUMENT, "null moduli");
+  if (log_n > (uint32_t)rnt::kMaxLogN)
+    return fail(RNT_ERR_INVALID_DEGREE, "ring degree 2^%u exceeds this backend's maximum 2^%d",
+                log_n, rnt::kMaxLogN);
+  const uint64_t n = 1ull << log_n;
+  bool wide = false;
+  for (size_t i = 0; i < count; ++i) {
+    if (!rnt::host::is_ntt_friendly(moduli[i], n))
+      return fail(RNT_ERR_NON_NTT_FRIENDLY,
+                  "modulus %" PRIu64 " is not NTT-friendly for degree %" PRIu64, moduli[i], n);
+    if (moduli[i] >= (1ull << 63))
+      return fail(RNT_ERR_BAD_ARGUMENT,
+                  "modulus %" PRIu64 " >= 2^63 (the reference's add_mod overflows)", moduli[i]);
+    if (moduli[i] >= (1ull << 31)) wide = true;
+  }
+  try {
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    if (device < 0 || device >= ndev)
+      return fail(RNT_ERR_BAD_ARGUMENT, "device %d out of range (%d devices)", device, ndev);
+    HIP_TRY(hipSetDevice(device), "hipSetDevice");
+    auto t = std::make_shared<rnt::Tables>();
+    t->device = device;
+    t->wide = wide ? 1 : 0;
+    t->log_n = log_n;
+    t->n = (size_t)n;
+    t->L = count;
+    t->moduli.assign(moduli, moduli + count);
+    int rc = wide ? build_tables<uint64_t>(t.get()) : build_tables<uint32_t>(t.get());
+    if (rc != RNT_OK) return rc;
+    HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking), "hipStreamCreate");
+    rnt_ctx* c = new rnt_ctx;
+    c->t = std::move(t);
+    c->L = count;
+    *out = c;
+    return RNT_OK;
+  } catch (const std::bad_alloc&) {
+    return fail(RNT_ERR_OUT_OF_MEMORY, "host allocation failed");
+  } catch (...) {
+    return fail(RNT_ERR_DEVICE, "unexpected exception in rnt_ctx_create");
+  }
+}
+
+extern "C" int rnt_ctx_destroy(rnt_ctx* ctx) {
+  delete ctx;  // the tables live on while any view or buffer context holds them
+  return RNT_OK;
+}
+
+extern "C" int rnt_ctx_drop_last(const rnt_ctx* ctx, size_t drop_count, rnt_ctx** out) {
+  if (!ctx || !out) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  *out = nullptr;
+  if (drop_count >= ctx->L)
+    return fail(RNT_ERR_INVALID_MOD_DROP, "invalid mod-drop count %zu for %zu channels",
+                drop_count, ctx->L);
+  try {
+    rnt_ctx* c = new rnt_ctx;
+    c->t = ctx->t;
+    c->L = ctx->L - drop_count;
+    *out = c;
+  } catch (...) {
+    return fail(RNT_ERR_OUT_OF_MEMORY, "host allocation failed");
+  }
+  return RNT_OK;
+}
+
+extern "C" int rnt_ctx_degree(const rnt_ctx* ctx, size_t* n) {
+  if (!ctx || !n) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  *n = ctx->t->n;
+  return RNT_OK;
+}
+extern "C" int rnt_ctx_channel_count(const rnt_ctx* ctx, size_t* count) {
+  if (!ctx || !count) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  *count = ctx->L;
+  return RNT_OK;
+}
+extern "C" int rnt_ctx_moduli(const rnt_ctx* ctx, uint64_t* out) {
+  if (!ctx || !out) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  std::copy(ctx->t->moduli.begin(), ctx->t->moduli.begin() + ctx->L, out);
+  return RNT_OK;
+}
+extern "C" int rnt_ctx_total_bits(const rnt_ctx* ctx, uint32_t* bits) {
+  if (!ctx || !bits) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  uint32_t s = 0;
+  for (size_t i = 0; i < ctx->L; ++i) s += 63u - (uint32_t)__builtin_clzll(ctx->t->moduli[i]);
+  *bits = s;
+  return RNT_OK;
+}
+extern "C" int rnt_ctx_psi(const rnt_ctx* ctx, size_t limb, uint64_t* psi) {
+  if (!ctx || !psi) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  if (limb >= ctx->L) return fail(RNT_ERR_BAD_ARGUMENT, "limb %zu out of range", limb);
+  *psi = ctx->t->psi[limb];
+  return RNT_OK;
+}
+extern "C" int rnt_ctx_stream(const rnt_ctx* ctx, void** stream) {
+  if (!ctx || !stream) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  *stream = (void*)ctx->t->stream;
+  return RNT_OK;
+}
+extern "C" int rnt_sync(const rnt_ctx* ctx) {
+  if (!ctx) return fail(RNT_ERR_BAD_ARGUMENT, "null ctx");
+  if (int rc = set_device(ctx)) return rc;
+  HIP_TRY(hipStreamSynchronize(ctx->t->stream), "hipStreamSynchronize");
+  return RNT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// buffers
+// ---------------------------------------------------------------------------
+extern "C" int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out) {
+  if (!ctx || !out) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  *out = nullptr;
+  if (n_polys == 0) return fail(RNT_ERR_BAD_ARGUMENT, "n_polys must be positive");
+  if (int rc = set_device(ctx)) return rc;
+  rnt_buf* b = nullptr;
+  try {
+    b = new rnt_buf;
+  } catch (...) {
+    return fail(RNT_ERR_OUT_OF_MEMORY, "host allocation failed");
+  }
+  b->ctx = ctx;
+  b->n_polys = n_polys;
+  const size_t bytes = poly_words(b) * word_bytes(ctx->t.get());
+  hipError_t e = hipMalloc(&b->data, bytes);
+  if (e != hipSuccess) {
+    delete b;
+    return hip_fail(e, "hipMalloc(buffer)");
+  }
+  e = hipMemsetAsync(b->data, 0, bytes, ctx->t->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->t->stream);
+  if (e != hipSuccess) {
+    (void)hipFree(b->data);
+    delete b;
+    return hip_fail(e, "hipMemset(buffer)");
+  }
+  *out = b;
+  return RNT_OK;
+}
+
+extern "C" int rnt_buf_free(rnt_buf* b) {
+  if (!b) return RNT_OK;
+  if (b->ctx) {
+    (void)hipSetDevice(b->ctx->t->device);
+    (void)hipStreamSynchronize(b->ctx->t->stream);
+  }
+  (void)hipFree(b->data);
+  (void)hipFree(b->ws);
+  (void)hipFree(b->stage);
+  delete b;
+  return RNT_OK;
+}
+
+extern "C" int rnt_buf_n_polys(const rnt_buf* b, size_t* n) {
+  if (!b || !n) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  *n = b->n_polys;
+  return RNT_OK;
+}
+extern "C" int rnt_buf_is_ntt(const rnt_buf* b, int* in_ntt) {
+  if (!b || !in_ntt) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  *in_ntt = b->in_ntt;
+  return RNT_OK;
+}
+
+extern "C" int rnt_upload(rnt_buf* b, const uint64_t* host, size_t n_polys, size_t channels,
+                          int in_ntt) {
+  if (int rc = check_buf(b, "rnt_upload")) return rc;
+  if (!host) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_upload: null host pointer");
+  // from_channels order (poly.rs:78-93): channel count, then reducedness.
+  if (channels != b->ctx->L)
+    return fail(RNT_ERR_CHANNEL_COUNT, "channel count mismatch: expected %zu, got %zu", b->ctx->L,
+                channels);
+  if (n_polys != b->n_polys)
+    return fail(RNT_ERR_BAD_ARGUMENT, "rnt_upload: buffer holds %zu polys, got %zu", b->n_polys,
+                n_polys);
+  if (int rc = set_device(b->ctx)) return rc;
+  rnt::Launch k = launch_for(b);
+  const size_t words = poly_words(b);
+  if (int rc = ensure_stage(b, words * 8 + 64)) return rc;
+  unsigned long long* err = (unsigned long long*)((char*)b->stage + words * 8);
+  HIP_TRY(hipMemcpyAsync(b->stage, host, words * 8, hipMemcpyHostToDevice, k.s), "hipMemcpy H2D");
+  HIP_TRY(hipMemsetAsync(err, 0xff, 8, k.s), "hipMemset");
+  LAUNCH(k.t, rnt::K_IMPORT, rnt::launch_import(k, b->data, (const uint64_t*)b->stage, in_ntt ? 1 : 0, err), "import");
+  unsigned long long bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, err, 8, hipMemcpyDeviceToHost, k.s), "hipMemcpy D2H");
+  HIP_TRY(hipStreamSynchronize(k.s), "hipStreamSynchronize");
+  if (bad != ~0ull) {
+    const size_t n = b->ctx->t->n;
+    const size_t ch = (size_t)((bad / n) % b->ctx->L);
+    // device data is now partially written; the reference returns Err and
+    // builds no polynomial, so zero the buffer to keep it well-defined.
+    (void)hipMemsetAsync(b->data, 0, words * word_bytes(k.t), k.s);
+    (void)hipStreamSynchronize(k.s);
+    b->in_ntt = 0;
+    return fail(RNT_ERR_NON_REDUCED, "coefficient %" PRIu64 " is not reduced modulo %" PRIu64,
+                host[bad], b->ctx->t->moduli[ch]);
+  }
+  b->in_ntt = in_ntt ? 1 : 0;
+  trim_stage(b);
+  return RNT_OK;
+}
+
+extern "C" int rnt_upload_coeffs(rnt_buf* b, const int64_t* coeffs, size_t n_polys) {
+  if (int rc = check_buf(b, "rnt_upload_coeffs")) return rc;
+  if (!coeffs) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_upload_coeffs: null pointer");
+  if (n_polys != b->n_polys)
+    return fail(RNT_ERR_BAD_ARGUMENT, "rnt_upload_coeffs: buffer holds %zu polys, got %zu",
+                b->n_polys, n_polys);
+  if (int rc = set_device(b->ctx)) return rc;
+  rnt::Launch k = launch_for(b);
+  const size_t words = n_polys * b->ctx->t->n;
+  if (int rc = ensure_stage(b, words * 8)) return rc;
+  HIP_TRY(hipMemcpyAsync(b->stage, coeffs, words * 8, hipMemcpyHostToDevice, k.s), "hipMemcpy H2D");
+  LAUNCH(k.t, rnt::K_IMPORT, rnt::launch_import_coeffs(k, b->data, (const int64_t*)b->stage), "import_coeffs");
+  HIP_TRY(hipStreamSynchronize(k.s), "hipStreamSynchronize");
+  b->in_ntt = 0;
+  trim_stage(b);
+  return RNT_OK;
+}
+
+extern "C" int rnt_download(const rnt_buf* cb, uint64_t* host, size_t n_polys) {
+  rnt_buf* b = const_cast<rnt_buf*>(cb);  // staging only; contents unchanged
+  if (int rc = check_buf(b, "rnt_download")) return rc;
+  if (!host) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_download: null host pointer");
+  if (n_polys != b->n_polys)
+    return fail(RNT_ERR_BAD_ARGUMENT, "rnt_download: buffer holds %zu polys, got %zu", b->n_polys,
+                n_polys);
+  if (int rc = set_device(b->ctx)) return rc;
+  rnt::Launch k = launch_for(b);
+  const size_t words = poly_words(b);
+  if (int rc = ensure_stage(b, words * 8)) return rc;
+  LAUNCH(k.t, rnt::K_EXPORT, rnt::launch_export(k, (uint64_t*)b->stage, b->data, b->in_ntt), "export");
+  HIP_TRY(hipMemcpyAsync(host, b->stage, words * 8, hipMemcpyDeviceToHost, k.s), "hipMemcpy D2H");
+  HIP_TRY(hipStreamSynchronize(k.s), "hipStreamSynchronize");
+  trim_stage(b);
+  return RNT_OK;
+}
+
+extern "C" int rnt_copy(rnt_buf* dst, const rnt_buf* src) {
+  if (int rc = check_buf(dst, "rnt_copy")) return rc;
+  if (int rc = check_buf(src, "rnt_copy")) return rc;
+  if (int rc = check_same(dst, src, "rnt_copy")) return rc;
+  if (dst == src) return RNT_OK;
+  if (int rc = set_device(dst->ctx)) return rc;
+  rnt::Launch k = launch_for(dst);
+  HIP_TRY(hipMemcpyAsync(dst->data, src->data, poly_words(src) * word_bytes(k.t),
+                         hipMemcpyDeviceToDevice, k.s),
+          "hipMemcpyAsync");
+  dst->in_ntt = src->in_ntt;
+  return RNT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// ring ops
+// ---------------------------------------------------------------------------
+extern "C" int rnt_ntt_fwd(rnt_buf* b) {
+  if (int rc = check_buf(b, "rnt_ntt_fwd")) return rc;
+  if (b->in_ntt) return RNT_OK;  // poly.rs:137-139
+  if (int rc = set_device(b->ctx)) return rc;
+  rnt::Launch k = launch_for(b);
+  const uint64_t ls = limb_stride(b);
+  LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, b->data, b->data, nullptr, nullptr, ls, ls), "column forward");
+  LAUNCH(k.t, rnt::K_ROW_FWD, rnt::launch_row(k, 0, b->data, nullptr, ls), "row forward");
+  b->in_ntt = 1;
+  return RNT_OK;
+}
+
+extern "C" int rnt_ntt_inv(rnt_buf* b) {
+  if (int rc = check_buf(b, "rnt_ntt_inv")) return rc;
+  if (!b->in_ntt) return RNT_OK;  // poly.rs:155-157
+  if (int rc = set_device(b->ctx)) return rc;
+  if (int rc = to_coeff_into(b, b->data)) return rc;
+  b->in_ntt = 0;
+  return RNT_OK;
+}
+
+extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
+  if (int rc = check_buf(out, "rnt_mul")) return rc;
+  if (int rc = check_buf(a, "rnt_mul")) return rc;
+  if (int rc = check_buf(b, "rnt_mul")) return rc;
+  if (int rc = check_same(a, b, "rnt_mul")) return rc;
+  if (int rc = check_same(out, a, "rnt_mul")) return rc;
+  if (a->in_ntt != b->in_ntt)
+    return fail(RNT_ERR_DOMAIN_MISMATCH, "mul_assign: domain mismatch (both must be in the same domain)");
+  if (int rc = set_device(out->ctx)) return rc;
+  rnt::Launch k = launch_for(out);
+  if (a->in_ntt) {  // poly.rs:297-306
+    LAUNCH(k.t, rnt::K_ELEMENTWISE, rnt::launch_elementwise(k, 3, out->data, a->data, b->data), "pointwise mul");
+    out->in_ntt = 1;
+    return RNT_OK;
+  }
+  // poly.rs:307-329: fwd(a), fwd(b), pointwise, inv -- three fused launches
+  const uint64_t ls = limb_stride(out);
+  const size_t wb = word_bytes(k.t);
+  if (int rc = ensure_ws(out, poly_words(out) * wb)) return rc;
+  LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, out->data, a->data, out->ws, b->data, ls, ls), "column forward");
+  LAUNCH(k.t, rnt::K_ROW_MUL, rnt::launch_row(k, 2, out->data, out->ws, ls), "row mul");
+  LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, out->data, ls, out->data, ls, 1, nullptr), "column inverse");
+  out->in_ntt = 0;
+  return RNT_OK;
+}
+
+static int binary_elementwise(rnt_buf* out, const rnt_buf* a, const rnt_buf* b, int op,
+                              const char* name) {
+  if (int rc = check_buf(out, name)) return rc;
+  if (int rc = check_buf(a, name)) return rc;
+  if (int rc = check_buf(b, name)) return rc;
+  if (int rc = check_same(a, b, name)) return rc;
+  if (int rc = check_same(out, a, name)) return rc;
+  if (a->in_ntt != b->in_ntt) return fail(RNT_ERR_DOMAIN_MISMATCH, "%s: domain mismatch", name);
+  if (int rc = set_device(out->ctx)) return rc;
+  rnt::Launch k = launch_for(out);
+  LAUNCH(k.t, rnt::K_ELEMENTWISE, rnt::launch_elementwise(k, op, out->data, a->data, b->data), name);
+  out->in_ntt = a->in_ntt;
+  return RNT_OK;
+}
+
+extern "C" int rnt_add(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
+  return binary_elementwise(out, a, b, 0, "add_assign");
+}
+extern "C" int rnt_sub(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
+  return binary_elementwise(out, a, b, 1, "sub");
+}
+extern "C" int rnt_neg(rnt_buf* out, const rnt_buf* a) {
+  if (int rc = check_buf(out, "rnt_neg")) return rc;
+  if (int rc = check_buf(a, "rnt_neg")) return rc;
+  if (int rc = check_same(out, a, "rnt_neg")) return rc;
+  if (int rc = set_device(out->ctx)) return rc;
+  rnt::Launch k = launch_for(out);
+  LAUNCH(k.t, rnt::K_ELEMENTWISE, rnt::launch_elementwise(k, 2, out->data, a->data, nullptr), "neg");
+  out->in_ntt = a->in_ntt;
+  return RNT_OK;
+}
+
+extern "C" int rnt_rescale(rnt_buf* out, const rnt_buf* in) {
+  if (int rc = check_buf(out, "rnt_rescale")) return rc;
+  if (int rc = check_buf(in, "rnt_rescale")) return rc;
+  const size_t L = in->ctx->L;
+  if (L < 2)  // poly.rs:191-197
+    return fail(RNT_ERR_INVALID_MOD_DROP, "invalid mod-drop count 1 for %zu channels", L);
+  if (out->ctx->t != in->ctx->t || out->ctx->L != L - 1)
+    return fail(RNT_ERR_BASIS_MISMATCH, "rescale: output basis is not drop_last(1) of the input's");
+  if (out->n_polys != in->n_polys)
+    return fail(RNT_ERR_BAD_ARGUMENT, "rescale: batch sizes differ");
+  if (int rc = set_device(in->ctx)) return rc;
+  rnt::Launch k = launch_for(in);
+  const void* src = in->data;
+  if (in->in_ntt) {  // poly.rs:199-210: clone + to_coeff_domain
+    if (int rc = ensure_ws(out, poly_words(in) * word_bytes(k.t))) return rc;
+    if (int rc = to_coeff_into(in, out->ws)) return rc;
+    src = out->ws;
+  }
+  LAUNCH(k.t, rnt::K_RESCALE, rnt::launch_rescale(k, out->data, src), "rescale");
+  out->in_ntt = 0;
+  return RNT_OK;
+}
+
+extern "C" int rnt_mod_drop_last(rnt_buf* out, const rnt_buf* in) {
+  if (int rc = check_buf(out, "rnt_mod_drop_last")) return rc;
+  if (int rc = check_buf(in, "rnt_mod_drop_last")) return rc;
+  if (out->ctx->t != in->ctx->t || out->ctx->L > in->ctx->L)
+    return fail(RNT_ERR_BASIS_MISMATCH, "mod_drop_last: output basis is not a prefix of the input's");
+  if (out->n_polys != in->n_polys)
+    return fail(RNT_ERR_BAD_ARGUMENT, "mod_drop_last: batch sizes differ");
+  if (int rc = set_device(in->ctx)) return rc;
+  rnt::Launch k = launch_for(out);
+  // [L][B][N]: the kept channels are a contiguous prefix
+  if (out != in)
+    HIP_TRY(hipMemcpyAsync(out->data, in->data, poly_words(out) * word_bytes(k.t),
+                           hipMemcpyDeviceToDevice, k.s),
+            "hipMemcpyAsync");
+  out->in_ntt = in->in_ntt;
+  return RNT_OK;
+}
+
+extern "C" int rnt_automorphism(rnt_buf* out, const rnt_buf* in, uint64_t g) {
+  if (int rc = check_buf(out, "rnt_automorphism")) return rc;
+  if (int rc = check_buf(in, "rnt_automorphism")) return rc;
+  if (int rc = check_same(out, in, "rnt_automorphism")) return rc;
+  if (int rc = set_device(in->ctx)) return rc;
+  rnt::Launch k = launch_for(in);
+  const uint64_t two_n = 2 * (uint64_t)k.t->n;
+  if (g % two_n == 0) return rnt_copy(out, in);  // poly.rs:508-511: self.clone()
+  const void* src = in->data;
+  if (in->in_ntt || out == in) {
+    if (int rc = ensure_ws(out, poly_words(in) * word_bytes(k.t))) return rc;
+    if (in->in_ntt) {
+      if (int rc = to_coeff_into(in, out->ws)) return rc;
+    } else {
+      HIP_TRY(hipMemcpyAsync(out->ws, in->data, poly_words(in) * word_bytes(k.t),
+                             hipMemcpyDeviceToDevice, k.s),
+              "hipMemcpyAsync");
+    }
+    src = out->ws;
+  }
+  LAUNCH(k.t, rnt::K_AUTOMORPHISM, rnt::launch_automorphism(k, out->data, src, g), "automorphism");
+  out->in_ntt = 0;
+  return RNT_OK;
+}
+
+static uint64_t rotation_exponent(int32_t k, uint64_t two_n) {
+  // poly.rs:546-569: 5^|k| mod 2N, and for k < 0 the composition with
+  // X -> X^(2N-1): both are odd, so the two automorphisms compose exactly
+  // into one with exponent 5^|k| * (2N-1) mod 2N.
+  const uint64_t r = k >= 0 ? (uint64_t)k : (uint64_t)(-(int64_t)k);
+  uint64_t e = rnt::host::powmod(5, r, two_n);
+  if (k < 0) e = rnt::host::mulmod(e, two_n - 1, two_n);
+  return e;
+}
+
+extern "C" int rnt_rotate_slots(rnt_buf* out, const rnt_buf* in, int32_t k) {
+  if (int rc = check_buf(in, "rnt_rotate_slots")) return rc;
+  return rnt_automorphism(out, in, rotation_exponent(k, 2 * (uint64_t)in->ctx->t->n));
+}
+
+// ---------------------------------------------------------------------------
+// key-switching
+// ---------------------------------------------------------------------------
+extern "C" int rnt_key_prepare(rnt_buf* key_a, rnt_buf* key_b) {
+  if (int rc = check_buf(key_a, "rnt_key_prepare")) return rc;
+  if (int rc = check_buf(key_b, "rnt_key_prepare")) return rc;
+  if (int rc = check_same(key_a, key_b, "rnt_key_prepare")) return rc;
+  if (key_a->n_polys != key_a->ctx->L)
+    return fail(RNT_ERR_CHANNEL_COUNT, "gadget key must hold one poly per channel: expected %zu, got %zu",
+                key_a->ctx->L, key_a->n_polys);
+  if (int rc = rnt_ntt_fwd(key_a)) return rc;
+  return rnt_ntt_fwd(key_b);
+}
+
+namespace {
+
+int check_key(const rnt_buf* d, const rnt_buf* key_a, const rnt_buf* key_b) {
+  if (int rc = check_buf(key_a, "key")) return rc;
+  if (int rc = check_buf(key_b, "key")) return rc;
+  if (key_a->ctx != d->ctx || key_b->ctx != d->ctx)
+    return fail(RNT_ERR_BASIS_MISMATCH, "key-switch: key and ciphertext belong to different bases");
+  if (key_a->n_polys != d->ctx->L || key_b->n_polys != d->ctx->L)
+    return fail(RNT_ERR_CHANNEL_COUNT, "gadget key must hold one poly per channel (%zu)", d->ctx->L);
+  if (!key_a->in_ntt || !key_b->in_ntt)
+    return fail(RNT_ERR_DOMAIN_MISMATCH, "key-switch: keys must be prepared (rnt_key_prepare)");
+  return RNT_OK;
+}
+
+// polys per key-switch chunk so that S ([L][L][Bc][N]) stays <= ~1 GiB
+size_t ks_chunk(const rnt::Tables* t, size_t L, size_t B) {
+  const size_t per = L * L * t->n * (t->wide ? 8 : 4);
+  size_t c = (size_t)1 << 30;
+  c = per ? c / per : B;
+  if (c < 1) c = 1;
+  return std::min(c, B);
+}
+
+// Gadget sum for polys [p0, p0+bc) of d into out0/out1 (full-batch layout):
+// out0 = INV(sum_i NTT(alpha_i) key_b[i] + init0) (+ add0), etc.
+// ws layout: S | U0 | U1.
+int ks_chunk_run(rnt::Launch k, void* ws, const rnt_buf* d, size_t p0, size_t bc,
+                 const rnt_buf* key_a, const rnt_buf* key_b, void* out0, void* out1,
+                 uint64_t out_ls, const void* init0, const void* init1, uint64_t init_ls,
+                 const void* add0, int with_init) {
+  const size_t n = k.t->n, L = k.L, wb = k.t->wide ? 8 : 4;
+  k.B = bc;
+  char* S = (char*)ws;
+  char* U0 = S + L * L * bc * n * wb;
+  char* U1 = U0 + L * bc * n * wb;
+  const uint64_t cls = (uint64_t)bc * n;  // chunk-local limb stride
+  const uint64_t d_ls = limb_stride(d);
+  LAUNCH(k.t, rnt::K_KS_DECOMPOSE, rnt::launch_ks_decompose(k, S, (const char*)d->data + p0 * n * wb, d_ls), "ks decompose");
+  const char* i0 = with_init && init0 ? (const char*)init0 + p0 * n * wb : nullptr;
+  const char* i1 = with_init && init1 ? (const char*)init1 + p0 * n * wb : nullptr;
+  LAUNCH(k.t, rnt::K_KS_ROWS, rnt::launch_ks_rows(k, U0, U1, cls, S, key_a->data, key_b->data, limb_stride(key_a), i0,
+                              i1, init_ls), "ks rows");
+  const char* a0 = add0 ? (const char*)add0 + p0 * n * wb : nullptr;
+  LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, (char*)out0 + p0 * n * wb, out_ls, U0, cls, 1, a0), "ks inverse");
+  LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, (char*)out1 + p0 * n * wb, out_ls, U1, cls, 1, nullptr), "ks inverse");
+  return RNT_OK;
+}
+
+}  // namespace
+
+extern "C" int rnt_keyswitch(rnt_buf* acc0, rnt_buf* acc1, const rnt_buf* d, const rnt_buf* key_a,
+                             const rnt_buf* key_b) {
+  if (int rc = check_buf(acc0, "rnt_keyswitch")) return rc;
+  if (int rc = check_buf(acc1, "rnt_keyswitch")) return rc;
+  if (int rc = check_buf(d, "rnt_keyswitch")) return rc;
+  if (int rc = check_same(acc0, d, "rnt_keyswitch")) return rc;
+  if (int rc = check_same(acc1, d, "rnt_keyswitch")) return rc;
+  if (int rc = check_key(d, key_a, key_b)) return rc;
+  if (d->in_ntt) return fail(RNT_ERR_DOMAIN_MISMATCH, "key-switch input must be in coefficient domain");
+  if (acc0 == acc1 || acc0 == d || acc1 == d)
+    return fail(RNT_ERR_BAD_ARGUMENT, "rnt_keyswitch: outputs must not alias each other or d");
+  if (int rc = set_device(d->ctx)) return rc;
+  rnt::Launch k = launch_for(d);
+  const size_t L = k.L, n = k.t->n, wb = word_bytes(k.t);
+  const size_t bc = ks_chunk(k.t, L, d->n_polys);
+  if (int rc = ensure_ws(acc0, (L * L + 2 * L) * bc * n * wb)) return rc;
+  for (size_t p0 = 0; p0 < d->n_polys; p0 += bc) {
+    const size_t c = std::min(bc, d->n_polys - p0);
+    if (int rc = ks_chunk_run(k, acc0->ws, d, p0, c, key_a, key_b, acc0->data, acc1->data,
+                              limb_stride(d), nullptr, nullptr, 0, nullptr, 0))
+      return rc;
+  }
+  acc0->in_ntt = acc1->in_ntt = 0;
+  return RNT_OK;
+}
+
+extern "C" int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
+                                const rnt_buf* c1, const rnt_buf* c0p, const rnt_buf* c1p,
+                                const rnt_buf* key_a, const rnt_buf* key_b) {
+  const rnt_buf* all[6] = {out0, out1, c0, c1, c0p, c1p};
+  for (const rnt_buf* b : all)
+    if (int rc = check_buf(b, "rnt_ct_mul_relin")) return rc;
+  for (int i = 1; i < 6; ++i)
+    if (int rc = check_same(all[0], all[i], "rnt_ct_mul_relin")) return rc;
+  if (int rc = check_key(c0, key_a, key_b)) return rc;
+  if (c0->in_ntt || c1->in_ntt || c0p->in_ntt || c1p->in_ntt)
+    return fail(RNT_ERR_DOMAIN_MISMATCH, "mul_ciphertexts_gadget: inputs must be in coefficient domain");
+  if (out0 == out1) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_ct_mul_relin: out0 aliases out1");
+  if (int rc = set_device(c0->ctx)) return rc;
+  rnt::Launch k = launch_for(c0);
+  const size_t L = k.L, n = k.t->n, wb = word_bytes(k.t), B = c0->n_polys;
+  const size_t bc = ks_chunk(k.t, L, B);
+  // ws: T0..T3 (column outputs, chunk-local) | D0 | D1 | D2 | key-switch (S|U0|U1)
+  const size_t chunk_words = L * bc * n;
+  const size_t need = (7 * chunk_words + (L * L + 2 * L) * bc * n) * wb;
+  if (int rc = ensure_ws(out0, need)) return rc;
+  char* ws = (char*)out0->ws;
+  char* T[4];
+  for (int i = 0; i < 4; ++i) T[i] = ws + i * chunk_words * wb;
+  char* D0 = ws + 4 * chunk_words * wb;
+  char* D1 = D0 + chunk_words * wb;
+  char* D2 = D1 + chunk_words * wb;
+  char* KS = D2 + chunk_words * wb;
+  const uint64_t full_ls = limb_stride(c0);
+  for (size_t p0 = 0; p0 < B; p0 += bc) {
+    const size_t c = std::min(bc, B - p0);
+    rnt::Launch kc = k;
+    kc.B = c;
+    const uint64_t cls = (uint64_t)c * n;
+    auto off = [&](const rnt_buf* b) { return (const char*)b->data + p0 * n * wb; };
+    LAUNCH(kc.t, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, T[0], off(c0), T[1], off(c1), full_ls, cls), "tensor column");
+    LAUNCH(kc.t, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, T[2], off(c0p), T[3], off(c1p), full_ls, cls), "tensor column");
+    LAUNCH(kc.t, rnt::K_TENSOR_ROWS, rnt::launch_tensor_rows(kc, D0, D1, D2, T[0], T[1], T[2], T[3], cls), "tensor rows");
+    // d2 -> coefficient domain (engine.rs:493), in place in D2
+    LAUNCH(kc.t, rnt::K_COL_INV, rnt::launch_col_inv(kc, D2, cls, D2, cls, 1, nullptr), "d2 inverse");
+    // gadget sum with d0hat / d1hat as accumulator seeds (engine.rs:530-531)
+    // d2 lives in a chunk-local buffer: present it as a full "buffer".
+    rnt_buf d2view;
+    d2view.ctx = c0->ctx;
+    d2view.n_polys = c;
+    d2view.data = D2;
+    if (int rc = ks_chunk_run(k, KS, &d2view, 0, c, key_a, key_b, (char*)out0->data + p0 * n * wb,
+                              (char*)out1->data + p0 * n * wb, full_ls, D0, D1, cls, nullptr, 1))
+      return rc;
+    d2view.data = nullptr;  // not owned
+  }
+  out0->in_ntt = out1->in_ntt = 0;
+  return RNT_OK;
+}
+
+extern "C" int rnt_ct_rotate(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, const rnt_buf* c1,
+                             int32_t kk, const rnt_buf* key_a, const rnt_buf* key_b) {
+  const rnt_buf* all[4] = {out0, out1, c0, c1};
+  for (const rnt_buf* b : all)
+    if (int rc = check_buf(b, "rnt_ct_rotate")) return rc;
+  for (int i = 1; i < 4; ++i)
+    if (int rc = check_same(all[0], all[i], "rnt_ct_rotate")) return rc;
+  if (int rc = check_key(c0, key_a, key_b)) return rc;
+  if (out0 == out1) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_ct_rotate: out0 aliases out1");
+  if (int rc = set_device(c0->ctx)) return rc;
+  rnt::Launch k = launch_for(c0);
+  const size_t L = k.L, n = k.t->n, wb = word_bytes(k.t), B = c0->n_polys;
+  const size_t words = L * B * n;
+  const uint64_t g = rotation_exponent(kk, 2 * (uint64_t)n);
+  // ws: SIG0 | SIG1 | [TMP when an input is NTT-domain] | key-switch chunk space
+  const size_t bc = ks_chunk(k.t, L, B);
+  const bool any_ntt = c0->in_ntt || c1->in_ntt;
+  const size_t tmp_words = any_ntt ? words : 0;
+  if (int rc = ensure_ws(out0, (2 * words + tmp_words + (L * L + 2 * L) * bc * n) * wb)) return rc;
+  char* sig0 = (char*)out0->ws;
+  char* sig1 = sig0 + words * wb;
+  char* tmp = sig1 + words * wb;
+  char* KS = tmp + tmp_words * wb;
+  // sigma(c0), sigma(c1) in coefficient domain (engine.rs:417-419; poly.rs:494-504
+  // converts an NTT-domain input first)
+  for (int i = 0; i < 2; ++i) {
+    const rnt_buf* src = i ? c1 : c0;
+    char* dst = i ? sig1 : sig0;
+    const void* s = src->data;
+    if (src->in_ntt) {
+      if (int rc = to_coeff_into(src, tmp)) return rc;
+      s = tmp;
+    }
+    LAUNCH(k.t, rnt::K_AUTOMORPHISM, rnt::launch_automorphism(k, dst, s, g), "automorphism");
+  }
+  rnt_buf sview;
+  sview.ctx = c0->ctx;
+  sview.n_polys = B;
+  sview.data = sig1;
+  const uint64_t ls = limb_stride(c0);
+  for (size_t p0 = 0; p0 < B; p0 += bc) {
+    const size_t c = std::min(bc, B - p0);
+    if (int rc = ks_chunk_run(k, KS, &sview, p0, c, key_a, key_b, out0->data, out1->data, ls,
+                              nullptr, nullptr, 0, sig0, 0))
+      return rc;
+  }
+  sview.data = nullptr;
+  out0->in_ntt = out1->in_ntt = 0;
+  return RNT_OK;
+}
+
+extern "C" int rnt_ct_rescale(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, const rnt_buf* c1) {
+  if (int rc = check_buf(out0, "rnt_ct_rescale")) return rc;
+  if (int rc = check_buf(out1, "rnt_ct_rescale")) return rc;
+  if (out0->ctx != out1->ctx)  // engine.rs:272-274: one shared new basis
+    return fail(RNT_ERR_BASIS_MISMATCH, "rescale_ciphertext: outputs must share one basis");
+  if (int rc = rnt_rescale(out0, c0)) return rc;
+  return rnt_rescale(out1, c1);
+}
+
+// ---------------------------------------------------------------------------
+// device count / profiling
+// ---------------------------------------------------------------------------
+extern "C" int rnt_device_count(int* n) {
+  if (!n) return fail(RNT_ERR_BAD_ARGUMENT, "null out");
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *n = c;
+  return RNT_OK;
+}
+
+extern "C" int rnt_profile_enable(const rnt_ctx* ctx, int enable) {
+  if (!ctx) return fail(RNT_ERR_BAD_ARGUMENT, "null ctx");
+  rnt::Tables* t = ctx->t.get();
+  if (int rc = set_device(ctx)) return rc;
+  HIP_TRY(hipStreamSynchronize(t->stream), "hipStreamSynchronize");
+  if (t->prof == nullptr) {
+    try {
+      t->prof = new rnt::Prof;
+    } catch (...) {
+      return fail(RNT_ERR_OUT_OF_MEMORY, "host allocation failed");
+    }
+  }
+  std::lock_guard<std::mutex> g(t->prof->mu);
+  for (auto& r : t->prof->pending) {
+    t->prof->pool.push_back(r.a);
+    t->prof->pool.push_back(r.b);
+  }
+  t->prof->pending.clear();
+  for (int i = 0; i < rnt::K_COUNT; ++i) {
+    t->prof->launches[i] = 0;
+    t->prof->ms[i] = 0;
+  }
+  t->prof->on = enable != 0;
+  return RNT_OK;
+}
+
+extern "C" int rnt_profile_read(const rnt_ctx* ctx, const char* kernel, uint64_t* launches,
+                                double* total_ms) {
+  if (!ctx || !kernel || !launches || !total_ms) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  rnt::Tables* t = ctx->t.get();
+  int id = -1;
+  for (int i = 0; i < rnt::K_COUNT; ++i)
+    if (std::strcmp(kKernelNames[i], kernel) == 0) id = i;
+  if (id < 0) return fail(RNT_ERR_BAD_ARGUMENT, "unknown kernel name '%s'", kernel);
+  *launches = 0;
+  *total_ms = 0;
+  if (t->prof == nullptr) return RNT_OK;
+  if (int rc = set_device(ctx)) return rc;
+  HIP_TRY(hipStreamSynchronize(t->stream), "hipStreamSynchronize");
+  std::lock_guard<std::mutex> g(t->prof->mu);
+  for (auto& r : t->prof->pending) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+      t->prof->launches[r.id] += 1;
+      t->prof->ms[r.id] += ms;
+    }
+    t->prof->pool.push_back(r.a);
+    t->prof->pool.push_back(r.b);
+  }
+  t->prof->pending.clear();
+  *launches = t->prof->launches[id];
+  *total_ms = t->prof->ms[id];
+  return RNT_OK;
+}

@@ -1,0 +1,169 @@
+// rnt_internal.hpp -- private types shared by the C-ABI layer (rnt_api.cpp)
+// and the kernels (rnt_kernels.hip).
+//
+// Device layout (private):
+//   A buffer of B polynomials over L limbs is one allocation of W words laid
+//   out [L][B][N] (limb-major, so a limb shard is contiguous and one prime's
+//   twiddles serve a whole contiguous launch range).  W = uint32_t when every
+//   modulus is < 2^31, else uint64_t.
+//   NTT-domain data is stored in bit-reversed order of the natural
+//   evaluation index (the output order of the merged negacyclic CT
+//   transform), i.e. device[brv(k)] = a(psi^(2k+1)).  Upload / download
+//   permute to and from the reference's natural order.
+//
+// Transform decomposition: N = R * C.  The column pass does the top log2(R)
+// CT stages (a stride-C radix-R butterfly network per column, in
+// registers); the row pass does the remaining log2(C) stages per row of C
+// contiguous words through LDS in radix-16 register passes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace rnt {
+
+constexpr int kMaxLogN = 17;
+constexpr int kRowElems = 16;  // elements per thread per operand in the row pass
+constexpr int kRowThreads = 256;
+
+template <class W>
+struct LimbConst {
+  W q;       // modulus
+  W qinv;    // q^-1 mod 2^w (Montgomery)
+  W one_p;   // floor(2^w / q): Shoup companion of 1 (canonical reduction of x < 2^w)
+  W rmod;    // 2^w mod q
+  W rmod_p;
+  W c1;      // n^-1                      (last inverse stage, plain)
+  W c1_p;
+  W c2;      // psi_inv_rev[1] * n^-1
+  W c2_p;
+  W c1r;     // n^-1 * 2^w                (last inverse stage, Montgomery-folded)
+  W c1r_p;
+  W c2r;     // psi_inv_rev[1] * n^-1 * 2^w
+  W c2r_p;
+};
+
+// Shared, immutable device tables of a root basis.  drop_last views hold a
+// shared_ptr to the same tables (no copy, unlike basis.rs:130-133).
+struct Tables {
+  int device = 0;
+  int wide = 0;            // 0: W = u32, 1: W = u64
+  uint32_t log_n = 0;
+  size_t n = 0;
+  size_t L = 0;            // channel count of the root basis
+  std::vector<uint64_t> moduli;
+  std::vector<uint64_t> psi;
+  void* tw_fwd = nullptr;   // [L][N] psi^{brv(g)}, heap order, g in [1, N)
+  void* tw_fwd_p = nullptr; // Shoup companions
+  void* tw_inv = nullptr;   // [L][N] psi^{-brv(g)}
+  void* tw_inv_p = nullptr;
+  void* lconst = nullptr;   // [L] LimbConst<W>
+  void* resc = nullptr;     // [L][L]: resc[l][i] = (q_l mod q_i)^-1 mod q_i, i < l
+  void* resc_p = nullptr;   // [L][L] Shoup companions
+  hipStream_t stream = nullptr;
+  struct Prof* prof = nullptr;  // per-kernel event timing (rnt_profile_*)
+  ~Tables();
+};
+
+// Kernel ids for rnt_profile_read.
+enum KernelId {
+  K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
+  K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_COUNT
+};
+
+struct Prof {
+  std::mutex mu;
+  bool on = false;
+  struct Rec {
+    int id;
+    hipEvent_t a, b;
+  };
+  std::vector<Rec> pending;
+  std::vector<hipEvent_t> pool;
+  uint64_t launches[K_COUNT] = {};
+  double ms[K_COUNT] = {};
+};
+
+}  // namespace rnt
+
+struct rnt_ctx {
+  std::shared_ptr<rnt::Tables> t;
+  size_t L = 0;  // channel count of this (possibly dropped) basis
+};
+
+struct rnt_buf {
+  const rnt_ctx* ctx = nullptr;
+  size_t n_polys = 0;
+  void* data = nullptr;       // [L][B][N] words
+  int in_ntt = 0;
+  // lazily grown per-buffer workspace (buffers are never used by two
+  // threads at once, so this needs no lock)
+  void* ws = nullptr;
+  size_t ws_bytes = 0;
+  void* stage = nullptr;      // u64 host-format staging for upload/download
+  size_t stage_bytes = 0;
+};
+
+namespace rnt {
+
+// Geometry of the N = R * C split.
+struct Geom {
+  uint32_t log_n, log_r, log_c;
+  size_t n, r, c;
+};
+Geom geom_for(uint32_t log_n);
+
+// Kernel argument bundle common to all launches.
+struct Launch {
+  const Tables* t;
+  size_t L;            // limbs processed (prefix of the root basis)
+  size_t B;            // polys per buffer
+  hipStream_t s;
+};
+
+// ---- launchers (rnt_kernels.hip), W-dispatched by t->wide ---------------
+// All arrays are [limb][poly][N] with an explicit limb stride `*_ls` (words);
+// k.B polys (a batch or a chunk of one) and k.L limbs are processed.
+// Forward column pass on up to two operands (in0->out0, in1->out1).
+hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* out1,
+                          const void* in1, uint64_t in_ls, uint64_t out_ls);
+// Row pass.  mode 0: forward rows (in place on x); 1: inverse rows (in place
+// on x); 2: poly-mul rows: x <- INVrow(FWDrow(x) (.) FWDrow(y) * 2^-w).
+hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls);
+// Inverse column pass with n^-1 folded into the last stage; rfold adds the
+// Montgomery factor 2^w.  addend (optional, coefficient domain, out layout).
+hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
+                          uint64_t in_ls, int rfold, const void* addend);
+// Elementwise over k.L*k.B*N contiguous words: op 0 add, 1 sub, 2 neg,
+// 3 pointwise mul (canonical a*b mod q), 4 Montgomery product (a*b*2^-w).
+hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a,
+                              const void* b);
+// k.L = limbs of the input; output has k.L - 1 (same poly count / stride B*N).
+hipError_t launch_rescale(const Launch& k, void* out, const void* in);
+hipError_t launch_automorphism(const Launch& k, void* out, const void* in, uint64_t g);
+// host u64 [B][L][N] staging <-> device; err_index receives the smallest
+// offending flat index (UINT64_MAX if none) for non-reduced input.
+hipError_t launch_import(const Launch& k, void* dst, const uint64_t* stage, int to_brv,
+                         unsigned long long* err_index);
+hipError_t launch_import_coeffs(const Launch& k, void* dst, const int64_t* stage);
+hipError_t launch_export(const Launch& k, uint64_t* stage, const void* src, int from_brv);
+// Key-switch pieces.  S: [L_target][L_source][k.B][N] scratch (chunk-local).
+hipError_t launch_ks_decompose(const Launch& k, void* S, const void* d, uint64_t d_ls);
+// u0 rows <- INVrow(sum_i FWDrow(S[j][i]) (.) key_b[i][j] (+ init0)), u1 with
+// key_a.  init0/init1 may be null (NTT-domain rows, Montgomery-scaled).
+hipError_t launch_ks_rows(const Launch& k, void* u0, void* u1, uint64_t u_ls, const void* S,
+                          const void* key_a, const void* key_b, uint64_t key_ls,
+                          const void* init0, const void* init1, uint64_t init_ls);
+// Tensor rows for ct x ct: inputs are column-transformed c0,c1,c0p,c1p.
+// Writes d0hat, d1hat (NTT rows, Montgomery-scaled) and the inverse-row
+// output of d2 into d2row.  All arrays share limb stride ls.
+hipError_t launch_tensor_rows(const Launch& k, void* d0hat, void* d1hat, void* d2row,
+                              const void* c0, const void* c1, const void* c0p,
+                              const void* c1p, uint64_t ls);
+
+}  // namespace rnt

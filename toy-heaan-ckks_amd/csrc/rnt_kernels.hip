@@ -1,0 +1,1097 @@
+// rnt_kernels.hip -- hand-written gfx950 kernels for the RNS-NTT hot path.
+//
+// Reference behaviour being replaced (oiwn/toy-heaan-ckks):
+//   to_ntt_domain / to_coeff_domain   src/rings/backends/rns_ntt/poly.rs:136-166
+//   forward_ntt / inverse_ntt / CT    poly.rs:574-625
+//   MulAssign (both domains)          poly.rs:277-331
+//   AddAssign / Neg                   poly.rs:254-275, 370-385
+//   rescale_into                      poly.rs:187-228
+//   automorphism                      poly.rs:492-541
+//   gadget key-switch sum             src/crypto/engine.rs:505-528, 429-452
+//   tensor product                    engine.rs:480-493
+//
+// Transform: merged negacyclic Cooley-Tukey (twist folded into the
+// twiddles: psi_rev[g] = psi^{brv(g)} over the heap g in [1, N)), output in
+// bit-reversed order; inverse is the matching Gentleman-Sande network with
+// n^-1 folded into its last stage.  Values equal the reference's
+// a(psi^(2k+1)) exactly; only the order is private.
+//
+// Decomposition N = R * C (see rnt_internal.hpp):
+//   column pass: stages with distance >= C, one column (stride C) per
+//                thread, R <= 16 registers, coalesced 256 B per wave load;
+//   row pass:    stages with distance < C, one row of C contiguous words per
+//                C/16 threads, radix-16 register passes, LDS exchanges with a
+//                1-in-16 pad (conflict-free for every pass distribution).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "rnt_internal.hpp"
+#include "rnt_modarith.hpp"
+
+namespace rnt {
+
+template <class W>
+struct TabPtrs {
+  const W* tw;
+  const W* twp;
+  const W* itw;
+  const W* itwp;
+  const LimbConst<W>* lc;
+  const W* resc;
+  const W* rescp;
+  uint32_t Lroot;
+};
+
+template <class W>
+static TabPtrs<W> tab_ptrs(const Tables* t) {
+  TabPtrs<W> p;
+  p.tw = (const W*)t->tw_fwd;
+  p.twp = (const W*)t->tw_fwd_p;
+  p.itw = (const W*)t->tw_inv;
+  p.itwp = (const W*)t->tw_inv_p;
+  p.lc = (const LimbConst<W>*)t->lconst;
+  p.resc = (const W*)t->resc;
+  p.rescp = (const W*)t->resc_p;
+  p.Lroot = (uint32_t)t->L;
+  return p;
+}
+
+Geom geom_for(uint32_t log_n) {
+  Geom g;
+  g.log_n = log_n;
+  if (log_n < 4) {  // tiny rings: one row holds the whole polynomial
+    g.log_r = 0;
+    g.log_c = log_n;
+  } else if (log_n < 8) {
+    g.log_r = log_n - 4;
+    g.log_c = 4;
+  } else {
+    g.log_r = 4;
+    g.log_c = log_n - 4;
+  }
+  g.n = (size_t)1 << log_n;
+  g.r = (size_t)1 << g.log_r;
+  g.c = (size_t)1 << g.log_c;
+  return g;
+}
+
+// ---------------------------------------------------------------------------
+// column passes
+// ---------------------------------------------------------------------------
+
+template <class W, int LOG_R>
+__device__ __forceinline__ void col_ct(W (&x)[1 << LOG_R], const W* tw, const W* twp, W q) {
+  constexpr int R = 1 << LOG_R;
+#pragma unroll
+  for (int k = 0; k < LOG_R; ++k) {
+    const int d = R >> (k + 1);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (i & d) continue;
+      const int node = (1 << k) + (i >> (LOG_R - k));
+      ct_bfly<W>(x[i], x[i + d], tw[node], twp[node], q);
+    }
+  }
+}
+
+// x <- GS network over the column with the last (distance N/2) stage scaled
+// by c1 (upper) and c2 (lower).
+template <class W, int LOG_R>
+__device__ __forceinline__ void col_gs(W (&x)[1 << LOG_R], const W* itw, const W* itwp, W q, W c1,
+                                       W c1p, W c2, W c2p) {
+  constexpr int R = 1 << LOG_R;
+#pragma unroll
+  for (int sl = 0; sl < LOG_R; ++sl) {
+    const int d = 1 << sl;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (i & d) continue;
+      if (sl == LOG_R - 1) {
+        W u = x[i], v = x[i + d];
+        x[i] = shoup_mul<W>(u + v, c1, c1p, q);
+        x[i + d] = shoup_mul<W>(u - v + q, c2, c2p, q);
+      } else {
+        const int node = (1 << (LOG_R - 1 - sl)) + (i >> (sl + 1));
+        gs_bfly<W>(x[i], x[i + d], itw[node], itwp[node], q);
+      }
+    }
+  }
+  if (LOG_R == 0) x[0] = shoup_mul<W>(x[0], c1, c1p, q);
+}
+
+// Forward column pass.  Thread = (limb l, poly p, column j1); j1 fastest.
+template <class W, int LOG_R>
+__global__ void __launch_bounds__(256)
+k_col_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t log_n,
+          uint32_t log_c, uint32_t B, uint64_t in_ls, uint64_t out_ls, uint64_t total) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  constexpr int R = 1 << LOG_R;
+  const uint32_t C = 1u << log_c;
+  const uint64_t N = 1ull << log_n;
+  const uint32_t j1 = (uint32_t)(gid & (C - 1));
+  const uint64_t lp = gid >> log_c;
+  const uint32_t l = (uint32_t)(lp / B);
+  const uint32_t p = (uint32_t)(lp - (uint64_t)l * B);
+  const uint64_t ib = (uint64_t)l * in_ls + (uint64_t)p * N + j1;
+  const uint64_t ob = (uint64_t)l * out_ls + (uint64_t)p * N + j1;
+  const W q = tp.lc[l].q;
+  const W* tw = tp.tw + (uint64_t)l * N;
+  const W* twp = tp.twp + (uint64_t)l * N;
+  W x[R];
+  // operand 1 first: out0 may alias in1 (out = a * b with out == b)
+  if (in1 != nullptr) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = in1[ib + (uint64_t)i * C];
+    col_ct<W, LOG_R>(x, tw, twp, q);
+#pragma unroll
+    for (int i = 0; i < R; ++i) out1[ob + (uint64_t)i * C] = x[i];
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) x[i] = in0[ib + (uint64_t)i * C];
+  col_ct<W, LOG_R>(x, tw, twp, q);
+#pragma unroll
+  for (int i = 0; i < R; ++i) out0[ob + (uint64_t)i * C] = x[i];
+}
+
+template <class W, int LOG_R>
+__global__ void __launch_bounds__(256)
+k_col_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, uint32_t log_c,
+          uint32_t B, uint64_t in_ls, uint64_t out_ls, uint64_t total, int rfold) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  constexpr int R = 1 << LOG_R;
+  const uint32_t C = 1u << log_c;
+  const uint64_t N = 1ull << log_n;
+  const uint32_t j1 = (uint32_t)(gid & (C - 1));
+  const uint64_t lp = gid >> log_c;
+  const uint32_t l = (uint32_t)(lp / B);
+  const uint32_t p = (uint32_t)(lp - (uint64_t)l * B);
+  const uint64_t ib = (uint64_t)l * in_ls + (uint64_t)p * N + j1;
+  const uint64_t base = (uint64_t)l * out_ls + (uint64_t)p * N + j1;
+  const LimbConst<W> lc = tp.lc[l];
+  const W* itw = tp.itw + (uint64_t)l * N;
+  const W* itwp = tp.itwp + (uint64_t)l * N;
+  W x[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) x[i] = in[ib + (uint64_t)i * C];
+  if (rfold)
+    col_gs<W, LOG_R>(x, itw, itwp, lc.q, lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p);
+  else
+    col_gs<W, LOG_R>(x, itw, itwp, lc.q, lc.c1, lc.c1_p, lc.c2, lc.c2_p);
+  if (addend != nullptr) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) x[i] = add_mod<W>(x[i], addend[base + (uint64_t)i * C], lc.q);
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) out[base + (uint64_t)i * C] = x[i];
+}
+
+// Key-switch decomposition + forward column pass (engine.rs:507-516 fused
+// with the first half of alpha_i's forward NTT): thread = (target limb j,
+// source limb i, poly p, column j1); reads limb i of d, reduces mod q_j
+// canonically (R5), transforms with q_j's tables, writes S[j][i][p].
+template <class W, int LOG_R>
+__global__ void __launch_bounds__(256)
+k_ks_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32_t log_n,
+               uint32_t log_c, uint32_t L, uint32_t B, uint64_t d_ls, uint64_t total) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  constexpr int R = 1 << LOG_R;
+  const uint32_t C = 1u << log_c;
+  const uint64_t N = 1ull << log_n;
+  const uint32_t j1 = (uint32_t)(gid & (C - 1));
+  uint64_t rest = gid >> log_c;  // ((j*L + i)*B + p)
+  const uint32_t p = (uint32_t)(rest % B);
+  rest /= B;
+  const uint32_t i = (uint32_t)(rest % L);
+  const uint32_t j = (uint32_t)(rest / L);
+  const LimbConst<W> lc = tp.lc[j];
+  const W* tw = tp.tw + (uint64_t)j * N;
+  const W* twp = tp.twp + (uint64_t)j * N;
+  const uint64_t src = (uint64_t)i * d_ls + (uint64_t)p * N + j1;
+  const uint64_t dst = (((uint64_t)j * L + i) * B + p) * N + j1;
+  W x[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) x[t] = shoup_mul<W>(d[src + (uint64_t)t * C], (W)1, lc.one_p, lc.q);
+  col_ct<W, LOG_R>(x, tw, twp, lc.q);
+#pragma unroll
+  for (int t = 0; t < R; ++t) S[dst + (uint64_t)t * C] = x[t];
+}
+
+// ---------------------------------------------------------------------------
+// row passes
+// ---------------------------------------------------------------------------
+
+// Row-local index of register i for a pass whose register bits are
+// [bb, bb+LOGE).
+template <int LOGE>
+__device__ __forceinline__ uint32_t relem(uint32_t tau, int bb, int i) {
+  const uint32_t lowmask = (1u << bb) - 1u;
+  return (tau & lowmask) | ((uint32_t)i << bb) | ((tau >> bb) << (bb + LOGE));
+}
+__device__ __forceinline__ uint32_t swz(uint32_t j) { return j + (j >> 4); }
+
+// Pass schedule of the row stages.  LOGE == 4: radix-16 passes from the top
+// bits down, then a partial pass on bits [0, log_c mod 4) with register bits
+// [0, 4).  LOGE < 4 (tiny rings, log_c == LOGE): one pass holding the row.
+template <int LOGE>
+struct RowSched {
+  int full, rem, P;
+  uint32_t log_c;
+  __device__ __forceinline__ explicit RowSched(uint32_t lc) : log_c(lc) {
+    if (LOGE == 4) {
+      full = (int)(lc >> 2);
+      rem = (int)(lc & 3);
+    } else {
+      full = 0;
+      rem = (int)lc;
+    }
+    P = full + (rem ? 1 : 0);
+  }
+  __device__ __forceinline__ int bb(int p) const {
+    return (p >= 0 && p < full) ? (int)log_c - 4 * (p + 1) : 0;
+  }
+  __device__ __forceinline__ int k(int p) const { return p < full ? 4 : rem; }
+  __device__ __forceinline__ int first_bb() const { return bb(0); }
+  __device__ __forceinline__ int last_bb() const { return bb(P - 1); }
+};
+
+// CT stages on bits [bb, bb+K) of the row for NOPS operands sharing twiddles.
+template <class W, int NOPS, int LOGE>
+__device__ __forceinline__ void row_ct(W (&x)[NOPS][1 << LOGE], int bb, int K, uint64_t gbase,
+                                       const W* tw, const W* twp, W q) {
+  constexpr int E = 1 << LOGE;
+  constexpr int H = E > 1 ? E / 2 : 1;
+#pragma unroll
+  for (int sl = LOGE - 1; sl >= 0; --sl) {
+    if (sl >= K) continue;
+    const int s = bb + sl;
+    const uint64_t nb = gbase >> (s + 1);
+    const int d = 1 << sl;
+    const int cnt = H >> sl;
+    W w[H], wp[H];
+#pragma unroll
+    for (int m = 0; m < H; ++m) {
+      if (m < cnt) {
+        w[m] = tw[nb + m];
+        wp[m] = twp[nb + m];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      if (i & d) continue;
+      const int m = i >> (sl + 1);
+#pragma unroll
+      for (int o = 0; o < NOPS; ++o) ct_bfly<W>(x[o][i], x[o][i | d], w[m], wp[m], q);
+    }
+  }
+}
+
+template <class W, int NOPS, int LOGE>
+__device__ __forceinline__ void row_gs(W (&x)[NOPS][1 << LOGE], int bb, int K, uint64_t gbase,
+                                       const W* itw, const W* itwp, W q) {
+  constexpr int E = 1 << LOGE;
+  constexpr int H = E > 1 ? E / 2 : 1;
+#pragma unroll
+  for (int sl = 0; sl < LOGE; ++sl) {
+    if (sl >= K) continue;
+    const int s = bb + sl;
+    const uint64_t nb = gbase >> (s + 1);
+    const int d = 1 << sl;
+    const int cnt = H >> sl;
+    W w[H], wp[H];
+#pragma unroll
+    for (int m = 0; m < H; ++m) {
+      if (m < cnt) {
+        w[m] = itw[nb + m];
+        wp[m] = itwp[nb + m];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      if (i & d) continue;
+      const int m = i >> (sl + 1);
+#pragma unroll
+      for (int o = 0; o < NOPS; ++o) gs_bfly<W>(x[o][i], x[o][i | d], w[m], wp[m], q);
+    }
+  }
+}
+
+// Move NOPS register sets from distribution bb_from to bb_to through LDS.
+// Region of operand o for this row: lds + (o * rows_per_wg + slot) * padc.
+template <class W, int NOPS, int LOGE>
+__device__ __forceinline__ void row_exchange(W (&x)[NOPS][1 << LOGE], W* lds, uint32_t padc,
+                                             uint32_t rows_per_wg, uint32_t slot, uint32_t tau,
+                                             int bb_from, int bb_to) {
+  constexpr int E = 1 << LOGE;
+#pragma unroll
+  for (int o = 0; o < NOPS; ++o) {
+    W* reg = lds + ((uint32_t)o * rows_per_wg + slot) * padc;
+#pragma unroll
+    for (int i = 0; i < E; ++i) reg[swz(relem<LOGE>(tau, bb_from, i))] = x[o][i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < NOPS; ++o) {
+    const W* reg = lds + ((uint32_t)o * rows_per_wg + slot) * padc;
+#pragma unroll
+    for (int i = 0; i < E; ++i) x[o][i] = reg[swz(relem<LOGE>(tau, bb_to, i))];
+  }
+  __syncthreads();
+}
+
+struct RowPos {
+  uint32_t slot, tau, rpw, padc, C;
+  uint32_t l, p, r;
+  bool active;
+  uint64_t gb;  // N + r*C: heap base of this row
+};
+
+template <int LOGE>
+__device__ __forceinline__ RowPos row_pos(uint32_t log_n, uint32_t log_c, uint32_t B,
+                                          uint64_t rows_total) {
+  RowPos rp;
+  const uint32_t log_t = log_c - LOGE;
+  rp.C = 1u << log_c;
+  rp.rpw = blockDim.x >> log_t;
+  rp.slot = threadIdx.x >> log_t;
+  rp.tau = threadIdx.x & ((1u << log_t) - 1u);
+  rp.padc = rp.C + (rp.C >> 4);
+  uint64_t row = (uint64_t)blockIdx.x * rp.rpw + rp.slot;
+  rp.active = row < rows_total;
+  if (!rp.active) row = 0;
+  const uint32_t log_r = log_n - log_c;
+  const uint64_t lp = row >> log_r;
+  rp.r = (uint32_t)(row & ((1u << log_r) - 1u));
+  rp.l = (uint32_t)(lp / B);
+  rp.p = (uint32_t)(lp - (uint64_t)rp.l * B);
+  rp.gb = (1ull << log_n) + (uint64_t)rp.r * rp.C;
+  return rp;
+}
+
+// All forward row passes on NOPS operands loaded in the first-pass
+// distribution; leaves the registers in the last-pass distribution.
+template <class W, int NOPS, int LOGE>
+__device__ __forceinline__ void rows_fwd(W (&x)[NOPS][1 << LOGE], const RowSched<LOGE>& sc,
+                                         const RowPos& rp, W* lds, const W* tw, const W* twp,
+                                         W q) {
+  int prev = sc.first_bb();
+  for (int p = 0; p < sc.P; ++p) {
+    const int bb = sc.bb(p);
+    if (p > 0) row_exchange<W, NOPS, LOGE>(x, lds, rp.padc, rp.rpw, rp.slot, rp.tau, prev, bb);
+    row_ct<W, NOPS, LOGE>(x, bb, sc.k(p), rp.gb + relem<LOGE>(rp.tau, bb, 0), tw, twp, q);
+    prev = bb;
+  }
+}
+
+// All inverse row passes; last-pass distribution in, first-pass out.
+template <class W, int NOPS, int LOGE>
+__device__ __forceinline__ void rows_inv(W (&x)[NOPS][1 << LOGE], const RowSched<LOGE>& sc,
+                                         const RowPos& rp, W* lds, const W* itw, const W* itwp,
+                                         W q) {
+  int prev = sc.last_bb();
+  for (int p = sc.P - 1; p >= 0; --p) {
+    const int bb = sc.bb(p);
+    if (p < sc.P - 1)
+      row_exchange<W, NOPS, LOGE>(x, lds, rp.padc, rp.rpw, rp.slot, rp.tau, prev, bb);
+    row_gs<W, NOPS, LOGE>(x, bb, sc.k(p), rp.gb + relem<LOGE>(rp.tau, bb, 0), itw, itwp, q);
+    prev = bb;
+  }
+}
+
+// mode 0: forward rows in place; 1: inverse rows in place;
+// 2: poly-mul rows: x <- INV(FWD(x) (.) FWD(y)) with Montgomery pointwise.
+template <class W, int MODE, int LOGE>
+__global__ void __launch_bounds__(512)
+k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_n,
+      uint32_t log_c, uint32_t B, uint64_t ls, uint64_t rows_total) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  constexpr int E = 1 << LOGE;
+  W* lds = (W*)smem_raw;
+  const RowPos rp = row_pos<LOGE>(log_n, log_c, B, rows_total);
+  const RowSched<LOGE> sc(log_c);
+  const uint64_t N = 1ull << log_n;
+  const uint64_t base = (uint64_t)rp.l * ls + (uint64_t)rp.p * N + (uint64_t)rp.r * rp.C;
+  const LimbConst<W> lc = tp.lc[rp.l];
+  const W* tw = tp.tw + (uint64_t)rp.l * N;
+  const W* twp = tp.twp + (uint64_t)rp.l * N;
+  const W* itw = tp.itw + (uint64_t)rp.l * N;
+  const W* itwp = tp.itwp + (uint64_t)rp.l * N;
+  const int bb0 = sc.first_bb();
+  const int bbl = sc.last_bb();
+  if (MODE == 2) {
+    W v[2][E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const uint32_t e = relem<LOGE>(rp.tau, bb0, i);
+      v[0][i] = xg[base + e];
+      v[1][i] = yg[base + e];
+    }
+    rows_fwd<W, 2, LOGE>(v, sc, rp, lds, tw, twp, lc.q);
+    W z[1][E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) z[0][i] = mont_mul<W>(v[0][i], v[1][i], lc.q, lc.qinv);
+    rows_inv<W, 1, LOGE>(z, sc, rp, lds, itw, itwp, lc.q);
+    if (rp.active) {
+#pragma unroll
+      for (int i = 0; i < E; ++i) xg[base + relem<LOGE>(rp.tau, bb0, i)] = z[0][i];
+    }
+  } else if (MODE == 0) {
+    W v[1][E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[0][i] = xg[base + relem<LOGE>(rp.tau, bb0, i)];
+    rows_fwd<W, 1, LOGE>(v, sc, rp, lds, tw, twp, lc.q);
+    if (rp.active) {
+#pragma unroll
+      for (int i = 0; i < E; ++i) xg[base + relem<LOGE>(rp.tau, bbl, i)] = v[0][i];
+    }
+  } else {
+    W v[1][E];
+#pragma unroll
+    for (int i = 0; i < E; ++i) v[0][i] = xg[base + relem<LOGE>(rp.tau, bbl, i)];
+    rows_inv<W, 1, LOGE>(v, sc, rp, lds, itw, itwp, lc.q);
+    if (rp.active) {
+#pragma unroll
+      for (int i = 0; i < E; ++i) xg[base + relem<LOGE>(rp.tau, bb0, i)] = v[0][i];
+    }
+  }
+}
+
+// Key-switch rows.  Row = (target limb j, poly p, row r).  For every source
+// limb i: forward rows of S[j][i][p], multiply-accumulate with the
+// NTT-resident keys; then the inverse rows of both accumulators.
+template <class W, int LOGE>
+__global__ void __launch_bounds__(512)
+k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
+          const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
+          const W* __restrict__ init0, const W* __restrict__ init1, uint64_t init_ls,
+          TabPtrs<W> tp, uint32_t log_n, uint32_t log_c, uint32_t L, uint32_t B, uint64_t ls,
+          uint64_t rows_total) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  constexpr int E = 1 << LOGE;
+  W* lds = (W*)smem_raw;
+  const RowPos rp = row_pos<LOGE>(log_n, log_c, B, rows_total);  // rp.l == target limb j
+  const RowSched<LOGE> sc(log_c);
+  const uint64_t N = 1ull << log_n;
+  const uint32_t j = rp.l;
+  const uint64_t rowoff = (uint64_t)rp.r * rp.C;
+  const uint64_t obase = (uint64_t)j * ls + (uint64_t)rp.p * N + rowoff;
+  const uint64_t ibase = (uint64_t)j * init_ls + (uint64_t)rp.p * N + rowoff;
+  const LimbConst<W> lc = tp.lc[j];
+  const W* tw = tp.tw + (uint64_t)j * N;
+  const W* twp = tp.twp + (uint64_t)j * N;
+  const W* itw = tp.itw + (uint64_t)j * N;
+  const W* itwp = tp.itwp + (uint64_t)j * N;
+  const int bb0 = sc.first_bb();
+  const int bbl = sc.last_bb();
+  W acc[2][E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const uint32_t pos = relem<LOGE>(rp.tau, bbl, e);
+    acc[0][e] = init0 ? init0[ibase + pos] : (W)0;
+    acc[1][e] = init1 ? init1[ibase + pos] : (W)0;
+  }
+  for (uint32_t i = 0; i < L; ++i) {
+    const uint64_t sbase = (((uint64_t)j * L + i) * B + rp.p) * N + rowoff;
+    W x[1][E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[0][e] = S[sbase + relem<LOGE>(rp.tau, bb0, e)];
+    rows_fwd<W, 1, LOGE>(x, sc, rp, lds, tw, twp, lc.q);
+    // key poly i, limb j (key buffers hold L polys: limb stride key_ls)
+    const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + rowoff;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint32_t pos = relem<LOGE>(rp.tau, bbl, e);
+      const W kb = key_b[kbase + pos];
+      const W ka = key_a[kbase + pos];
+      acc[0][e] = add_mod<W>(acc[0][e], mont_mul<W>(x[0][e], kb, lc.q, lc.qinv), lc.q);
+      acc[1][e] = add_mod<W>(acc[1][e], mont_mul<W>(x[0][e], ka, lc.q, lc.qinv), lc.q);
+    }
+  }
+  rows_inv<W, 2, LOGE>(acc, sc, rp, lds, itw, itwp, lc.q);
+  if (rp.active) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const uint32_t pos = relem<LOGE>(rp.tau, bb0, e);
+      u0[obase + pos] = acc[0][e];
+      u1[obase + pos] = acc[1][e];
+    }
+  }
+}
+
+// Tensor-product rows (engine.rs:480-493): inputs are the column-pass
+// outputs of c0, c1, c0', c1'.  d0 = c0 c0', d1 = c0 c1' + c1 c0',
+// d2 = c1 c1' (pointwise, Montgomery-scaled by 2^-w).  d0hat / d1hat are
+// written as NTT-domain rows (last-pass distribution) for the key-switch
+// accumulators; d2 goes through the inverse rows into d2row.
+template <class W, int LOGE>
+__global__ void __launch_bounds__(512)
+k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2row,
+              const W* __restrict__ c0, const W* __restrict__ c1, const W* __restrict__ c0p,
+              const W* __restrict__ c1p, TabPtrs<W> tp, uint32_t log_n, uint32_t log_c,
+              uint32_t B, uint64_t ls, uint64_t rows_total) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  constexpr int E = 1 << LOGE;
+  W* lds = (W*)smem_raw;
+  const RowPos rp = row_pos<LOGE>(log_n, log_c, B, rows_total);
+  const RowSched<LOGE> sc(log_c);
+  const uint64_t N = 1ull << log_n;
+  const uint64_t base = (uint64_t)rp.l * ls + (uint64_t)rp.p * N + (uint64_t)rp.r * rp.C;
+  const LimbConst<W> lc = tp.lc[rp.l];
+  const W* tw = tp.tw + (uint64_t)rp.l * N;
+  const W* twp = tp.twp + (uint64_t)rp.l * N;
+  const W* itw = tp.itw + (uint64_t)rp.l * N;
+  const W* itwp = tp.itwp + (uint64_t)rp.l * N;
+  const int bb0 = sc.first_bb();
+  const int bbl = sc.last_bb();
+  W a[2][E], b[2][E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const uint32_t e = relem<LOGE>(rp.tau, bb0, i);
+    a[0][i] = c0[base + e];
+    a[1][i] = c1[base + e];
+  }
+  rows_fwd<W, 2, LOGE>(a, sc, rp, lds, tw, twp, lc.q);
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const uint32_t e = relem<LOGE>(rp.tau, bb0, i);
+    b[0][i] = c0p[base + e];
+    b[1][i] = c1p[base + e];
+  }
+  rows_fwd<W, 2, LOGE>(b, sc, rp, lds, tw, twp, lc.q);
+  W d2[1][E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const W q = lc.q, qi = lc.qinv;
+    const W d0 = mont_mul<W>(a[0][i], b[0][i], q, qi);
+    const W d1 = add_mod<W>(mont_mul<W>(a[0][i], b[1][i], q, qi),
+                            mont_mul<W>(a[1][i], b[0][i], q, qi), q);
+    d2[0][i] = mont_mul<W>(a[1][i], b[1][i], q, qi);
+    if (rp.active) {
+      const uint32_t pos = relem<LOGE>(rp.tau, bbl, i);
+      d0hat[base + pos] = d0;
+      d1hat[base + pos] = d1;
+    }
+  }
+  rows_inv<W, 1, LOGE>(d2, sc, rp, lds, itw, itwp, lc.q);
+  if (rp.active) {
+#pragma unroll
+    for (int i = 0; i < E; ++i) d2row[base + relem<LOGE>(rp.tau, bb0, i)] = d2[0][i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// elementwise / permutation kernels
+// ---------------------------------------------------------------------------
+
+template <class W>
+__global__ void __launch_bounds__(256)
+k_elementwise(W* __restrict__ out, const W* __restrict__ a, const W* __restrict__ b, int op,
+              TabPtrs<W> tp, uint64_t limb_words, uint64_t total) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const uint32_t l = (uint32_t)(gid / limb_words);
+  const LimbConst<W> lc = tp.lc[l];
+  const W x = a[gid];
+  W r;
+  switch (op) {
+    case 0: r = add_mod<W>(x, b[gid], lc.q); break;
+    case 1: r = sub_mod<W>(x, b[gid], lc.q); break;
+    case 2: r = x == 0 ? (W)0 : (W)(lc.q - x); break;
+    case 3: {
+      const W m = mont_mul<W>(x, b[gid], lc.q, lc.qinv);
+      r = shoup_mul<W>(m, lc.rmod, lc.rmod_p, lc.q);
+      break;
+    }
+    default: r = mont_mul<W>(x, b[gid], lc.q, lc.qinv);
+  }
+  out[gid] = r;
+}
+
+// rescale_into (poly.rs:212-225): out[l] = (c_l - (c_last mod q_l)) * q_last^-1.
+template <class W>
+__global__ void __launch_bounds__(256)
+k_rescale(W* __restrict__ out, const W* __restrict__ in, TabPtrs<W> tp, uint32_t last,
+          uint64_t ls_in, uint64_t ls_out, uint64_t poly_words, uint64_t total) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const uint32_t l = (uint32_t)(gid / poly_words);
+  const uint64_t off = gid - (uint64_t)l * poly_words;
+  const LimbConst<W> lc = tp.lc[l];
+  const W inv = tp.resc[(uint64_t)last * tp.Lroot + l];
+  const W invp = tp.rescp[(uint64_t)last * tp.Lroot + l];
+  const W ci = in[(uint64_t)l * ls_in + off];
+  const W cl = shoup_mul<W>(in[(uint64_t)last * ls_in + off], (W)1, lc.one_p, lc.q);
+  out[(uint64_t)l * ls_out + off] = shoup_mul<W>(sub_mod<W>(ci, cl, lc.q), inv, invp, lc.q);
+}
+
+// automorphism for odd g: out[t] gathers its unique source (poly.rs:520-537).
+template <class W>
+__global__ void __launch_bounds__(256)
+k_automorph_odd(W* __restrict__ out, const W* __restrict__ in, TabPtrs<W> tp, uint32_t log_n,
+                uint64_t ginv, uint64_t poly_words, uint64_t total) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const uint64_t N = 1ull << log_n;
+  const uint32_t l = (uint32_t)(gid / poly_words);
+  const uint64_t jo = gid & (N - 1);
+  const uint64_t pbase = gid - jo;
+  const uint64_t t = (jo * ginv) & (2 * N - 1);
+  const W q = tp.lc[l].q;
+  W v;
+  if (t < N) {
+    v = in[pbase + t];
+  } else {
+    const W c = in[pbase + t - N];
+    v = c == 0 ? (W)0 : (W)(q - c);
+  }
+  out[gid] = v;
+}
+
+// automorphism for even g != 0 mod 2N (not a ring automorphism): the
+// reference's scatter loop keeps, per output slot, the LAST (largest i)
+// non-zero writer (poly.rs:520-537).  g = 2^e * h, h odd; i*g = r (mod 2N)
+// iff 2^e | r and i = (r >> e) * h^-1 (mod M), M = 2N >> e.
+template <class W>
+__global__ void __launch_bounds__(256)
+k_automorph_even(W* __restrict__ out, const W* __restrict__ in, TabPtrs<W> tp, uint32_t log_n,
+                 uint32_t e, uint64_t hinv, uint64_t poly_words, uint64_t total) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const uint64_t N = 1ull << log_n;
+  const uint32_t l = (uint32_t)(gid / poly_words);
+  const uint64_t jo = gid & (N - 1);
+  const uint64_t pbase = gid - jo;
+  const uint64_t M = (2 * N) >> e;
+  const W q = tp.lc[l].q;
+  int64_t best = -1;
+  int best_neg = 0;
+  W best_val = 0;
+  for (int h = 0; h < 2; ++h) {
+    const uint64_t r = jo + (h ? N : 0);
+    if (r & ((1ull << e) - 1)) continue;
+    const uint64_t i0 = ((r >> e) * hinv) & (M - 1);
+    if (i0 >= N) continue;
+    // largest i = i0 + k*M < N with a non-zero coefficient
+    uint64_t kmax = (N - 1 - i0) / M;
+    for (int64_t k = (int64_t)kmax; k >= 0; --k) {
+      const uint64_t i = i0 + (uint64_t)k * M;
+      if ((int64_t)i <= best) break;
+      const W c = in[pbase + i];
+      if (c != 0) {
+        best = (int64_t)i;
+        best_neg = h;
+        best_val = c;
+        break;
+      }
+    }
+  }
+  W v = 0;
+  if (best >= 0) v = best_neg ? (W)(q - best_val) : best_val;
+  out[gid] = v;
+}
+
+__device__ __forceinline__ uint64_t brv_dev(uint64_t k, uint32_t bits) {
+  return bits == 0 ? 0 : (__brevll(k) >> (64 - bits));
+}
+
+// host [B][L][N] u64 staging -> device [L][B][N] W (with validation).
+template <class W>
+__global__ void __launch_bounds__(256)
+k_import(W* __restrict__ dst, const uint64_t* __restrict__ stage, TabPtrs<W> tp, uint32_t log_n,
+         uint32_t L, uint64_t ls, int to_brv, unsigned long long* err, uint64_t total) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const uint64_t N = 1ull << log_n;
+  const uint64_t k = gid & (N - 1);
+  const uint64_t pl = gid >> log_n;  // p*L + l
+  const uint32_t l = (uint32_t)(pl % L);
+  const uint64_t p = pl / L;
+  const uint64_t v = stage[gid];
+  const uint64_t q = (uint64_t)tp.lc[l].q;
+  if (v >= q) atomicMin(err, (unsigned long long)gid);
+  const uint64_t pos = to_brv ? brv_dev(k, log_n) : k;
+  dst[(uint64_t)l * ls + p * N + pos] = (W)(v >= q ? 0 : v);
+}
+
+// from_coeffs (poly.rs:55-61): rem_euclid per channel.
+template <class W>
+__global__ void __launch_bounds__(256)
+k_import_coeffs(W* __restrict__ dst, const int64_t* __restrict__ coeffs, TabPtrs<W> tp,
+                uint32_t log_n, uint32_t L, uint32_t B, uint64_t ls, uint64_t total) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;  // total = L * B * N, order [L][B][N]
+  const uint64_t N = 1ull << log_n;
+  const uint64_t k = gid & (N - 1);
+  const uint64_t lp = gid >> log_n;
+  const uint32_t l = (uint32_t)(lp / B);
+  const uint64_t p = lp - (uint64_t)l * B;
+  const int64_t c = coeffs[p * N + k];
+  const uint64_t q = (uint64_t)tp.lc[l].q;
+  uint64_t v;
+  if (c >= 0) {
+    v = (uint64_t)c % q;
+  } else {
+    // rem_euclid: |c| <= 2^63
+    const uint64_t m = (uint64_t)(-(c + 1)) + 1u;  // |c| without overflow
+    const uint64_t r = m % q;
+    v = r == 0 ? 0 : q - r;
+  }
+  dst[(uint64_t)l * ls + p * N + k] = (W)v;
+}
+
+template <class W>
+__global__ void __launch_bounds__(256)
+k_export(uint64_t* __restrict__ stage, const W* __restrict__ src, uint32_t log_n, uint32_t L,
+         uint64_t ls, int from_brv, uint64_t total) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const uint64_t N = 1ull << log_n;
+  const uint64_t k = gid & (N - 1);
+  const uint64_t pl = gid >> log_n;
+  const uint32_t l = (uint32_t)(pl % L);
+  const uint64_t p = pl / L;
+  const uint64_t pos = from_brv ? brv_dev(k, log_n) : k;
+  stage[gid] = (uint64_t)src[(uint64_t)l * ls + p * N + pos];
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+
+static inline unsigned grid_for(uint64_t total, unsigned block) {
+  return (unsigned)((total + block - 1) / block);
+}
+
+static inline int row_loge(const Geom& g) { return g.log_c >= 4 ? 4 : (int)g.log_c; }
+
+template <class W>
+static size_t row_lds_bytes(const Geom& g, int nops) {
+  const size_t T = g.c >> row_loge(g);
+  const size_t threads = T > (size_t)kRowThreads ? T : (size_t)kRowThreads;
+  const size_t rpw = threads / T;
+  return (size_t)nops * rpw * (g.c + g.c / 16) * sizeof(W);
+}
+
+static unsigned row_threads(const Geom& g) {
+  const size_t T = g.c >> row_loge(g);
+  return (unsigned)(T > (size_t)kRowThreads ? T : (size_t)kRowThreads);
+}
+
+template <class K>
+static hipError_t allow_lds(K kernel, size_t bytes) {
+  if (bytes <= 65536) return hipSuccess;
+  return hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes);
+}
+
+#define RNT_DISPATCH_LOGR(LOGR, MACRO) \
+  switch (LOGR) {                      \
+    case 0: MACRO(0); break;           \
+    case 1: MACRO(1); break;           \
+    case 2: MACRO(2); break;           \
+    case 3: MACRO(3); break;           \
+    case 4: MACRO(4); break;           \
+    default: return hipErrorInvalidValue; \
+  }
+
+template <class W>
+static hipError_t col_fwd_t(const Launch& k, void* out0, const void* in0, void* out1,
+                            const void* in1, uint64_t in_ls, uint64_t out_ls) {
+  const Geom g = geom_for(k.t->log_n);
+  const uint64_t total = (uint64_t)k.L * k.B * g.c;
+  const TabPtrs<W> tp = tab_ptrs<W>(k.t);
+  if (total == 0) return hipSuccess;
+#define RNT_L(R)                                                                              \
+  hipLaunchKernelGGL((k_col_fwd<W, R>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,      \
+                     (W*)out0, (const W*)in0, (W*)out1, (const W*)in1, tp, g.log_n, g.log_c, \
+                     (uint32_t)k.B, in_ls, out_ls, total)
+  RNT_DISPATCH_LOGR(g.log_r, RNT_L)
+#undef RNT_L
+  return hipGetLastError();
+}
+
+template <class W>
+static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const void* in,
+                            uint64_t in_ls, int rfold, const void* addend) {
+  const Geom g = geom_for(k.t->log_n);
+  const uint64_t total = (uint64_t)k.L * k.B * g.c;
+  const TabPtrs<W> tp = tab_ptrs<W>(k.t);
+  if (total == 0) return hipSuccess;
+#define RNT_L(R)                                                                          \
+  hipLaunchKernelGGL((k_col_inv<W, R>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,  \
+                     (W*)out, (const W*)in, (const W*)addend, tp, g.log_n, g.log_c,      \
+                     (uint32_t)k.B, in_ls, out_ls, total, rfold)
+  RNT_DISPATCH_LOGR(g.log_r, RNT_L)
+#undef RNT_L
+  return hipGetLastError();
+}
+
+#define RNT_DISPATCH_LOGE(LOGE, MACRO) \
+  switch (LOGE) {                      \
+    case 0: MACRO(0); break;           \
+    case 1: MACRO(1); break;           \
+    case 2: MACRO(2); break;           \
+    case 3: MACRO(3); break;           \
+    case 4: MACRO(4); break;           \
+    default: return hipErrorInvalidValue; \
+  }
+
+template <class W, int MODE, int LOGE>
+static hipError_t row_launch(const Launch& k, const Geom& g, void* x, const void* y,
+                             uint64_t ls) {
+  const uint64_t rows = (uint64_t)k.L * k.B * g.r;
+  if (rows == 0) return hipSuccess;
+  const unsigned threads = row_threads(g);
+  const uint64_t rpw = threads / (g.c >> LOGE);
+  const unsigned blocks = (unsigned)((rows + rpw - 1) / rpw);
+  const size_t lds = row_lds_bytes<W>(g, MODE == 2 ? 2 : 1);
+  hipError_t e = allow_lds(k_row<W, MODE, LOGE>, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_row<W, MODE, LOGE>), dim3(blocks), dim3(threads), lds, k.s, (W*)x,
+                     (const W*)y, tab_ptrs<W>(k.t), g.log_n, g.log_c, (uint32_t)k.B, ls, rows);
+  return hipGetLastError();
+}
+
+template <class W>
+static hipError_t row_t(const Launch& k, int mode, void* x, const void* y, uint64_t ls) {
+  const Geom g = geom_for(k.t->log_n);
+  const int loge = row_loge(g);
+#define RNT_L0(E) return row_launch<W, 0, E>(k, g, x, y, ls)
+#define RNT_L1(E) return row_launch<W, 1, E>(k, g, x, y, ls)
+#define RNT_L2(E) return row_launch<W, 2, E>(k, g, x, y, ls)
+  if (mode == 0) {
+    RNT_DISPATCH_LOGE(loge, RNT_L0)
+  } else if (mode == 1) {
+    RNT_DISPATCH_LOGE(loge, RNT_L1)
+  } else {
+    RNT_DISPATCH_LOGE(loge, RNT_L2)
+  }
+#undef RNT_L0
+#undef RNT_L1
+#undef RNT_L2
+  return hipErrorInvalidValue;
+}
+
+template <class W>
+static hipError_t elementwise_t(const Launch& k, int op, void* out, const void* a,
+                                const void* b) {
+  const uint64_t limb_words = (uint64_t)k.B << k.t->log_n;
+  const uint64_t total = limb_words * k.L;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_elementwise<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, (W*)out,
+                     (const W*)a, (const W*)b, op, tab_ptrs<W>(k.t), limb_words, total);
+  return hipGetLastError();
+}
+
+// k.L = limbs of the INPUT; output has k.L - 1.
+template <class W>
+static hipError_t rescale_t(const Launch& k, void* out, const void* in) {
+  const uint64_t pw = (uint64_t)k.B << k.t->log_n;
+  const uint64_t total = pw * (k.L - 1);
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_rescale<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, (W*)out,
+                     (const W*)in, tab_ptrs<W>(k.t), (uint32_t)(k.L - 1), pw, pw, pw, total);
+  return hipGetLastError();
+}
+
+static uint64_t inv_mod_pow2(uint64_t h, uint64_t M) {
+  // h odd, M power of two: Newton iteration for h^-1 mod 2^64, then mask.
+  uint64_t x = h;  // correct to 3 bits
+  for (int i = 0; i < 6; ++i) x *= 2 - h * x;
+  return x & (M - 1);
+}
+
+template <class W>
+static hipError_t automorphism_t(const Launch& k, void* out, const void* in, uint64_t g) {
+  const uint64_t N = 1ull << k.t->log_n;
+  const uint64_t two_n = 2 * N;
+  const uint64_t e = g % two_n;
+  const uint64_t pw = (uint64_t)k.B * N;
+  const uint64_t total = pw * k.L;
+  if (total == 0) return hipSuccess;
+  if (e & 1) {
+    const uint64_t ginv = inv_mod_pow2(e, two_n);
+    hipLaunchKernelGGL((k_automorph_odd<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,
+                       (W*)out, (const W*)in, tab_ptrs<W>(k.t), k.t->log_n, ginv, pw, total);
+  } else {
+    uint32_t ex = 0;
+    uint64_t h = e;
+    while ((h & 1) == 0) {
+      h >>= 1;
+      ++ex;
+    }
+    const uint64_t M = two_n >> ex;
+    const uint64_t hinv = inv_mod_pow2(h, M);
+    hipLaunchKernelGGL((k_automorph_even<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,
+                       (W*)out, (const W*)in, tab_ptrs<W>(k.t), k.t->log_n, ex, hinv, pw, total);
+  }
+  return hipGetLastError();
+}
+
+template <class W>
+static hipError_t import_t(const Launch& k, void* dst, const uint64_t* stage, int to_brv,
+                           unsigned long long* err) {
+  const uint64_t total = ((uint64_t)k.B * k.L) << k.t->log_n;
+  if (total == 0) return hipSuccess;
+  const uint64_t ls = (uint64_t)k.B << k.t->log_n;
+  hipLaunchKernelGGL((k_import<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, (W*)dst,
+                     stage, tab_ptrs<W>(k.t), k.t->log_n, (uint32_t)k.L, ls, to_brv, err, total);
+  return hipGetLastError();
+}
+
+template <class W>
+static hipError_t import_coeffs_t(const Launch& k, void* dst, const int64_t* stage) {
+  const uint64_t total = ((uint64_t)k.B * k.L) << k.t->log_n;
+  if (total == 0) return hipSuccess;
+  const uint64_t ls = (uint64_t)k.B << k.t->log_n;
+  hipLaunchKernelGGL((k_import_coeffs<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,
+                     (W*)dst, stage, tab_ptrs<W>(k.t), k.t->log_n, (uint32_t)k.L, (uint32_t)k.B,
+                     ls, total);
+  return hipGetLastError();
+}
+
+template <class W>
+static hipError_t export_t(const Launch& k, uint64_t* stage, const void* src, int from_brv) {
+  const uint64_t total = ((uint64_t)k.B * k.L) << k.t->log_n;
+  if (total == 0) return hipSuccess;
+  const uint64_t ls = (uint64_t)k.B << k.t->log_n;
+  hipLaunchKernelGGL((k_export<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, stage,
+                     (const W*)src, k.t->log_n, (uint32_t)k.L, ls, from_brv, total);
+  return hipGetLastError();
+}
+
+template <class W>
+static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64_t d_ls) {
+  const Geom g = geom_for(k.t->log_n);
+  const uint64_t total = (uint64_t)k.L * k.L * k.B * g.c;
+  if (total == 0) return hipSuccess;
+  const TabPtrs<W> tp = tab_ptrs<W>(k.t);
+#define RNT_L(R)                                                                               \
+  hipLaunchKernelGGL((k_ks_decompose<W, R>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,  \
+                     (W*)S, (const W*)d, tp, g.log_n, g.log_c, (uint32_t)k.L, (uint32_t)k.B, \
+                     d_ls, total)
+  RNT_DISPATCH_LOGR(g.log_r, RNT_L)
+#undef RNT_L
+  return hipGetLastError();
+}
+
+template <class W, int LOGE>
+static hipError_t ks_rows_launch(const Launch& k, const Geom& g, void* u0, void* u1,
+                                 uint64_t ls, const void* S, const void* key_a,
+                                 const void* key_b, uint64_t key_ls, const void* init0,
+                                 const void* init1, uint64_t init_ls) {
+  const uint64_t rows = (uint64_t)k.L * k.B * g.r;
+  if (rows == 0) return hipSuccess;
+  const unsigned threads = row_threads(g);
+  const uint64_t rpw = threads / (g.c >> LOGE);
+  const unsigned blocks = (unsigned)((rows + rpw - 1) / rpw);
+  const size_t lds = row_lds_bytes<W>(g, 2);
+  hipError_t e = allow_lds(k_ks_rows<W, LOGE>, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_ks_rows<W, LOGE>), dim3(blocks), dim3(threads), lds, k.s, (W*)u0,
+                     (W*)u1, (const W*)S, (const W*)key_a, (const W*)key_b, (uint64_t)key_ls,
+                     (const W*)init0, (const W*)init1, init_ls, tab_ptrs<W>(k.t), g.log_n, g.log_c,
+                     (uint32_t)k.L, (uint32_t)k.B, ls, rows);
+  return hipGetLastError();
+}
+
+template <class W>
+static hipError_t ks_rows_t(const Launch& k, void* u0, void* u1, uint64_t ls, const void* S,
+                            const void* key_a, const void* key_b, uint64_t key_ls,
+                            const void* init0, const void* init1, uint64_t init_ls) {
+  const Geom g = geom_for(k.t->log_n);
+#define RNT_L(E) \
+  return ks_rows_launch<W, E>(k, g, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls)
+  RNT_DISPATCH_LOGE(row_loge(g), RNT_L)
+#undef RNT_L
+  return hipErrorInvalidValue;
+}
+
+template <class W, int LOGE>
+static hipError_t tensor_rows_launch(const Launch& k, const Geom& g, void* d0hat, void* d1hat,
+                                     void* d2row, const void* c0, const void* c1,
+                                     const void* c0p, const void* c1p, uint64_t ls) {
+  const uint64_t rows = (uint64_t)k.L * k.B * g.r;
+  if (rows == 0) return hipSuccess;
+  const unsigned threads = row_threads(g);
+  const uint64_t rpw = threads / (g.c >> LOGE);
+  const unsigned blocks = (unsigned)((rows + rpw - 1) / rpw);
+  const size_t lds = row_lds_bytes<W>(g, 2);
+  hipError_t e = allow_lds(k_tensor_rows<W, LOGE>, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_tensor_rows<W, LOGE>), dim3(blocks), dim3(threads), lds, k.s,
+                     (W*)d0hat, (W*)d1hat, (W*)d2row, (const W*)c0, (const W*)c1,
+                     (const W*)c0p, (const W*)c1p, tab_ptrs<W>(k.t), g.log_n, g.log_c,
+                     (uint32_t)k.B, ls, rows);
+  return hipGetLastError();
+}
+
+template <class W>
+static hipError_t tensor_rows_t(const Launch& k, void* d0hat, void* d1hat, void* d2row,
+                                const void* c0, const void* c1, const void* c0p,
+                                const void* c1p, uint64_t ls) {
+  const Geom g = geom_for(k.t->log_n);
+#define RNT_L(E) \
+  return tensor_rows_launch<W, E>(k, g, d0hat, d1hat, d2row, c0, c1, c0p, c1p, ls)
+  RNT_DISPATCH_LOGE(row_loge(g), RNT_L)
+#undef RNT_L
+  return hipErrorInvalidValue;
+}
+
+// W dispatch -----------------------------------------------------------------
+#define RNT_WIDE(CALL32, CALL64) return k.t->wide ? (CALL64) : (CALL32)
+
+hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* out1,
+                          const void* in1, uint64_t in_ls, uint64_t out_ls) {
+  RNT_WIDE(col_fwd_t<uint32_t>(k, out0, in0, out1, in1, in_ls, out_ls),
+           col_fwd_t<uint64_t>(k, out0, in0, out1, in1, in_ls, out_ls));
+}
+hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls) {
+  RNT_WIDE(row_t<uint32_t>(k, mode, x, y, ls), row_t<uint64_t>(k, mode, x, y, ls));
+}
+hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
+                          uint64_t in_ls, int rfold, const void* addend) {
+  RNT_WIDE(col_inv_t<uint32_t>(k, out, out_ls, in, in_ls, rfold, addend),
+           col_inv_t<uint64_t>(k, out, out_ls, in, in_ls, rfold, addend));
+}
+hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a, const void* b) {
+  RNT_WIDE(elementwise_t<uint32_t>(k, op, out, a, b), elementwise_t<uint64_t>(k, op, out, a, b));
+}
+hipError_t launch_rescale(const Launch& k, void* out, const void* in) {
+  RNT_WIDE(rescale_t<uint32_t>(k, out, in), rescale_t<uint64_t>(k, out, in));
+}
+hipError_t launch_automorphism(const Launch& k, void* out, const void* in, uint64_t g) {
+  RNT_WIDE(automorphism_t<uint32_t>(k, out, in, g), automorphism_t<uint64_t>(k, out, in, g));
+}
+hipError_t launch_import(const Launch& k, void* dst, const uint64_t* stage, int to_brv,
+                         unsigned long long* err) {
+  RNT_WIDE(import_t<uint32_t>(k, dst, stage, to_brv, err),
+           import_t<uint64_t>(k, dst, stage, to_brv, err));
+}
+hipError_t launch_import_coeffs(const Launch& k, void* dst, const int64_t* stage) {
+  RNT_WIDE(import_coeffs_t<uint32_t>(k, dst, stage), import_coeffs_t<uint64_t>(k, dst, stage));
+}
+hipError_t launch_export(const Launch& k, uint64_t* stage, const void* src, int from_brv) {
+  RNT_WIDE(export_t<uint32_t>(k, stage, src, from_brv),
+           export_t<uint64_t>(k, stage, src, from_brv));
+}
+hipError_t launch_ks_decompose(const Launch& k, void* S, const void* d, uint64_t d_ls) {
+  RNT_WIDE(ks_decompose_t<uint32_t>(k, S, d, d_ls), ks_decompose_t<uint64_t>(k, S, d, d_ls));
+}
+hipError_t launch_ks_rows(const Launch& k, void* u0, void* u1, uint64_t u_ls, const void* S,
+                          const void* key_a, const void* key_b, uint64_t key_ls,
+                          const void* init0, const void* init1, uint64_t init_ls) {
+  RNT_WIDE(ks_rows_t<uint32_t>(k, u0, u1, u_ls, S, key_a, key_b, key_ls, init0, init1, init_ls),
+           ks_rows_t<uint64_t>(k, u0, u1, u_ls, S, key_a, key_b, key_ls, init0, init1, init_ls));
+}
+hipError_t launch_tensor_rows(const Launch& k, void* d0hat, void* d1hat, void* d2row,
+                              const void* c0, const void* c1, const void* c0p, const void* c1p,
+                              uint64_t ls) {
+  RNT_WIDE(tensor_rows_t<uint32_t>(k, d0hat, d1hat, d2row, c0, c1, c0p, c1p, ls),
+           tensor_rows_t<uint64_t>(k, d0hat, d1hat, d2row, c0, c1, c0p, c1p, ls));
+}
+
+}  // namespace rnt

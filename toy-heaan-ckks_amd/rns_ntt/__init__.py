@@ -1,0 +1,427 @@
+"""Host-side mirror of oiwn/toy-heaan-ckks's RNS-NTT ring interface over the
+MI355X C-ABI (include/rnsntt.h).
+
+Names, argument meaning and error behaviour follow the reference:
+
+* :class:`RnsBasis`  -- ``RnsBasis<N>`` (src/rings/backends/rns_ntt/basis.rs:90-180)
+* :class:`RnsPoly`   -- ``RnsPoly<N>`` (src/rings/backends/rns_ntt/poly.rs:25-570);
+  one object holds a *batch* of ``n_polys`` polynomials that every op
+  processes together (``n_polys=1`` is the reference's single polynomial).
+* :func:`mul_ciphertexts_gadget`, :func:`rotate_ciphertext`,
+  :func:`rescale_ciphertext` -- ``CkksEngine`` (src/crypto/engine.rs:263-539).
+* :class:`RnsNttError` -- ``RnsNttError`` (errors.rs:4-20), raised with the
+  same variant name.
+
+All arithmetic runs in librnsntt.so on the GPU.  Host code here only moves
+data across the boundary (``from_channels`` / ``channels``) and does the
+reference's decode-side u128 CRT in :meth:`RnsPoly.to_coeffs`.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import RnsNttError, check, load
+
+__all__ = [
+    "device_count",
+    "RnsNttError",
+    "RnsBasis",
+    "RnsPoly",
+    "RnsGadgetKey",
+    "Ciphertext",
+    "generate_primes",
+    "is_ntt_friendly_prime",
+    "find_psi",
+    "keyswitch",
+    "mul_ciphertexts_gadget",
+    "rotate_ciphertext",
+    "rescale_ciphertext",
+]
+
+
+def _u64p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))
+
+
+def _i64p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+
+
+# ---------------------------------------------------------------------------
+# host-side number theory (setup)
+# ---------------------------------------------------------------------------
+
+
+def device_count() -> int:
+    """Visible HIP devices (0 on a CPU-only host)."""
+    r = ctypes.c_int(0)
+    check(load().rnt_device_count(ctypes.byref(r)))
+    return int(r.value)
+
+
+def generate_primes(bit_size: int, count: int, degree: int) -> list[int]:
+    """src/math/utils.rs:47-80."""
+    out = np.zeros(max(count, 1), dtype=np.uint64)
+    check(load().rnt_generate_primes(bit_size, count, degree, _u64p(out)))
+    return [int(x) for x in out[:count]]
+
+
+def is_ntt_friendly_prime(p: int, n: int) -> bool:
+    """src/math/primes.rs:125-131."""
+    r = ctypes.c_int(0)
+    check(load().rnt_is_ntt_friendly_prime(p, n, ctypes.byref(r)))
+    return bool(r.value)
+
+
+def find_psi(modulus: int, degree: int) -> int:
+    """psi of NttTable::new (basis.rs:39-40, 217-237)."""
+    r = ctypes.c_uint64(0)
+    check(load().rnt_find_psi(modulus, degree, ctypes.byref(r)))
+    return int(r.value)
+
+
+# ---------------------------------------------------------------------------
+# RnsBasis
+# ---------------------------------------------------------------------------
+
+
+class RnsBasis:
+    """``Arc<RnsBasis<N>>``: an immutable RNS basis with device NTT tables.
+
+    ``RnsBasis(moduli, degree)`` validates like ``RnsBasis::new``
+    (basis.rs:97-106): ``EmptyBasis`` for no moduli, ``InvalidDegree`` for a
+    non power-of-two degree, ``NonNttFriendlyModulus`` otherwise.
+    """
+
+    def __init__(self, moduli: Sequence[int], degree: int, device: int = 0):
+        lib = load()
+        if degree <= 0 or degree & (degree - 1):
+            raise RnsNttError(_lib.INVALID_DEGREE, f"ring degree must be a power of two, got {degree}")
+        log_n = degree.bit_length() - 1
+        arr = np.ascontiguousarray(np.array(list(moduli), dtype=np.uint64)) if len(moduli) else np.zeros(1, np.uint64)
+        h = ctypes.c_void_p()
+        check(lib.rnt_ctx_create(log_n, _u64p(arr), len(moduli), device, ctypes.byref(h)))
+        self._h = h
+        self._parent = None
+        self.degree = degree
+        self.device = device
+
+    @classmethod
+    def _from_handle(cls, h, parent: "RnsBasis") -> "RnsBasis":
+        self = cls.__new__(cls)
+        self._h = h
+        self._parent = parent  # keeps the shared tables' owner reachable
+        self.degree = parent.degree
+        self.device = parent.device
+        return self
+
+    @property
+    def handle(self):
+        return self._h
+
+    def moduli(self) -> list[int]:
+        out = np.zeros(self.channel_count(), dtype=np.uint64)
+        check(load().rnt_ctx_moduli(self._h, _u64p(out)))
+        return [int(x) for x in out]
+
+    def channel_count(self) -> int:
+        r = ctypes.c_size_t(0)
+        check(load().rnt_ctx_channel_count(self._h, ctypes.byref(r)))
+        return int(r.value)
+
+    def drop_last(self, drop_count: int) -> "RnsBasis":
+        """basis.rs:121-134 (a view sharing the device tables)."""
+        h = ctypes.c_void_p()
+        check(load().rnt_ctx_drop_last(self._h, drop_count, ctypes.byref(h)))
+        return RnsBasis._from_handle(h, self)
+
+    def total_bits(self) -> int:
+        r = ctypes.c_uint32(0)
+        check(load().rnt_ctx_total_bits(self._h, ctypes.byref(r)))
+        return int(r.value)
+
+    def psi(self, limb: int) -> int:
+        r = ctypes.c_uint64(0)
+        check(load().rnt_ctx_psi(self._h, limb, ctypes.byref(r)))
+        return int(r.value)
+
+    def stream(self) -> int:
+        r = ctypes.c_void_p()
+        check(load().rnt_ctx_stream(self._h, ctypes.byref(r)))
+        return int(r.value or 0)
+
+    def sync(self) -> None:
+        check(load().rnt_sync(self._h))
+
+    def profile_enable(self, enable: bool = True) -> None:
+        """Bracket every kernel launched on this basis' stream with HIP events."""
+        check(load().rnt_profile_enable(self._h, 1 if enable else 0))
+
+    def profile_read(self, kernel: str) -> tuple[int, float]:
+        """(launches, summed device ms) for one kernel since profile_enable."""
+        n = ctypes.c_uint64(0)
+        ms = ctypes.c_double(0)
+        check(load().rnt_profile_read(self._h, kernel.encode(), ctypes.byref(n), ctypes.byref(ms)))
+        return int(n.value), float(ms.value)
+
+    def reconstruct_centered_coeff(self, residues: Sequence[int]) -> int:
+        """basis.rs:158-180 (host-side decode; the reference needs Q < 2^128)."""
+        mods = self.moduli()
+        Q = 1
+        for m in mods:
+            Q *= m
+        if Q >= 1 << 128:
+            raise OverflowError("reconstruct_centered_coeff requires Q < 2^128 (basis.rs:152-157)")
+        acc = 0
+        for r, m in zip(residues, mods):
+            qi = Q // m
+            acc = (acc + (int(r) * pow(qi % m, -1, m) % m) * qi) % Q
+        return acc - Q if acc > Q // 2 else acc
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.rnt_ctx_destroy(h)
+            self._h = None
+
+
+# ---------------------------------------------------------------------------
+# RnsPoly
+# ---------------------------------------------------------------------------
+
+
+class RnsPoly:
+    """A batch of ``n_polys`` polynomials in Z_{q_0} x ... x Z_{q_{L-1}}[X]/(X^N+1).
+
+    Mirrors ``RnsPoly<N>`` (poly.rs:25-570).  Operators follow the Rust ones:
+    ``a *= b`` (MulAssign), ``a += b`` (AddAssign), ``-a`` (Neg).
+    """
+
+    def __init__(self, basis: RnsBasis, n_polys: int = 1):
+        lib = load()
+        h = ctypes.c_void_p()
+        check(lib.rnt_buf_alloc(basis.handle, n_polys, ctypes.byref(h)))
+        self._h = h
+        self.basis = basis
+        self.n_polys = n_polys
+
+    # -- constructors (poly.rs:34-114) --------------------------------------
+    @classmethod
+    def zero(cls, basis: RnsBasis, n_polys: int = 1) -> "RnsPoly":
+        return cls(basis, n_polys)
+
+    @classmethod
+    def from_coeffs(cls, coeffs, basis: RnsBasis) -> "RnsPoly":
+        """poly.rs:49-67; ``coeffs`` is [N] or [B][N] signed integers."""
+        c = np.asarray(coeffs, dtype=np.int64)
+        if c.ndim == 1:
+            c = c[None, :]
+        if c.shape[1] < basis.degree:
+            raise ValueError(f"from_coeffs: need at least {basis.degree} coefficients, got {c.shape[1]}")
+        c = np.ascontiguousarray(c[:, : basis.degree])
+        p = cls(basis, c.shape[0])
+        check(load().rnt_upload_coeffs(p._h, _i64p(c), c.shape[0]))
+        return p
+
+    @classmethod
+    def from_channels(cls, channels, basis: RnsBasis, in_ntt_domain: bool = False) -> "RnsPoly":
+        """poly.rs:73-99; ``channels`` is [L][N] or [B][L][N] residues.
+
+        Raises ChannelCountMismatch / NonReducedCoefficient like the reference.
+        """
+        ch = np.asarray(channels, dtype=np.uint64)
+        if ch.ndim == 2:
+            ch = ch[None, :, :]
+        if ch.ndim != 3 or ch.shape[2] != basis.degree:
+            raise ValueError("from_channels: expected [L][N] or [B][L][N] with N == degree")
+        ch = np.ascontiguousarray(ch)
+        p = cls(basis, ch.shape[0])
+        check(load().rnt_upload(p._h, _u64p(ch), ch.shape[0], ch.shape[1], 1 if in_ntt_domain else 0))
+        return p
+
+    # -- accessors (poly.rs:118-129) ----------------------------------------
+    @property
+    def handle(self):
+        return self._h
+
+    def channels(self) -> np.ndarray:
+        """[L][N] for a single polynomial, [B][L][N] for a batch."""
+        out = np.zeros((self.n_polys, self.basis.channel_count(), self.basis.degree), dtype=np.uint64)
+        check(load().rnt_download(self._h, _u64p(out), self.n_polys))
+        return out[0] if self.n_polys == 1 else out
+
+    def is_ntt_domain(self) -> bool:
+        r = ctypes.c_int(0)
+        check(load().rnt_buf_is_ntt(self._h, ctypes.byref(r)))
+        return bool(r.value)
+
+    def clone(self) -> "RnsPoly":
+        p = RnsPoly(self.basis, self.n_polys)
+        check(load().rnt_copy(p._h, self._h))
+        return p
+
+    # -- domain conversion (poly.rs:136-166) --------------------------------
+    def to_ntt_domain(self) -> None:
+        check(load().rnt_ntt_fwd(self._h))
+
+    def to_coeff_domain(self) -> None:
+        check(load().rnt_ntt_inv(self._h))
+
+    # -- arithmetic (poly.rs:254-385) ---------------------------------------
+    def __imul__(self, rhs: "RnsPoly") -> "RnsPoly":
+        check(load().rnt_mul(self._h, self._h, rhs._h))
+        return self
+
+    def __iadd__(self, rhs: "RnsPoly") -> "RnsPoly":
+        check(load().rnt_add(self._h, self._h, rhs._h))
+        return self
+
+    def __isub__(self, rhs: "RnsPoly") -> "RnsPoly":
+        check(load().rnt_sub(self._h, self._h, rhs._h))
+        return self
+
+    def __mul__(self, rhs: "RnsPoly") -> "RnsPoly":
+        out = RnsPoly(self.basis, self.n_polys)
+        check(load().rnt_mul(out._h, self._h, rhs._h))
+        return out
+
+    def __add__(self, rhs: "RnsPoly") -> "RnsPoly":
+        out = RnsPoly(self.basis, self.n_polys)
+        check(load().rnt_add(out._h, self._h, rhs._h))
+        return out
+
+    def __neg__(self) -> "RnsPoly":
+        out = RnsPoly(self.basis, self.n_polys)
+        check(load().rnt_neg(out._h, self._h))
+        return out
+
+    # -- rescale / mod-drop (poly.rs:168-249) -------------------------------
+    def rescale_into(self, new_basis: RnsBasis) -> "RnsPoly":
+        out = RnsPoly(new_basis, self.n_polys)
+        check(load().rnt_rescale(out._h, self._h))
+        return out
+
+    def rescale(self) -> "RnsPoly":
+        if self.basis.channel_count() < 2:
+            raise RnsNttError(_lib.INVALID_MOD_DROP,
+                              f"invalid mod-drop count 1 for {self.basis.channel_count()} channels")
+        return self.rescale_into(self.basis.drop_last(1))
+
+    def mod_drop_last(self, drop_count: int) -> "RnsPoly":
+        nb = self.basis.drop_last(drop_count)
+        out = RnsPoly(nb, self.n_polys)
+        check(load().rnt_mod_drop_last(out._h, self._h))
+        return out
+
+    # -- automorphisms (poly.rs:482-570) ------------------------------------
+    def automorphism(self, exponent: int) -> "RnsPoly":
+        out = RnsPoly(self.basis, self.n_polys)
+        check(load().rnt_automorphism(out._h, self._h, exponent))
+        return out
+
+    def rotate_slots(self, k: int) -> "RnsPoly":
+        out = RnsPoly(self.basis, self.n_polys)
+        check(load().rnt_rotate_slots(out._h, self._h, k))
+        return out
+
+    # -- PolyRing::to_coeffs (poly.rs:404-427) ------------------------------
+    def to_coeffs(self) -> np.ndarray:
+        """Centered CRT of each coefficient (host u128 decode, Q < 2^128)."""
+        tmp = self
+        if self.is_ntt_domain():
+            tmp = self.clone()
+            tmp.to_coeff_domain()
+        ch = tmp.channels()
+        if ch.ndim == 2:
+            ch = ch[None]
+        out = np.zeros((ch.shape[0], ch.shape[2]), dtype=object)
+        for b in range(ch.shape[0]):
+            for i in range(ch.shape[2]):
+                out[b, i] = self.basis.reconstruct_centered_coeff([int(v) for v in ch[b, :, i]])
+        out = out.astype(np.int64)
+        return out[0] if self.n_polys == 1 else out
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.rnt_buf_free(h)
+            self._h = None
+
+
+# ---------------------------------------------------------------------------
+# engine-level ops (src/crypto/engine.rs)
+# ---------------------------------------------------------------------------
+
+
+class RnsGadgetKey:
+    """RnsGadgetRelinKey / RnsGadgetRotationKey (engine.rs:224-253).
+
+    ``a`` and ``b`` are RnsPoly batches holding the L key polynomials; they
+    are made NTT-resident once by :meth:`prepare`.
+    """
+
+    def __init__(self, a: RnsPoly, b: RnsPoly, rotation: Optional[int] = None):
+        self.a = a
+        self.b = b
+        self.rotation = rotation
+        check(load().rnt_key_prepare(a.handle, b.handle))
+
+    @classmethod
+    def from_channels(cls, a_channels, b_channels, basis: RnsBasis, rotation: Optional[int] = None):
+        """a_channels / b_channels: [L][L][N] coefficient-domain residues."""
+        return cls(RnsPoly.from_channels(a_channels, basis), RnsPoly.from_channels(b_channels, basis), rotation)
+
+
+@dataclass
+class Ciphertext:
+    """types.rs:27-35."""
+
+    c0: RnsPoly
+    c1: RnsPoly
+    logp: int = 0
+    logq: int = 0
+
+
+def keyswitch(d: RnsPoly, key: RnsGadgetKey) -> tuple[RnsPoly, RnsPoly]:
+    """Gadget sum (engine.rs:505-528 / 429-452) on a coefficient-domain batch."""
+    acc0 = RnsPoly(d.basis, d.n_polys)
+    acc1 = RnsPoly(d.basis, d.n_polys)
+    check(load().rnt_keyswitch(acc0.handle, acc1.handle, d.handle, key.a.handle, key.b.handle))
+    return acc0, acc1
+
+
+def mul_ciphertexts_gadget(ct1: Ciphertext, ct2: Ciphertext, rlk: RnsGadgetKey) -> Ciphertext:
+    """engine.rs:473-539."""
+    assert ct1.logq == ct2.logq, "logq mismatch in gadget multiplication"
+    basis = ct1.c0.basis
+    out0 = RnsPoly(basis, ct1.c0.n_polys)
+    out1 = RnsPoly(basis, ct1.c0.n_polys)
+    check(load().rnt_ct_mul_relin(out0.handle, out1.handle, ct1.c0.handle, ct1.c1.handle,
+                                  ct2.c0.handle, ct2.c1.handle, rlk.a.handle, rlk.b.handle))
+    return Ciphertext(out0, out1, ct1.logp + ct2.logp, ct1.logq)
+
+
+def rotate_ciphertext(ct: Ciphertext, rotk: RnsGadgetKey) -> Ciphertext:
+    """engine.rs:412-463."""
+    basis = ct.c0.basis
+    out0 = RnsPoly(basis, ct.c0.n_polys)
+    out1 = RnsPoly(basis, ct.c0.n_polys)
+    check(load().rnt_ct_rotate(out0.handle, out1.handle, ct.c0.handle, ct.c1.handle,
+                               int(rotk.rotation or 0), rotk.a.handle, rotk.b.handle))
+    return Ciphertext(out0, out1, ct.logp, ct.logq)
+
+
+def rescale_ciphertext(ct: Ciphertext) -> Ciphertext:
+    """engine.rs:263-282: both components onto one shared dropped basis."""
+    q_last = ct.c0.basis.moduli()[-1]
+    bits_dropped = q_last.bit_length()
+    new_basis = ct.c0.basis.drop_last(1)
+    out0 = RnsPoly(new_basis, ct.c0.n_polys)
+    out1 = RnsPoly(new_basis, ct.c0.n_polys)
+    check(load().rnt_ct_rescale(out0.handle, out1.handle, ct.c0.handle, ct.c1.handle))
+    return Ciphertext(out0, out1, ct.logp - bits_dropped, ct.logq - bits_dropped)
