@@ -92,6 +92,8 @@ int rnt_find_psi(uint64_t modulus, uint64_t degree, uint64_t* psi);
  * validates like the reference, builds the device tables on `device`. */
 int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t count,
                    int device, rnt_ctx** out);
+/* Releases the caller's handle; like dropping an Arc, the context (and its
+ * device tables) stays alive until every buffer allocated on it is freed. */
 int rnt_ctx_destroy(rnt_ctx* ctx);
 /* RnsBasis::drop_last (basis.rs:121-134): a prefix view sharing the
  * parent's device tables (no table copy). */

@@ -16,7 +16,7 @@ step() {  # step <name> <seconds> <cmd...>
   fi
   return 0
 }
-step mulrate 120 ./tools/bin/mulrate
+#step mulrate 120 ./tools/bin/mulrate
 step pytest_gpu 1200 python -m pytest tests -m gpu -x -q
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 10 --warmup 2

@@ -383,8 +383,12 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
   }
 }
 
+static void ctx_release(const rnt_ctx* ctx) {
+  if (ctx && const_cast<rnt_ctx*>(ctx)->refs.fetch_sub(1) == 1) delete ctx;
+}
+
 extern "C" int rnt_ctx_destroy(rnt_ctx* ctx) {
-  delete ctx;  // the tables live on while any view or buffer context holds them
+  ctx_release(ctx);  // freed once its last buffer is freed too
   return RNT_OK;
 }
 
@@ -460,10 +464,12 @@ extern "C" int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out) 
     return fail(RNT_ERR_OUT_OF_MEMORY, "host allocation failed");
   }
   b->ctx = ctx;
+  const_cast<rnt_ctx*>(ctx)->refs.fetch_add(1);
   b->n_polys = n_polys;
   const size_t bytes = poly_words(b) * word_bytes(ctx->t.get());
   hipError_t e = hipMalloc(&b->data, bytes);
   if (e != hipSuccess) {
+    ctx_release(ctx);
     delete b;
     return hip_fail(e, "hipMalloc(buffer)");
   }
@@ -471,6 +477,7 @@ extern "C" int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out) 
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->t->stream);
   if (e != hipSuccess) {
     (void)hipFree(b->data);
+    ctx_release(ctx);
     delete b;
     return hip_fail(e, "hipMemset(buffer)");
   }
@@ -487,6 +494,7 @@ extern "C" int rnt_buf_free(rnt_buf* b) {
   (void)hipFree(b->data);
   (void)hipFree(b->ws);
   (void)hipFree(b->stage);
+  ctx_release(b->ctx);
   delete b;
   return RNT_OK;
 }

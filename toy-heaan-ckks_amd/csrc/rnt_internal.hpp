@@ -91,9 +91,13 @@ struct Prof {
 
 }  // namespace rnt
 
+// Arc<RnsBasis> semantics: a context lives until rnt_ctx_destroy has been
+// called AND every buffer allocated on it has been freed, so handles may be
+// released in any order (e.g. by a garbage collector).
 struct rnt_ctx {
   std::shared_ptr<rnt::Tables> t;
   size_t L = 0;  // channel count of this (possibly dropped) basis
+  std::atomic<long> refs{1};  // 1 for the creator + 1 per live buffer
 };
 
 struct rnt_buf {
