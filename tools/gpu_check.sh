@@ -1,22 +1,27 @@
 #!/bin/bash
-# One gpurun call: microbench, GPU parity tests, smoke, short bench.
-# Every GPU step has its own time limit; a fault/abort/timeout stops the
-# script (exit codes >= 124 or signals), plain test failures do not.
+# One gpurun call: GPU parity tests, smoke, short bench, rocprofv3 kernel
+# trace.  Every GPU step has its own time limit; a fault/abort/timeout stops
+# the script, plain test failures do not.
 mkdir -p gpurun_out
+export TMPDIR=/tmp
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 step() {  # step <name> <seconds> <cmd...>
   local name=$1 secs=$2; shift 2
   echo "== $name" >&2
   timeout -k 10 "$secs" "$@" > "gpurun_out/$name.out" 2> "gpurun_out/$name.err"
   local rc=$?
   echo "== $name rc=$rc" >&2
-  tail -5 "gpurun_out/$name.out" >&2
+  tail -3 "gpurun_out/$name.out" >&2
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
     echo "stopping after $name (rc=$rc)" >&2
+    tail -20 "gpurun_out/$name.err" >&2
     exit $rc
   fi
   return 0
 }
-#step mulrate 120 ./tools/bin/mulrate
 step pytest_gpu 1200 python -m pytest tests -m gpu -x -q
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py --steps 10 --warmup 2
+step bench 600 python bench.py --steps 20 --warmup 3
+if [ "${PROFILE:-1}" = "1" ]; then
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof" -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
+fi

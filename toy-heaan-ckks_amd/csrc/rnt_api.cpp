@@ -171,9 +171,7 @@ rnt::Tables::~Tables() {
     (void)hipStreamDestroy(stream);
   }
   (void)hipFree(tw_fwd);
-  (void)hipFree(tw_fwd_p);
   (void)hipFree(tw_inv);
-  (void)hipFree(tw_inv_p);
   (void)hipFree(lconst);
   (void)hipFree(resc);
   (void)hipFree(resc_p);
@@ -252,7 +250,7 @@ int build_tables(rnt::Tables* t) {
   using namespace rnt::host;
   const size_t n = t->n, L = t->L;
   const unsigned wbits = sizeof(W) * 8;
-  std::vector<W> tw(L * n), twp(L * n), itw(L * n), itwp(L * n);
+  std::vector<rnt::Tw<W>> tw(L * n), itw(L * n);
   std::vector<rnt::LimbConst<W>> lc(L);
   std::vector<W> resc(L * L, 0), rescp(L * L, 0);
   std::vector<uint64_t> pw(n), ipw(n);
@@ -269,20 +267,14 @@ int build_tables(rnt::Tables* t) {
       a = mulmod(a, psi, q);
       b = mulmod(b, psi_inv, q);
     }
-    W* T = tw.data() + l * n;
-    W* TP = twp.data() + l * n;
-    W* I = itw.data() + l * n;
-    W* IP = itwp.data() + l * n;
-    T[0] = 1;
-    I[0] = 1;
-    TP[0] = (W)shoup_companion(1, q, wbits);
-    IP[0] = TP[0];
+    rnt::Tw<W>* T = tw.data() + l * n;
+    rnt::Tw<W>* I = itw.data() + l * n;
+    T[0] = {(W)1, (W)shoup_companion(1, q, wbits)};
+    I[0] = T[0];
     for (size_t g = 1; g < n; ++g) {
       const uint64_t e = brv(g, t->log_n);
-      T[g] = (W)pw[e];
-      I[g] = (W)ipw[e];
-      TP[g] = (W)shoup_companion(pw[e], q, wbits);
-      IP[g] = (W)shoup_companion(ipw[e], q, wbits);
+      T[g] = {(W)pw[e], (W)shoup_companion(pw[e], q, wbits)};
+      I[g] = {(W)ipw[e], (W)shoup_companion(ipw[e], q, wbits)};
     }
     rnt::LimbConst<W>& c = lc[l];
     c.q = (W)q;
@@ -292,7 +284,7 @@ int build_tables(rnt::Tables* t) {
     c.rmod = (W)r;
     c.rmod_p = (W)shoup_companion(r, q, wbits);
     const uint64_t ninv = invmod(n % q, q);
-    const uint64_t w1 = n > 1 ? (uint64_t)I[1] : 1;
+    const uint64_t w1 = n > 1 ? (uint64_t)I[1].w : 1;
     c.c1 = (W)ninv;
     c.c1_p = (W)shoup_companion(ninv, q, wbits);
     c.c2 = (W)mulmod(w1, ninv, q);
@@ -311,18 +303,14 @@ int build_tables(rnt::Tables* t) {
       rescp[l * L + i] = (W)shoup_companion(inv, qi, wbits);
     }
   }
-  const size_t tb = L * n * sizeof(W);
+  const size_t tb = L * n * sizeof(rnt::Tw<W>);
   HIP_TRY(hipMalloc(&t->tw_fwd, tb), "hipMalloc(tables)");
-  HIP_TRY(hipMalloc(&t->tw_fwd_p, tb), "hipMalloc(tables)");
   HIP_TRY(hipMalloc(&t->tw_inv, tb), "hipMalloc(tables)");
-  HIP_TRY(hipMalloc(&t->tw_inv_p, tb), "hipMalloc(tables)");
   HIP_TRY(hipMalloc(&t->lconst, L * sizeof(rnt::LimbConst<W>)), "hipMalloc(tables)");
   HIP_TRY(hipMalloc(&t->resc, L * L * sizeof(W)), "hipMalloc(tables)");
   HIP_TRY(hipMalloc(&t->resc_p, L * L * sizeof(W)), "hipMalloc(tables)");
   HIP_TRY(hipMemcpy(t->tw_fwd, tw.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
-  HIP_TRY(hipMemcpy(t->tw_fwd_p, twp.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
   HIP_TRY(hipMemcpy(t->tw_inv, itw.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
-  HIP_TRY(hipMemcpy(t->tw_inv_p, itwp.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
   HIP_TRY(hipMemcpy(t->lconst, lc.data(), L * sizeof(rnt::LimbConst<W>), hipMemcpyHostToDevice),
           "hipMemcpy");
   HIP_TRY(hipMemcpy(t->resc, resc.data(), L * L * sizeof(W), hipMemcpyHostToDevice), "hipMemcpy");

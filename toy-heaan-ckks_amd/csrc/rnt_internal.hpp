@@ -48,6 +48,13 @@ struct LimbConst {
   W c2r_p;
 };
 
+// A twiddle and its Shoup companion, interleaved so one load fetches both.
+template <class W>
+struct alignas(2 * sizeof(W)) Tw {
+  W w;  // psi^{+-brv(g)} mod q
+  W p;  // floor(w * 2^w / q)
+};
+
 // Shared, immutable device tables of a root basis.  drop_last views hold a
 // shared_ptr to the same tables (no copy, unlike basis.rs:130-133).
 struct Tables {
@@ -58,10 +65,8 @@ struct Tables {
   size_t L = 0;            // channel count of the root basis
   std::vector<uint64_t> moduli;
   std::vector<uint64_t> psi;
-  void* tw_fwd = nullptr;   // [L][N] psi^{brv(g)}, heap order, g in [1, N)
-  void* tw_fwd_p = nullptr; // Shoup companions
-  void* tw_inv = nullptr;   // [L][N] psi^{-brv(g)}
-  void* tw_inv_p = nullptr;
+  void* tw_fwd = nullptr;   // [L][N] Tw<W>{psi^{brv(g)}, companion}, heap order g in [1, N)
+  void* tw_inv = nullptr;   // [L][N] Tw<W>{psi^{-brv(g)}, companion}
   void* lconst = nullptr;   // [L] LimbConst<W>
   void* resc = nullptr;     // [L][L]: resc[l][i] = (q_l mod q_i)^-1 mod q_i, i < l
   void* resc_p = nullptr;   // [L][L] Shoup companions

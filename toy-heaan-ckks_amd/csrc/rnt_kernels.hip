@@ -15,6 +15,8 @@
 // bit-reversed order; inverse is the matching Gentleman-Sande network with
 // n^-1 folded into its last stage.  Values equal the reference's
 // a(psi^(2k+1)) exactly; only the order is private.
+// Twiddles are stored interleaved with their Shoup companions ({w, w'}
+// pairs) so one 8-byte load fetches both.
 //
 // Decomposition N = R * C (see rnt_internal.hpp):
 //   column pass: stages with distance >= C, one column (stride C) per
@@ -22,6 +24,9 @@
 //   row pass:    stages with distance < C, one row of C contiguous words per
 //                C/16 threads, radix-16 register passes, LDS exchanges with a
 //                1-in-16 pad (conflict-free for every pass distribution).
+//                The row geometry is a template (RowGeo<LOG_C>): pass bit
+//                ranges, LDS offsets and twiddle-subtree shapes are all
+//                compile-time, so only one base address per thread is live.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -33,10 +38,8 @@ namespace rnt {
 
 template <class W>
 struct TabPtrs {
-  const W* tw;
-  const W* twp;
-  const W* itw;
-  const W* itwp;
+  const Tw<W>* tw;   // [L][N] forward {w, w'}
+  const Tw<W>* itw;  // [L][N] inverse {w, w'}
   const LimbConst<W>* lc;
   const W* resc;
   const W* rescp;
@@ -46,10 +49,8 @@ struct TabPtrs {
 template <class W>
 static TabPtrs<W> tab_ptrs(const Tables* t) {
   TabPtrs<W> p;
-  p.tw = (const W*)t->tw_fwd;
-  p.twp = (const W*)t->tw_fwd_p;
-  p.itw = (const W*)t->tw_inv;
-  p.itwp = (const W*)t->tw_inv_p;
+  p.tw = (const Tw<W>*)t->tw_fwd;
+  p.itw = (const Tw<W>*)t->tw_inv;
   p.lc = (const LimbConst<W>*)t->lconst;
   p.resc = (const W*)t->resc;
   p.rescp = (const W*)t->resc_p;
@@ -81,7 +82,7 @@ Geom geom_for(uint32_t log_n) {
 // ---------------------------------------------------------------------------
 
 template <class W, int LOG_R>
-__device__ __forceinline__ void col_ct(W (&x)[1 << LOG_R], const W* tw, const W* twp, W q) {
+__device__ __forceinline__ void col_ct(W (&x)[1 << LOG_R], const Tw<W>* tw, W q) {
   constexpr int R = 1 << LOG_R;
 #pragma unroll
   for (int k = 0; k < LOG_R; ++k) {
@@ -89,8 +90,8 @@ __device__ __forceinline__ void col_ct(W (&x)[1 << LOG_R], const W* tw, const W*
 #pragma unroll
     for (int i = 0; i < R; ++i) {
       if (i & d) continue;
-      const int node = (1 << k) + (i >> (LOG_R - k));
-      ct_bfly<W>(x[i], x[i + d], tw[node], twp[node], q);
+      const Tw<W> t = tw[(1 << k) + (i >> (LOG_R - k))];
+      ct_bfly<W>(x[i], x[i + d], t.w, t.p, q);
     }
   }
 }
@@ -98,8 +99,8 @@ __device__ __forceinline__ void col_ct(W (&x)[1 << LOG_R], const W* tw, const W*
 // x <- GS network over the column with the last (distance N/2) stage scaled
 // by c1 (upper) and c2 (lower).
 template <class W, int LOG_R>
-__device__ __forceinline__ void col_gs(W (&x)[1 << LOG_R], const W* itw, const W* itwp, W q, W c1,
-                                       W c1p, W c2, W c2p) {
+__device__ __forceinline__ void col_gs(W (&x)[1 << LOG_R], const Tw<W>* itw, W q, W c1, W c1p,
+                                       W c2, W c2p) {
   constexpr int R = 1 << LOG_R;
 #pragma unroll
   for (int sl = 0; sl < LOG_R; ++sl) {
@@ -112,8 +113,8 @@ __device__ __forceinline__ void col_gs(W (&x)[1 << LOG_R], const W* itw, const W
         x[i] = shoup_mul<W>(u + v, c1, c1p, q);
         x[i + d] = shoup_mul<W>(u - v + q, c2, c2p, q);
       } else {
-        const int node = (1 << (LOG_R - 1 - sl)) + (i >> (sl + 1));
-        gs_bfly<W>(x[i], x[i + d], itw[node], itwp[node], q);
+        const Tw<W> t = itw[(1 << (LOG_R - 1 - sl)) + (i >> (sl + 1))];
+        gs_bfly<W>(x[i], x[i + d], t.w, t.p, q);
       }
     }
   }
@@ -121,6 +122,7 @@ __device__ __forceinline__ void col_gs(W (&x)[1 << LOG_R], const W* itw, const W
 }
 
 // Forward column pass.  Thread = (limb l, poly p, column j1); j1 fastest.
+// Operand 1 is processed first: out0 may alias in1 (out = a * b, out == b).
 template <class W, int LOG_R>
 __global__ void __launch_bounds__(256)
 k_col_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t log_n,
@@ -137,20 +139,18 @@ k_col_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t 
   const uint64_t ib = (uint64_t)l * in_ls + (uint64_t)p * N + j1;
   const uint64_t ob = (uint64_t)l * out_ls + (uint64_t)p * N + j1;
   const W q = tp.lc[l].q;
-  const W* tw = tp.tw + (uint64_t)l * N;
-  const W* twp = tp.twp + (uint64_t)l * N;
+  const Tw<W>* tw = tp.tw + (uint64_t)l * N;
   W x[R];
-  // operand 1 first: out0 may alias in1 (out = a * b with out == b)
   if (in1 != nullptr) {
 #pragma unroll
     for (int i = 0; i < R; ++i) x[i] = in1[ib + (uint64_t)i * C];
-    col_ct<W, LOG_R>(x, tw, twp, q);
+    col_ct<W, LOG_R>(x, tw, q);
 #pragma unroll
     for (int i = 0; i < R; ++i) out1[ob + (uint64_t)i * C] = x[i];
   }
 #pragma unroll
   for (int i = 0; i < R; ++i) x[i] = in0[ib + (uint64_t)i * C];
-  col_ct<W, LOG_R>(x, tw, twp, q);
+  col_ct<W, LOG_R>(x, tw, q);
 #pragma unroll
   for (int i = 0; i < R; ++i) out0[ob + (uint64_t)i * C] = x[i];
 }
@@ -171,15 +171,14 @@ k_col_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, u
   const uint64_t ib = (uint64_t)l * in_ls + (uint64_t)p * N + j1;
   const uint64_t base = (uint64_t)l * out_ls + (uint64_t)p * N + j1;
   const LimbConst<W> lc = tp.lc[l];
-  const W* itw = tp.itw + (uint64_t)l * N;
-  const W* itwp = tp.itwp + (uint64_t)l * N;
+  const Tw<W>* itw = tp.itw + (uint64_t)l * N;
   W x[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) x[i] = in[ib + (uint64_t)i * C];
   if (rfold)
-    col_gs<W, LOG_R>(x, itw, itwp, lc.q, lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p);
+    col_gs<W, LOG_R>(x, itw, lc.q, lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p);
   else
-    col_gs<W, LOG_R>(x, itw, itwp, lc.q, lc.c1, lc.c1_p, lc.c2, lc.c2_p);
+    col_gs<W, LOG_R>(x, itw, lc.q, lc.c1, lc.c1_p, lc.c2, lc.c2_p);
   if (addend != nullptr) {
 #pragma unroll
     for (int i = 0; i < R; ++i) x[i] = add_mod<W>(x[i], addend[base + (uint64_t)i * C], lc.q);
@@ -208,14 +207,13 @@ k_ks_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32
   const uint32_t i = (uint32_t)(rest % L);
   const uint32_t j = (uint32_t)(rest / L);
   const LimbConst<W> lc = tp.lc[j];
-  const W* tw = tp.tw + (uint64_t)j * N;
-  const W* twp = tp.twp + (uint64_t)j * N;
+  const Tw<W>* tw = tp.tw + (uint64_t)j * N;
   const uint64_t src = (uint64_t)i * d_ls + (uint64_t)p * N + j1;
   const uint64_t dst = (((uint64_t)j * L + i) * B + p) * N + j1;
   W x[R];
 #pragma unroll
   for (int t = 0; t < R; ++t) x[t] = shoup_mul<W>(d[src + (uint64_t)t * C], (W)1, lc.one_p, lc.q);
-  col_ct<W, LOG_R>(x, tw, twp, lc.q);
+  col_ct<W, LOG_R>(x, tw, lc.q);
 #pragma unroll
   for (int t = 0; t < R; ++t) S[dst + (uint64_t)t * C] = x[t];
 }
@@ -224,237 +222,234 @@ k_ks_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32
 // row passes
 // ---------------------------------------------------------------------------
 
-// Row-local index of register i for a pass whose register bits are
-// [bb, bb+LOGE).
-template <int LOGE>
-__device__ __forceinline__ uint32_t relem(uint32_t tau, int bb, int i) {
-  const uint32_t lowmask = (1u << bb) - 1u;
-  return (tau & lowmask) | ((uint32_t)i << bb) | ((tau >> bb) << (bb + LOGE));
-}
-__device__ __forceinline__ uint32_t swz(uint32_t j) { return j + (j >> 4); }
-
-// Pass schedule of the row stages.  LOGE == 4: radix-16 passes from the top
-// bits down, then a partial pass on bits [0, log_c mod 4) with register bits
-// [0, 4).  LOGE < 4 (tiny rings, log_c == LOGE): one pass holding the row.
-template <int LOGE>
-struct RowSched {
-  int full, rem, P;
-  uint32_t log_c;
-  __device__ __forceinline__ explicit RowSched(uint32_t lc) : log_c(lc) {
-    if (LOGE == 4) {
-      full = (int)(lc >> 2);
-      rem = (int)(lc & 3);
-    } else {
-      full = 0;
-      rem = (int)lc;
-    }
-    P = full + (rem ? 1 : 0);
+// Compile-time row geometry.  A row of C = 2^LOG_C words is held by T
+// threads with E = 2^LOGE registers each.  Passes run from the top bits
+// down: full radix-16 passes on bits [bb, bb+4), then (if LOG_C % 4) a
+// partial pass on bits [0, REM) with register bits [0, 4).  Tiny rows
+// (LOG_C < 4) are one thread holding the whole row.
+template <int LOG_C>
+struct RowGeo {
+  static constexpr int LOGC = LOG_C;
+  static constexpr int LOGE = LOG_C >= 4 ? 4 : LOG_C;
+  static constexpr int E = 1 << LOGE;
+  static constexpr int LOG_T = LOG_C - LOGE;
+  static constexpr int T = 1 << LOG_T;
+  static constexpr int C = 1 << LOG_C;
+  static constexpr int PADC = C + (C >> 4);
+  static constexpr int THREADS = T > kRowThreads ? T : kRowThreads;
+  static constexpr int RPW = THREADS / T;  // rows per workgroup
+  static constexpr int FULL = LOGE == 4 ? LOG_C / 4 : 0;
+  static constexpr int REM = LOGE == 4 ? LOG_C % 4 : LOG_C;
+  static constexpr int P = FULL + (REM ? 1 : 0);
+  static constexpr int bb(int p) { return (p >= 0 && p < FULL) ? LOG_C - 4 * (p + 1) : 0; }
+  static constexpr int k(int p) { return p < FULL ? 4 : REM; }
+  static constexpr int BB0 = bb(0);
+  static constexpr int BBL = bb(P - 1);
+  // row-local index of register i in the distribution with register bits
+  // [bb, bb+LOGE): base(tau) | (i << bb)
+  __device__ static __forceinline__ uint32_t base(uint32_t tau, int b) {
+    const uint32_t lowmask = (1u << b) - 1u;
+    return (tau & lowmask) | ((tau >> b) << (b + LOGE));
   }
-  __device__ __forceinline__ int bb(int p) const {
-    return (p >= 0 && p < full) ? (int)log_c - 4 * (p + 1) : 0;
-  }
-  __device__ __forceinline__ int k(int p) const { return p < full ? 4 : rem; }
-  __device__ __forceinline__ int first_bb() const { return bb(0); }
-  __device__ __forceinline__ int last_bb() const { return bb(P - 1); }
+  // padded LDS offset: swz(base | (i<<b)) = swz(base) + (i<<b) + ((i<<b)>>4)
+  // (base has zero bits in [b, b+LOGE), so no carries)
+  __device__ static __forceinline__ uint32_t swz(uint32_t j) { return j + (j >> 4); }
+  static constexpr uint32_t ioff(int i, int b) { return ((uint32_t)i << b) + (((uint32_t)i << b) >> 4); }
 };
 
-// CT stages on bits [bb, bb+K) of the row for NOPS operands sharing twiddles.
-template <class W, int NOPS, int LOGE>
-__device__ __forceinline__ void row_ct(W (&x)[NOPS][1 << LOGE], int bb, int K, uint64_t gbase,
-                                       const W* tw, const W* twp, W q) {
+// Load CNT consecutive twiddle pairs starting at a CNT-aligned node.
+template <class W, int CNT>
+__device__ __forceinline__ void load_tw(Tw<W> (&t)[CNT], const Tw<W>* p) {
+#pragma unroll
+  for (int m = 0; m < CNT; ++m) t[m] = p[m];
+}
+
+// CT stages on bits [bb, bb+K) for NOPS operands sharing twiddles.  `node0`
+// = (N + r*C + P0) where P0 = row-local index of register 0.
+template <class W, int NOPS, int LOGE, int K, int BB>
+__device__ __forceinline__ void row_ct(W (&x)[NOPS][1 << LOGE], uint64_t node0,
+                                       const Tw<W>* tw, W q) {
   constexpr int E = 1 << LOGE;
-  constexpr int H = E > 1 ? E / 2 : 1;
 #pragma unroll
-  for (int sl = LOGE - 1; sl >= 0; --sl) {
-    if (sl >= K) continue;
-    const int s = bb + sl;
-    const uint64_t nb = gbase >> (s + 1);
+  for (int sl = K - 1; sl >= 0; --sl) {
+    constexpr int H = E > 1 ? E / 2 : 1;
+    const int cnt = H >> sl;  // distinct twiddles at this stage
+    const uint64_t nb = node0 >> (BB + sl + 1);
+    Tw<W> t[H];
+#pragma unroll
+    for (int m = 0; m < H; ++m)
+      if (m < cnt) t[m] = tw[nb + m];
     const int d = 1 << sl;
-    const int cnt = H >> sl;
-    W w[H], wp[H];
-#pragma unroll
-    for (int m = 0; m < H; ++m) {
-      if (m < cnt) {
-        w[m] = tw[nb + m];
-        wp[m] = twp[nb + m];
-      }
-    }
 #pragma unroll
     for (int i = 0; i < E; ++i) {
       if (i & d) continue;
       const int m = i >> (sl + 1);
 #pragma unroll
-      for (int o = 0; o < NOPS; ++o) ct_bfly<W>(x[o][i], x[o][i | d], w[m], wp[m], q);
+      for (int o = 0; o < NOPS; ++o) ct_bfly<W>(x[o][i], x[o][i | d], t[m].w, t[m].p, q);
     }
   }
 }
 
-template <class W, int NOPS, int LOGE>
-__device__ __forceinline__ void row_gs(W (&x)[NOPS][1 << LOGE], int bb, int K, uint64_t gbase,
-                                       const W* itw, const W* itwp, W q) {
+template <class W, int NOPS, int LOGE, int K, int BB>
+__device__ __forceinline__ void row_gs(W (&x)[NOPS][1 << LOGE], uint64_t node0,
+                                       const Tw<W>* itw, W q) {
   constexpr int E = 1 << LOGE;
-  constexpr int H = E > 1 ? E / 2 : 1;
 #pragma unroll
-  for (int sl = 0; sl < LOGE; ++sl) {
-    if (sl >= K) continue;
-    const int s = bb + sl;
-    const uint64_t nb = gbase >> (s + 1);
-    const int d = 1 << sl;
+  for (int sl = 0; sl < K; ++sl) {
+    constexpr int H = E > 1 ? E / 2 : 1;
     const int cnt = H >> sl;
-    W w[H], wp[H];
+    const uint64_t nb = node0 >> (BB + sl + 1);
+    Tw<W> t[H];
 #pragma unroll
-    for (int m = 0; m < H; ++m) {
-      if (m < cnt) {
-        w[m] = itw[nb + m];
-        wp[m] = itwp[nb + m];
-      }
-    }
+    for (int m = 0; m < H; ++m)
+      if (m < cnt) t[m] = itw[nb + m];
+    const int d = 1 << sl;
 #pragma unroll
     for (int i = 0; i < E; ++i) {
       if (i & d) continue;
       const int m = i >> (sl + 1);
 #pragma unroll
-      for (int o = 0; o < NOPS; ++o) gs_bfly<W>(x[o][i], x[o][i | d], w[m], wp[m], q);
+      for (int o = 0; o < NOPS; ++o) gs_bfly<W>(x[o][i], x[o][i | d], t[m].w, t[m].p, q);
     }
   }
 }
 
-// Move NOPS register sets from distribution bb_from to bb_to through LDS.
-// Region of operand o for this row: lds + (o * rows_per_wg + slot) * padc.
-template <class W, int NOPS, int LOGE>
-__device__ __forceinline__ void row_exchange(W (&x)[NOPS][1 << LOGE], W* lds, uint32_t padc,
-                                             uint32_t rows_per_wg, uint32_t slot, uint32_t tau,
-                                             int bb_from, int bb_to) {
-  constexpr int E = 1 << LOGE;
-#pragma unroll
-  for (int o = 0; o < NOPS; ++o) {
-    W* reg = lds + ((uint32_t)o * rows_per_wg + slot) * padc;
-#pragma unroll
-    for (int i = 0; i < E; ++i) reg[swz(relem<LOGE>(tau, bb_from, i))] = x[o][i];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int o = 0; o < NOPS; ++o) {
-    const W* reg = lds + ((uint32_t)o * rows_per_wg + slot) * padc;
-#pragma unroll
-    for (int i = 0; i < E; ++i) x[o][i] = reg[swz(relem<LOGE>(tau, bb_to, i))];
-  }
-  __syncthreads();
-}
-
+// Per-thread row coordinates.
 struct RowPos {
-  uint32_t slot, tau, rpw, padc, C;
+  uint32_t slot, tau;
   uint32_t l, p, r;
   bool active;
   uint64_t gb;  // N + r*C: heap base of this row
 };
 
-template <int LOGE>
-__device__ __forceinline__ RowPos row_pos(uint32_t log_n, uint32_t log_c, uint32_t B,
-                                          uint64_t rows_total) {
+template <class G>
+__device__ __forceinline__ RowPos row_pos(uint32_t log_n, uint32_t B, uint64_t rows_total) {
   RowPos rp;
-  const uint32_t log_t = log_c - LOGE;
-  rp.C = 1u << log_c;
-  rp.rpw = blockDim.x >> log_t;
-  rp.slot = threadIdx.x >> log_t;
-  rp.tau = threadIdx.x & ((1u << log_t) - 1u);
-  rp.padc = rp.C + (rp.C >> 4);
-  uint64_t row = (uint64_t)blockIdx.x * rp.rpw + rp.slot;
+  rp.slot = threadIdx.x >> G::LOG_T;
+  rp.tau = threadIdx.x & (G::T - 1);
+  uint64_t row = (uint64_t)blockIdx.x * G::RPW + rp.slot;
   rp.active = row < rows_total;
   if (!rp.active) row = 0;
-  const uint32_t log_r = log_n - log_c;
+  const uint32_t log_r = log_n - G::LOGC;
   const uint64_t lp = row >> log_r;
   rp.r = (uint32_t)(row & ((1u << log_r) - 1u));
   rp.l = (uint32_t)(lp / B);
   rp.p = (uint32_t)(lp - (uint64_t)rp.l * B);
-  rp.gb = (1ull << log_n) + (uint64_t)rp.r * rp.C;
+  rp.gb = (1ull << log_n) + (uint64_t)rp.r * G::C;
   return rp;
+}
+
+// Move NOPS register sets from distribution BF to BT through LDS.
+template <class G, class W, int NOPS, int BF, int BT>
+__device__ __forceinline__ void row_exchange(W (&x)[NOPS][G::E], W* lds, uint32_t slot,
+                                             uint32_t tau) {
+  const uint32_t wb = G::swz(G::base(tau, BF));
+  const uint32_t rb = G::swz(G::base(tau, BT));
+#pragma unroll
+  for (int o = 0; o < NOPS; ++o) {
+    W* reg = lds + ((uint32_t)o * G::RPW + slot) * G::PADC;
+#pragma unroll
+    for (int i = 0; i < G::E; ++i) reg[wb + G::ioff(i, BF)] = x[o][i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < NOPS; ++o) {
+    const W* reg = lds + ((uint32_t)o * G::RPW + slot) * G::PADC;
+#pragma unroll
+    for (int i = 0; i < G::E; ++i) x[o][i] = reg[rb + G::ioff(i, BT)];
+  }
+  __syncthreads();
+}
+
+// Forward pass p (with the exchange from pass p-1's distribution).
+template <class G, class W, int NOPS, int PP>
+__device__ __forceinline__ void fwd_pass(W (&x)[NOPS][G::E], const RowPos& rp, W* lds,
+                                         const Tw<W>* tw, W q) {
+  constexpr int BB = G::bb(PP);
+  if constexpr (PP > 0) row_exchange<G, W, NOPS, G::bb(PP - 1), BB>(x, lds, rp.slot, rp.tau);
+  row_ct<W, NOPS, G::LOGE, G::k(PP), BB>(x, rp.gb + G::base(rp.tau, BB), tw, q);
+}
+
+template <class G, class W, int NOPS, int PP>
+__device__ __forceinline__ void inv_pass(W (&x)[NOPS][G::E], const RowPos& rp, W* lds,
+                                         const Tw<W>* itw, W q) {
+  constexpr int BB = G::bb(PP);
+  if constexpr (PP < G::P - 1) row_exchange<G, W, NOPS, G::bb(PP + 1), BB>(x, lds, rp.slot, rp.tau);
+  row_gs<W, NOPS, G::LOGE, G::k(PP), BB>(x, rp.gb + G::base(rp.tau, BB), itw, q);
 }
 
 // All forward row passes on NOPS operands loaded in the first-pass
 // distribution; leaves the registers in the last-pass distribution.
-template <class W, int NOPS, int LOGE>
-__device__ __forceinline__ void rows_fwd(W (&x)[NOPS][1 << LOGE], const RowSched<LOGE>& sc,
-                                         const RowPos& rp, W* lds, const W* tw, const W* twp,
-                                         W q) {
-  int prev = sc.first_bb();
-  for (int p = 0; p < sc.P; ++p) {
-    const int bb = sc.bb(p);
-    if (p > 0) row_exchange<W, NOPS, LOGE>(x, lds, rp.padc, rp.rpw, rp.slot, rp.tau, prev, bb);
-    row_ct<W, NOPS, LOGE>(x, bb, sc.k(p), rp.gb + relem<LOGE>(rp.tau, bb, 0), tw, twp, q);
-    prev = bb;
-  }
+template <class G, class W, int NOPS>
+__device__ __forceinline__ void rows_fwd(W (&x)[NOPS][G::E], const RowPos& rp, W* lds,
+                                         const Tw<W>* tw, W q) {
+  if constexpr (G::P > 0) fwd_pass<G, W, NOPS, 0>(x, rp, lds, tw, q);
+  if constexpr (G::P > 1) fwd_pass<G, W, NOPS, 1>(x, rp, lds, tw, q);
+  if constexpr (G::P > 2) fwd_pass<G, W, NOPS, 2>(x, rp, lds, tw, q);
+  if constexpr (G::P > 3) fwd_pass<G, W, NOPS, 3>(x, rp, lds, tw, q);
 }
 
 // All inverse row passes; last-pass distribution in, first-pass out.
-template <class W, int NOPS, int LOGE>
-__device__ __forceinline__ void rows_inv(W (&x)[NOPS][1 << LOGE], const RowSched<LOGE>& sc,
-                                         const RowPos& rp, W* lds, const W* itw, const W* itwp,
-                                         W q) {
-  int prev = sc.last_bb();
-  for (int p = sc.P - 1; p >= 0; --p) {
-    const int bb = sc.bb(p);
-    if (p < sc.P - 1)
-      row_exchange<W, NOPS, LOGE>(x, lds, rp.padc, rp.rpw, rp.slot, rp.tau, prev, bb);
-    row_gs<W, NOPS, LOGE>(x, bb, sc.k(p), rp.gb + relem<LOGE>(rp.tau, bb, 0), itw, itwp, q);
-    prev = bb;
-  }
+template <class G, class W, int NOPS>
+__device__ __forceinline__ void rows_inv(W (&x)[NOPS][G::E], const RowPos& rp, W* lds,
+                                         const Tw<W>* itw, W q) {
+  if constexpr (G::P > 3) inv_pass<G, W, NOPS, 3>(x, rp, lds, itw, q);
+  if constexpr (G::P > 2) inv_pass<G, W, NOPS, 2>(x, rp, lds, itw, q);
+  if constexpr (G::P > 1) inv_pass<G, W, NOPS, 1>(x, rp, lds, itw, q);
+  if constexpr (G::P > 0) inv_pass<G, W, NOPS, 0>(x, rp, lds, itw, q);
 }
 
 // mode 0: forward rows in place; 1: inverse rows in place;
 // 2: poly-mul rows: x <- INV(FWD(x) (.) FWD(y)) with Montgomery pointwise.
-template <class W, int MODE, int LOGE>
-__global__ void __launch_bounds__(512)
-k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_n,
-      uint32_t log_c, uint32_t B, uint64_t ls, uint64_t rows_total) {
+template <class W, int MODE, int LOG_C>
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS)
+k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_n, uint32_t B,
+      uint64_t ls, uint64_t rows_total) {
+  using G = RowGeo<LOG_C>;
+  constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  constexpr int E = 1 << LOGE;
   W* lds = (W*)smem_raw;
-  const RowPos rp = row_pos<LOGE>(log_n, log_c, B, rows_total);
-  const RowSched<LOGE> sc(log_c);
+  const RowPos rp = row_pos<G>(log_n, B, rows_total);
   const uint64_t N = 1ull << log_n;
-  const uint64_t base = (uint64_t)rp.l * ls + (uint64_t)rp.p * N + (uint64_t)rp.r * rp.C;
+  const uint64_t base = (uint64_t)rp.l * ls + (uint64_t)rp.p * N + (uint64_t)rp.r * G::C;
   const LimbConst<W> lc = tp.lc[rp.l];
-  const W* tw = tp.tw + (uint64_t)rp.l * N;
-  const W* twp = tp.twp + (uint64_t)rp.l * N;
-  const W* itw = tp.itw + (uint64_t)rp.l * N;
-  const W* itwp = tp.itwp + (uint64_t)rp.l * N;
-  const int bb0 = sc.first_bb();
-  const int bbl = sc.last_bb();
-  if (MODE == 2) {
+  const Tw<W>* tw = tp.tw + (uint64_t)rp.l * N;
+  const Tw<W>* itw = tp.itw + (uint64_t)rp.l * N;
+  const uint32_t b0 = G::base(rp.tau, G::BB0);
+  const uint32_t bl = G::base(rp.tau, G::BBL);
+  if constexpr (MODE == 2) {
     W v[2][E];
 #pragma unroll
     for (int i = 0; i < E; ++i) {
-      const uint32_t e = relem<LOGE>(rp.tau, bb0, i);
-      v[0][i] = xg[base + e];
-      v[1][i] = yg[base + e];
+      v[0][i] = xg[base + b0 + ((uint32_t)i << G::BB0)];
+      v[1][i] = yg[base + b0 + ((uint32_t)i << G::BB0)];
     }
-    rows_fwd<W, 2, LOGE>(v, sc, rp, lds, tw, twp, lc.q);
+    rows_fwd<G, W, 2>(v, rp, lds, tw, lc.q);
     W z[1][E];
 #pragma unroll
     for (int i = 0; i < E; ++i) z[0][i] = mont_mul<W>(v[0][i], v[1][i], lc.q, lc.qinv);
-    rows_inv<W, 1, LOGE>(z, sc, rp, lds, itw, itwp, lc.q);
+    rows_inv<G, W, 1>(z, rp, lds, itw, lc.q);
     if (rp.active) {
 #pragma unroll
-      for (int i = 0; i < E; ++i) xg[base + relem<LOGE>(rp.tau, bb0, i)] = z[0][i];
+      for (int i = 0; i < E; ++i) xg[base + b0 + ((uint32_t)i << G::BB0)] = z[0][i];
     }
-  } else if (MODE == 0) {
+  } else if constexpr (MODE == 0) {
     W v[1][E];
 #pragma unroll
-    for (int i = 0; i < E; ++i) v[0][i] = xg[base + relem<LOGE>(rp.tau, bb0, i)];
-    rows_fwd<W, 1, LOGE>(v, sc, rp, lds, tw, twp, lc.q);
+    for (int i = 0; i < E; ++i) v[0][i] = xg[base + b0 + ((uint32_t)i << G::BB0)];
+    rows_fwd<G, W, 1>(v, rp, lds, tw, lc.q);
     if (rp.active) {
 #pragma unroll
-      for (int i = 0; i < E; ++i) xg[base + relem<LOGE>(rp.tau, bbl, i)] = v[0][i];
+      for (int i = 0; i < E; ++i) xg[base + bl + ((uint32_t)i << G::BBL)] = v[0][i];
     }
   } else {
     W v[1][E];
 #pragma unroll
-    for (int i = 0; i < E; ++i) v[0][i] = xg[base + relem<LOGE>(rp.tau, bbl, i)];
-    rows_inv<W, 1, LOGE>(v, sc, rp, lds, itw, itwp, lc.q);
+    for (int i = 0; i < E; ++i) v[0][i] = xg[base + bl + ((uint32_t)i << G::BBL)];
+    rows_inv<G, W, 1>(v, rp, lds, itw, lc.q);
     if (rp.active) {
 #pragma unroll
-      for (int i = 0; i < E; ++i) xg[base + relem<LOGE>(rp.tau, bb0, i)] = v[0][i];
+      for (int i = 0; i < E; ++i) xg[base + b0 + ((uint32_t)i << G::BB0)] = v[0][i];
     }
   }
 }
@@ -462,34 +457,32 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
 // Key-switch rows.  Row = (target limb j, poly p, row r).  For every source
 // limb i: forward rows of S[j][i][p], multiply-accumulate with the
 // NTT-resident keys; then the inverse rows of both accumulators.
-template <class W, int LOGE>
-__global__ void __launch_bounds__(512)
+template <class W, int LOG_C>
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS)
 k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
           const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
           const W* __restrict__ init0, const W* __restrict__ init1, uint64_t init_ls,
-          TabPtrs<W> tp, uint32_t log_n, uint32_t log_c, uint32_t L, uint32_t B, uint64_t ls,
+          TabPtrs<W> tp, uint32_t log_n, uint32_t L, uint32_t B, uint64_t ls,
           uint64_t rows_total) {
+  using G = RowGeo<LOG_C>;
+  constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  constexpr int E = 1 << LOGE;
   W* lds = (W*)smem_raw;
-  const RowPos rp = row_pos<LOGE>(log_n, log_c, B, rows_total);  // rp.l == target limb j
-  const RowSched<LOGE> sc(log_c);
+  const RowPos rp = row_pos<G>(log_n, B, rows_total);  // rp.l == target limb j
   const uint64_t N = 1ull << log_n;
   const uint32_t j = rp.l;
-  const uint64_t rowoff = (uint64_t)rp.r * rp.C;
+  const uint64_t rowoff = (uint64_t)rp.r * G::C;
   const uint64_t obase = (uint64_t)j * ls + (uint64_t)rp.p * N + rowoff;
   const uint64_t ibase = (uint64_t)j * init_ls + (uint64_t)rp.p * N + rowoff;
   const LimbConst<W> lc = tp.lc[j];
-  const W* tw = tp.tw + (uint64_t)j * N;
-  const W* twp = tp.twp + (uint64_t)j * N;
-  const W* itw = tp.itw + (uint64_t)j * N;
-  const W* itwp = tp.itwp + (uint64_t)j * N;
-  const int bb0 = sc.first_bb();
-  const int bbl = sc.last_bb();
+  const Tw<W>* tw = tp.tw + (uint64_t)j * N;
+  const Tw<W>* itw = tp.itw + (uint64_t)j * N;
+  const uint32_t b0 = G::base(rp.tau, G::BB0);
+  const uint32_t bl = G::base(rp.tau, G::BBL);
   W acc[2][E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
-    const uint32_t pos = relem<LOGE>(rp.tau, bbl, e);
+    const uint32_t pos = bl + ((uint32_t)e << G::BBL);
     acc[0][e] = init0 ? init0[ibase + pos] : (W)0;
     acc[1][e] = init1 ? init1[ibase + pos] : (W)0;
   }
@@ -497,24 +490,24 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     const uint64_t sbase = (((uint64_t)j * L + i) * B + rp.p) * N + rowoff;
     W x[1][E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) x[0][e] = S[sbase + relem<LOGE>(rp.tau, bb0, e)];
-    rows_fwd<W, 1, LOGE>(x, sc, rp, lds, tw, twp, lc.q);
+    for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
+    rows_fwd<G, W, 1>(x, rp, lds, tw, lc.q);
     // key poly i, limb j (key buffers hold L polys: limb stride key_ls)
     const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + rowoff;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const uint32_t pos = relem<LOGE>(rp.tau, bbl, e);
+      const uint32_t pos = bl + ((uint32_t)e << G::BBL);
       const W kb = key_b[kbase + pos];
       const W ka = key_a[kbase + pos];
       acc[0][e] = add_mod<W>(acc[0][e], mont_mul<W>(x[0][e], kb, lc.q, lc.qinv), lc.q);
       acc[1][e] = add_mod<W>(acc[1][e], mont_mul<W>(x[0][e], ka, lc.q, lc.qinv), lc.q);
     }
   }
-  rows_inv<W, 2, LOGE>(acc, sc, rp, lds, itw, itwp, lc.q);
+  rows_inv<G, W, 2>(acc, rp, lds, itw, lc.q);
   if (rp.active) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const uint32_t pos = relem<LOGE>(rp.tau, bb0, e);
+      const uint32_t pos = b0 + ((uint32_t)e << G::BB0);
       u0[obase + pos] = acc[0][e];
       u1[obase + pos] = acc[1][e];
     }
@@ -526,41 +519,39 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
 // d2 = c1 c1' (pointwise, Montgomery-scaled by 2^-w).  d0hat / d1hat are
 // written as NTT-domain rows (last-pass distribution) for the key-switch
 // accumulators; d2 goes through the inverse rows into d2row.
-template <class W, int LOGE>
-__global__ void __launch_bounds__(512)
+template <class W, int LOG_C>
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS)
 k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2row,
               const W* __restrict__ c0, const W* __restrict__ c1, const W* __restrict__ c0p,
-              const W* __restrict__ c1p, TabPtrs<W> tp, uint32_t log_n, uint32_t log_c,
-              uint32_t B, uint64_t ls, uint64_t rows_total) {
+              const W* __restrict__ c1p, TabPtrs<W> tp, uint32_t log_n, uint32_t B, uint64_t ls,
+              uint64_t rows_total) {
+  using G = RowGeo<LOG_C>;
+  constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  constexpr int E = 1 << LOGE;
   W* lds = (W*)smem_raw;
-  const RowPos rp = row_pos<LOGE>(log_n, log_c, B, rows_total);
-  const RowSched<LOGE> sc(log_c);
+  const RowPos rp = row_pos<G>(log_n, B, rows_total);
   const uint64_t N = 1ull << log_n;
-  const uint64_t base = (uint64_t)rp.l * ls + (uint64_t)rp.p * N + (uint64_t)rp.r * rp.C;
+  const uint64_t base = (uint64_t)rp.l * ls + (uint64_t)rp.p * N + (uint64_t)rp.r * G::C;
   const LimbConst<W> lc = tp.lc[rp.l];
-  const W* tw = tp.tw + (uint64_t)rp.l * N;
-  const W* twp = tp.twp + (uint64_t)rp.l * N;
-  const W* itw = tp.itw + (uint64_t)rp.l * N;
-  const W* itwp = tp.itwp + (uint64_t)rp.l * N;
-  const int bb0 = sc.first_bb();
-  const int bbl = sc.last_bb();
+  const Tw<W>* tw = tp.tw + (uint64_t)rp.l * N;
+  const Tw<W>* itw = tp.itw + (uint64_t)rp.l * N;
+  const uint32_t b0 = G::base(rp.tau, G::BB0);
+  const uint32_t bl = G::base(rp.tau, G::BBL);
   W a[2][E], b[2][E];
 #pragma unroll
   for (int i = 0; i < E; ++i) {
-    const uint32_t e = relem<LOGE>(rp.tau, bb0, i);
+    const uint32_t e = b0 + ((uint32_t)i << G::BB0);
     a[0][i] = c0[base + e];
     a[1][i] = c1[base + e];
   }
-  rows_fwd<W, 2, LOGE>(a, sc, rp, lds, tw, twp, lc.q);
+  rows_fwd<G, W, 2>(a, rp, lds, tw, lc.q);
 #pragma unroll
   for (int i = 0; i < E; ++i) {
-    const uint32_t e = relem<LOGE>(rp.tau, bb0, i);
+    const uint32_t e = b0 + ((uint32_t)i << G::BB0);
     b[0][i] = c0p[base + e];
     b[1][i] = c1p[base + e];
   }
-  rows_fwd<W, 2, LOGE>(b, sc, rp, lds, tw, twp, lc.q);
+  rows_fwd<G, W, 2>(b, rp, lds, tw, lc.q);
   W d2[1][E];
 #pragma unroll
   for (int i = 0; i < E; ++i) {
@@ -570,15 +561,15 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
                             mont_mul<W>(a[1][i], b[0][i], q, qi), q);
     d2[0][i] = mont_mul<W>(a[1][i], b[1][i], q, qi);
     if (rp.active) {
-      const uint32_t pos = relem<LOGE>(rp.tau, bbl, i);
+      const uint32_t pos = bl + ((uint32_t)i << G::BBL);
       d0hat[base + pos] = d0;
       d1hat[base + pos] = d1;
     }
   }
-  rows_inv<W, 1, LOGE>(d2, sc, rp, lds, itw, itwp, lc.q);
+  rows_inv<G, W, 1>(d2, rp, lds, itw, lc.q);
   if (rp.active) {
 #pragma unroll
-    for (int i = 0; i < E; ++i) d2row[base + relem<LOGE>(rp.tau, bb0, i)] = d2[0][i];
+    for (int i = 0; i < E; ++i) d2row[base + b0 + ((uint32_t)i << G::BB0)] = d2[0][i];
   }
 }
 
@@ -765,21 +756,6 @@ static inline unsigned grid_for(uint64_t total, unsigned block) {
   return (unsigned)((total + block - 1) / block);
 }
 
-static inline int row_loge(const Geom& g) { return g.log_c >= 4 ? 4 : (int)g.log_c; }
-
-template <class W>
-static size_t row_lds_bytes(const Geom& g, int nops) {
-  const size_t T = g.c >> row_loge(g);
-  const size_t threads = T > (size_t)kRowThreads ? T : (size_t)kRowThreads;
-  const size_t rpw = threads / T;
-  return (size_t)nops * rpw * (g.c + g.c / 16) * sizeof(W);
-}
-
-static unsigned row_threads(const Geom& g) {
-  const size_t T = g.c >> row_loge(g);
-  return (unsigned)(T > (size_t)kRowThreads ? T : (size_t)kRowThreads);
-}
-
 template <class K>
 static hipError_t allow_lds(K kernel, size_t bytes) {
   if (bytes <= 65536) return hipSuccess;
@@ -796,6 +772,31 @@ static hipError_t allow_lds(K kernel, size_t bytes) {
     case 4: MACRO(4); break;           \
     default: return hipErrorInvalidValue; \
   }
+
+#define RNT_DISPATCH_LOGC(LOGC, MACRO) \
+  switch (LOGC) {                      \
+    case 0: MACRO(0);                  \
+    case 1: MACRO(1);                  \
+    case 2: MACRO(2);                  \
+    case 3: MACRO(3);                  \
+    case 4: MACRO(4);                  \
+    case 5: MACRO(5);                  \
+    case 6: MACRO(6);                  \
+    case 7: MACRO(7);                  \
+    case 8: MACRO(8);                  \
+    case 9: MACRO(9);                  \
+    case 10: MACRO(10);                \
+    case 11: MACRO(11);                \
+    case 12: MACRO(12);                \
+    case 13: MACRO(13);                \
+    default: return hipErrorInvalidValue; \
+  }
+
+template <class W, int LOG_C>
+static size_t row_lds(int nops) {
+  using G = RowGeo<LOG_C>;
+  return (size_t)nops * G::RPW * G::PADC * sizeof(W);
+}
 
 template <class W>
 static hipError_t col_fwd_t(const Launch& k, void* out0, const void* in0, void* out1,
@@ -829,45 +830,33 @@ static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const v
   return hipGetLastError();
 }
 
-#define RNT_DISPATCH_LOGE(LOGE, MACRO) \
-  switch (LOGE) {                      \
-    case 0: MACRO(0); break;           \
-    case 1: MACRO(1); break;           \
-    case 2: MACRO(2); break;           \
-    case 3: MACRO(3); break;           \
-    case 4: MACRO(4); break;           \
-    default: return hipErrorInvalidValue; \
-  }
-
-template <class W, int MODE, int LOGE>
-static hipError_t row_launch(const Launch& k, const Geom& g, void* x, const void* y,
-                             uint64_t ls) {
+template <class W, int MODE, int LOG_C>
+static hipError_t row_launch(const Launch& k, void* x, const void* y, uint64_t ls) {
+  using G = RowGeo<LOG_C>;
+  const Geom g = geom_for(k.t->log_n);
   const uint64_t rows = (uint64_t)k.L * k.B * g.r;
   if (rows == 0) return hipSuccess;
-  const unsigned threads = row_threads(g);
-  const uint64_t rpw = threads / (g.c >> LOGE);
-  const unsigned blocks = (unsigned)((rows + rpw - 1) / rpw);
-  const size_t lds = row_lds_bytes<W>(g, MODE == 2 ? 2 : 1);
-  hipError_t e = allow_lds(k_row<W, MODE, LOGE>, lds);
+  const unsigned blocks = (unsigned)((rows + G::RPW - 1) / G::RPW);
+  const size_t lds = row_lds<W, LOG_C>(MODE == 2 ? 2 : 1);
+  hipError_t e = allow_lds(k_row<W, MODE, LOG_C>, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_row<W, MODE, LOGE>), dim3(blocks), dim3(threads), lds, k.s, (W*)x,
-                     (const W*)y, tab_ptrs<W>(k.t), g.log_n, g.log_c, (uint32_t)k.B, ls, rows);
+  hipLaunchKernelGGL((k_row<W, MODE, LOG_C>), dim3(blocks), dim3(G::THREADS), lds, k.s, (W*)x,
+                     (const W*)y, tab_ptrs<W>(k.t), g.log_n, (uint32_t)k.B, ls, rows);
   return hipGetLastError();
 }
 
 template <class W>
 static hipError_t row_t(const Launch& k, int mode, void* x, const void* y, uint64_t ls) {
   const Geom g = geom_for(k.t->log_n);
-  const int loge = row_loge(g);
-#define RNT_L0(E) return row_launch<W, 0, E>(k, g, x, y, ls)
-#define RNT_L1(E) return row_launch<W, 1, E>(k, g, x, y, ls)
-#define RNT_L2(E) return row_launch<W, 2, E>(k, g, x, y, ls)
+#define RNT_L0(C) return row_launch<W, 0, C>(k, x, y, ls)
+#define RNT_L1(C) return row_launch<W, 1, C>(k, x, y, ls)
+#define RNT_L2(C) return row_launch<W, 2, C>(k, x, y, ls)
   if (mode == 0) {
-    RNT_DISPATCH_LOGE(loge, RNT_L0)
+    RNT_DISPATCH_LOGC(g.log_c, RNT_L0)
   } else if (mode == 1) {
-    RNT_DISPATCH_LOGE(loge, RNT_L1)
+    RNT_DISPATCH_LOGC(g.log_c, RNT_L1)
   } else {
-    RNT_DISPATCH_LOGE(loge, RNT_L2)
+    RNT_DISPATCH_LOGC(g.log_c, RNT_L2)
   }
 #undef RNT_L0
 #undef RNT_L1
@@ -978,22 +967,21 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
   return hipGetLastError();
 }
 
-template <class W, int LOGE>
-static hipError_t ks_rows_launch(const Launch& k, const Geom& g, void* u0, void* u1,
-                                 uint64_t ls, const void* S, const void* key_a,
-                                 const void* key_b, uint64_t key_ls, const void* init0,
-                                 const void* init1, uint64_t init_ls) {
+template <class W, int LOG_C>
+static hipError_t ks_rows_launch(const Launch& k, void* u0, void* u1, uint64_t ls, const void* S,
+                                 const void* key_a, const void* key_b, uint64_t key_ls,
+                                 const void* init0, const void* init1, uint64_t init_ls) {
+  using G = RowGeo<LOG_C>;
+  const Geom g = geom_for(k.t->log_n);
   const uint64_t rows = (uint64_t)k.L * k.B * g.r;
   if (rows == 0) return hipSuccess;
-  const unsigned threads = row_threads(g);
-  const uint64_t rpw = threads / (g.c >> LOGE);
-  const unsigned blocks = (unsigned)((rows + rpw - 1) / rpw);
-  const size_t lds = row_lds_bytes<W>(g, 2);
-  hipError_t e = allow_lds(k_ks_rows<W, LOGE>, lds);
+  const unsigned blocks = (unsigned)((rows + G::RPW - 1) / G::RPW);
+  const size_t lds = row_lds<W, LOG_C>(2);
+  hipError_t e = allow_lds(k_ks_rows<W, LOG_C>, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_ks_rows<W, LOGE>), dim3(blocks), dim3(threads), lds, k.s, (W*)u0,
-                     (W*)u1, (const W*)S, (const W*)key_a, (const W*)key_b, (uint64_t)key_ls,
-                     (const W*)init0, (const W*)init1, init_ls, tab_ptrs<W>(k.t), g.log_n, g.log_c,
+  hipLaunchKernelGGL((k_ks_rows<W, LOG_C>), dim3(blocks), dim3(G::THREADS), lds, k.s, (W*)u0,
+                     (W*)u1, (const W*)S, (const W*)key_a, (const W*)key_b, key_ls,
+                     (const W*)init0, (const W*)init1, init_ls, tab_ptrs<W>(k.t), g.log_n,
                      (uint32_t)k.L, (uint32_t)k.B, ls, rows);
   return hipGetLastError();
 }
@@ -1003,29 +991,29 @@ static hipError_t ks_rows_t(const Launch& k, void* u0, void* u1, uint64_t ls, co
                             const void* key_a, const void* key_b, uint64_t key_ls,
                             const void* init0, const void* init1, uint64_t init_ls) {
   const Geom g = geom_for(k.t->log_n);
-#define RNT_L(E) \
-  return ks_rows_launch<W, E>(k, g, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls)
-  RNT_DISPATCH_LOGE(row_loge(g), RNT_L)
+#define RNT_L(C) \
+  return ks_rows_launch<W, C>(k, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls)
+  RNT_DISPATCH_LOGC(g.log_c, RNT_L)
 #undef RNT_L
   return hipErrorInvalidValue;
 }
 
-template <class W, int LOGE>
-static hipError_t tensor_rows_launch(const Launch& k, const Geom& g, void* d0hat, void* d1hat,
-                                     void* d2row, const void* c0, const void* c1,
-                                     const void* c0p, const void* c1p, uint64_t ls) {
+template <class W, int LOG_C>
+static hipError_t tensor_rows_launch(const Launch& k, void* d0hat, void* d1hat, void* d2row,
+                                     const void* c0, const void* c1, const void* c0p,
+                                     const void* c1p, uint64_t ls) {
+  using G = RowGeo<LOG_C>;
+  const Geom g = geom_for(k.t->log_n);
   const uint64_t rows = (uint64_t)k.L * k.B * g.r;
   if (rows == 0) return hipSuccess;
-  const unsigned threads = row_threads(g);
-  const uint64_t rpw = threads / (g.c >> LOGE);
-  const unsigned blocks = (unsigned)((rows + rpw - 1) / rpw);
-  const size_t lds = row_lds_bytes<W>(g, 2);
-  hipError_t e = allow_lds(k_tensor_rows<W, LOGE>, lds);
+  const unsigned blocks = (unsigned)((rows + G::RPW - 1) / G::RPW);
+  const size_t lds = row_lds<W, LOG_C>(2);
+  hipError_t e = allow_lds(k_tensor_rows<W, LOG_C>, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_tensor_rows<W, LOGE>), dim3(blocks), dim3(threads), lds, k.s,
+  hipLaunchKernelGGL((k_tensor_rows<W, LOG_C>), dim3(blocks), dim3(G::THREADS), lds, k.s,
                      (W*)d0hat, (W*)d1hat, (W*)d2row, (const W*)c0, (const W*)c1,
-                     (const W*)c0p, (const W*)c1p, tab_ptrs<W>(k.t), g.log_n, g.log_c,
-                     (uint32_t)k.B, ls, rows);
+                     (const W*)c0p, (const W*)c1p, tab_ptrs<W>(k.t), g.log_n, (uint32_t)k.B, ls,
+                     rows);
   return hipGetLastError();
 }
 
@@ -1034,9 +1022,8 @@ static hipError_t tensor_rows_t(const Launch& k, void* d0hat, void* d1hat, void*
                                 const void* c0, const void* c1, const void* c0p,
                                 const void* c1p, uint64_t ls) {
   const Geom g = geom_for(k.t->log_n);
-#define RNT_L(E) \
-  return tensor_rows_launch<W, E>(k, g, d0hat, d1hat, d2row, c0, c1, c0p, c1p, ls)
-  RNT_DISPATCH_LOGE(row_loge(g), RNT_L)
+#define RNT_L(C) return tensor_rows_launch<W, C>(k, d0hat, d1hat, d2row, c0, c1, c0p, c1p, ls)
+  RNT_DISPATCH_LOGC(g.log_c, RNT_L)
 #undef RNT_L
   return hipErrorInvalidValue;
 }
