@@ -151,7 +151,7 @@ def main():
     kernels = {}
     for k in ("col_fwd", "row_mul", "col_inv"):
         cnt, ms = B.profile_read(k)
-        kernels[k] = {"launches": cnt, "avg_ms": ms / cnt if cnt else None}
+        kernels[k] = {"launches": cnt, "avg_ms": ms / cnt if cnt else None, "total_ms": ms}
     B.profile_enable(False)
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -172,11 +172,14 @@ def main():
     else:
         parity_ok = True
 
-    # roofline of the dominant kernel (algorithmic bytes per launch / avg launch time)
+    # roofline of the dominant kernel: algorithmic bytes per launch / average
+    # launch time (a step may issue several launches when the batch is
+    # chunked; bytes per launch = bytes per step * steps / launches)
     elem = L * batch * n
-    alg_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb}
-    dom = max(kernels, key=lambda k: (kernels[k]["avg_ms"] or 0.0))
+    step_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb}
+    dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
     dom_ms = kernels[dom]["avg_ms"]
+    alg_bytes = {k: step_bytes[k] * args.steps / max(kernels[k]["launches"], 1) for k in kernels}
     achieved = alg_bytes[dom] / (dom_ms * 1e-3) / 1e9
     traffic = None
     tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")

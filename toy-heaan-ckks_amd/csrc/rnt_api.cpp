@@ -8,6 +8,7 @@
 #include <cinttypes>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -294,6 +295,13 @@ int build_tables(rnt::Tables* t) {
     c.c1r_p = (W)shoup_companion(ninvr, q, wbits);
     c.c2r = (W)mulmod(w1, ninvr, q);
     c.c2r_p = (W)shoup_companion(c.c2r, q, wbits);
+    {
+      // q = k * 2^s + 1; the 32-bit path uses s capped so that 32 - s <= 24
+      unsigned sh = (unsigned)__builtin_ctzll(q - 1);
+      if (sh > 31) sh = 31;
+      c.s = (W)sh;
+      c.k = (W)((q - 1) >> sh);
+    }
     for (size_t i = 0; i < l; ++i) {
       const uint64_t qi = t->moduli[i];
       const uint64_t inv = invmod(q % qi, qi);
@@ -610,6 +618,21 @@ extern "C" int rnt_ntt_inv(rnt_buf* b) {
   return RNT_OK;
 }
 
+// Polys per launch chunk of the coefficient-domain product.  0 / unset
+// RNT_MUL_CHUNK_MB: whole batch; otherwise chunks of about that many MiB of
+// a-operand data (experiment knob for Infinity-Cache residency).
+static size_t mul_chunk(const rnt::Tables* t, size_t L, size_t B) {
+  static const long mb = [] {
+    const char* e = getenv("RNT_MUL_CHUNK_MB");
+    return e ? atol(e) : 0L;
+  }();
+  if (mb <= 0) return B;
+  const size_t per = L * t->n * (t->wide ? 8 : 4);
+  size_t c = ((size_t)mb << 20) / (per ? per : 1);
+  if (c < 1) c = 1;
+  return std::min(c, B);
+}
+
 extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   if (int rc = check_buf(out, "rnt_mul")) return rc;
   if (int rc = check_buf(a, "rnt_mul")) return rc;
@@ -625,13 +648,27 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
     out->in_ntt = 1;
     return RNT_OK;
   }
-  // poly.rs:307-329: fwd(a), fwd(b), pointwise, inv -- three fused launches
+  // poly.rs:307-329: fwd(a), fwd(b), pointwise, inv -- three fused launches,
+  // issued per chunk of polys so a chunk's intermediates can stay resident
+  // in the Infinity Cache between the launches.
   const uint64_t ls = limb_stride(out);
   const size_t wb = word_bytes(k.t);
   if (int rc = ensure_ws(out, poly_words(out) * wb)) return rc;
-  LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, out->data, a->data, out->ws, b->data, ls, ls), "column forward");
-  LAUNCH(k.t, rnt::K_ROW_MUL, rnt::launch_row(k, 2, out->data, out->ws, ls), "row mul");
-  LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, out->data, ls, out->data, ls, 1, nullptr), "column inverse");
+  const size_t B = out->n_polys;
+  const size_t bc = mul_chunk(k.t, k.L, B);
+  const size_t n = k.t->n;
+  for (size_t p0 = 0; p0 < B; p0 += bc) {
+    rnt::Launch kc = k;
+    kc.B = std::min(bc, B - p0);
+    const size_t off = p0 * n * wb;
+    char* o = (char*)out->data + off;
+    char* w = (char*)out->ws + off;
+    const char* pa = (const char*)a->data + off;
+    const char* pb = (const char*)b->data + off;
+    LAUNCH(kc.t, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, o, pa, w, pb, ls, ls), "column forward");
+    LAUNCH(kc.t, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, o, w, ls), "row mul");
+    LAUNCH(kc.t, rnt::K_COL_INV, rnt::launch_col_inv(kc, o, ls, o, ls, 1, nullptr), "column inverse");
+  }
   out->in_ntt = 0;
   return RNT_OK;
 }

@@ -46,6 +46,8 @@ struct LimbConst {
   W c1r_p;
   W c2r;     // psi_inv_rev[1] * n^-1 * 2^w
   W c2r_p;
+  W k;       // q = k * 2^s + 1 (32-bit path: s >= 8, see rnt_modarith.hpp)
+  W s;
 };
 
 // A twiddle and its Shoup companion, interleaved so one load fetches both.

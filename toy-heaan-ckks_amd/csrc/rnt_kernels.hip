@@ -58,6 +58,11 @@ static TabPtrs<W> tab_ptrs(const Tables* t) {
   return p;
 }
 
+template <class W>
+__device__ __forceinline__ Mod<W> mod_of(const LimbConst<W>& lc) {
+  return Mod<W>{lc.q, (W)(W(0) - lc.q)};
+}
+
 Geom geom_for(uint32_t log_n) {
   Geom g;
   g.log_n = log_n;
@@ -68,8 +73,10 @@ Geom geom_for(uint32_t log_n) {
     g.log_r = log_n - 4;
     g.log_c = 4;
   } else {
-    g.log_r = 4;
-    g.log_c = log_n - 4;
+    // balance the stages between the (memory-bound) column passes and the
+    // (ALU-bound) row pass: R = 2^floor(log_n / 2), at least 16
+    g.log_r = log_n / 2 > 4 ? log_n / 2 : 4;
+    g.log_c = log_n - g.log_r;
   }
   g.n = (size_t)1 << log_n;
   g.r = (size_t)1 << g.log_r;
@@ -82,7 +89,7 @@ Geom geom_for(uint32_t log_n) {
 // ---------------------------------------------------------------------------
 
 template <class W, int LOG_R>
-__device__ __forceinline__ void col_ct(W (&x)[1 << LOG_R], const Tw<W>* tw, W q) {
+__device__ __forceinline__ void col_ct(W (&x)[1 << LOG_R], const Tw<W>* tw, const Mod<W>& m) {
   constexpr int R = 1 << LOG_R;
 #pragma unroll
   for (int k = 0; k < LOG_R; ++k) {
@@ -91,7 +98,11 @@ __device__ __forceinline__ void col_ct(W (&x)[1 << LOG_R], const Tw<W>* tw, W q)
     for (int i = 0; i < R; ++i) {
       if (i & d) continue;
       const Tw<W> t = tw[(1 << k) + (i >> (LOG_R - k))];
-      ct_bfly<W>(x[i], x[i + d], t.w, t.p, q);
+      // outputs that the next stage only multiplies stay unreduced
+      if (k + 1 < LOG_R && (i & (d >> 1)))
+        ct_bfly_lazy<W>(x[i], x[i + d], t.w, t.p, m);
+      else
+        ct_bfly<W>(x[i], x[i + d], t.w, t.p, m);
     }
   }
 }
@@ -99,8 +110,9 @@ __device__ __forceinline__ void col_ct(W (&x)[1 << LOG_R], const Tw<W>* tw, W q)
 // x <- GS network over the column with the last (distance N/2) stage scaled
 // by c1 (upper) and c2 (lower).
 template <class W, int LOG_R>
-__device__ __forceinline__ void col_gs(W (&x)[1 << LOG_R], const Tw<W>* itw, W q, W c1, W c1p,
-                                       W c2, W c2p) {
+__device__ __forceinline__ void col_gs(W (&x)[1 << LOG_R], const Tw<W>* itw, const Mod<W>& m,
+                                       W c1, W c1p, W c2, W c2p) {
+  const W q = m.q;
   constexpr int R = 1 << LOG_R;
 #pragma unroll
   for (int sl = 0; sl < LOG_R; ++sl) {
@@ -110,15 +122,15 @@ __device__ __forceinline__ void col_gs(W (&x)[1 << LOG_R], const Tw<W>* itw, W q
       if (i & d) continue;
       if (sl == LOG_R - 1) {
         W u = x[i], v = x[i + d];
-        x[i] = shoup_mul<W>(u + v, c1, c1p, q);
-        x[i + d] = shoup_mul<W>(u - v + q, c2, c2p, q);
+        x[i] = shoup_mul<W>(u + v, c1, c1p, m);
+        x[i + d] = shoup_mul<W>(u - v + q, c2, c2p, m);
       } else {
         const Tw<W> t = itw[(1 << (LOG_R - 1 - sl)) + (i >> (sl + 1))];
-        gs_bfly<W>(x[i], x[i + d], t.w, t.p, q);
+        gs_bfly<W>(x[i], x[i + d], t.w, t.p, m);
       }
     }
   }
-  if (LOG_R == 0) x[0] = shoup_mul<W>(x[0], c1, c1p, q);
+  if (LOG_R == 0) x[0] = shoup_mul<W>(x[0], c1, c1p, m);
 }
 
 // Forward column pass.  Thread = (limb l, poly p, column j1); j1 fastest.
@@ -138,19 +150,19 @@ k_col_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t 
   const uint32_t p = (uint32_t)(lp - (uint64_t)l * B);
   const uint64_t ib = (uint64_t)l * in_ls + (uint64_t)p * N + j1;
   const uint64_t ob = (uint64_t)l * out_ls + (uint64_t)p * N + j1;
-  const W q = tp.lc[l].q;
+  const Mod<W> m = mod_of(tp.lc[l]);
   const Tw<W>* tw = tp.tw + (uint64_t)l * N;
   W x[R];
   if (in1 != nullptr) {
 #pragma unroll
     for (int i = 0; i < R; ++i) x[i] = in1[ib + (uint64_t)i * C];
-    col_ct<W, LOG_R>(x, tw, q);
+    col_ct<W, LOG_R>(x, tw, m);
 #pragma unroll
     for (int i = 0; i < R; ++i) out1[ob + (uint64_t)i * C] = x[i];
   }
 #pragma unroll
   for (int i = 0; i < R; ++i) x[i] = in0[ib + (uint64_t)i * C];
-  col_ct<W, LOG_R>(x, tw, q);
+  col_ct<W, LOG_R>(x, tw, m);
 #pragma unroll
   for (int i = 0; i < R; ++i) out0[ob + (uint64_t)i * C] = x[i];
 }
@@ -176,9 +188,9 @@ k_col_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, u
 #pragma unroll
   for (int i = 0; i < R; ++i) x[i] = in[ib + (uint64_t)i * C];
   if (rfold)
-    col_gs<W, LOG_R>(x, itw, lc.q, lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p);
+    col_gs<W, LOG_R>(x, itw, mod_of(lc), lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p);
   else
-    col_gs<W, LOG_R>(x, itw, lc.q, lc.c1, lc.c1_p, lc.c2, lc.c2_p);
+    col_gs<W, LOG_R>(x, itw, mod_of(lc), lc.c1, lc.c1_p, lc.c2, lc.c2_p);
   if (addend != nullptr) {
 #pragma unroll
     for (int i = 0; i < R; ++i) x[i] = add_mod<W>(x[i], addend[base + (uint64_t)i * C], lc.q);
@@ -213,7 +225,7 @@ k_ks_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32
   W x[R];
 #pragma unroll
   for (int t = 0; t < R; ++t) x[t] = shoup_mul<W>(d[src + (uint64_t)t * C], (W)1, lc.one_p, lc.q);
-  col_ct<W, LOG_R>(x, tw, lc.q);
+  col_ct<W, LOG_R>(x, tw, mod_of(lc));
 #pragma unroll
   for (int t = 0; t < R; ++t) S[dst + (uint64_t)t * C] = x[t];
 }
@@ -222,53 +234,86 @@ k_ks_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32
 // row passes
 // ---------------------------------------------------------------------------
 
-// Compile-time row geometry.  A row of C = 2^LOG_C words is held by T
-// threads with E = 2^LOGE registers each.  Passes run from the top bits
-// down: full radix-16 passes on bits [bb, bb+4), then (if LOG_C % 4) a
-// partial pass on bits [0, REM) with register bits [0, 4).  Tiny rows
-// (LOG_C < 4) are one thread holding the whole row.
-template <int LOG_C>
-struct RowGeo {
-  static constexpr int LOGC = LOG_C;
-  static constexpr int LOGE = LOG_C >= 4 ? 4 : LOG_C;
+// Radix-16 pass schedule of one transform of length 2^LOGX held by T
+// threads x E registers.  Passes run from the top bits down: full radix-16
+// passes on bits [bb, bb+4), then (if LOGX % 4) a partial pass on bits
+// [0, REM) with register bits [0, 4).  LOGX < 4: one thread holds it all.
+template <int LOGX>
+struct PassSched {
+  static constexpr int LOGX_ = LOGX;
+  static constexpr int LOGE = LOGX >= 4 ? 4 : LOGX;
   static constexpr int E = 1 << LOGE;
-  static constexpr int LOG_T = LOG_C - LOGE;
+  static constexpr int LOG_T = LOGX - LOGE;
   static constexpr int T = 1 << LOG_T;
-  static constexpr int C = 1 << LOG_C;
-  static constexpr int PADC = C + (C >> 4);
-  static constexpr int THREADS = T > kRowThreads ? T : kRowThreads;
-  static constexpr int RPW = THREADS / T;  // rows per workgroup
-  static constexpr int FULL = LOGE == 4 ? LOG_C / 4 : 0;
-  static constexpr int REM = LOGE == 4 ? LOG_C % 4 : LOG_C;
+  static constexpr int X = 1 << LOGX;
+  static constexpr int FULL = LOGE == 4 ? LOGX / 4 : 0;
+  static constexpr int REM = LOGE == 4 ? LOGX % 4 : LOGX;
   static constexpr int P = FULL + (REM ? 1 : 0);
-  static constexpr int bb(int p) { return (p >= 0 && p < FULL) ? LOG_C - 4 * (p + 1) : 0; }
+  static constexpr int bb(int p) { return (p >= 0 && p < FULL) ? LOGX - 4 * (p + 1) : 0; }
   static constexpr int k(int p) { return p < FULL ? 4 : REM; }
   static constexpr int BB0 = bb(0);
   static constexpr int BBL = bb(P - 1);
-  // row-local index of register i in the distribution with register bits
-  // [bb, bb+LOGE): base(tau) | (i << bb)
+  // transform-local index of register i in the distribution with register
+  // bits [b, b+LOGE): base(tau, b) | (i << b)
   __device__ static __forceinline__ uint32_t base(uint32_t tau, int b) {
     const uint32_t lowmask = (1u << b) - 1u;
     return (tau & lowmask) | ((tau >> b) << (b + LOGE));
   }
-  // padded LDS offset: swz(base | (i<<b)) = swz(base) + (i<<b) + ((i<<b)>>4)
-  // (base has zero bits in [b, b+LOGE), so no carries)
-  __device__ static __forceinline__ uint32_t swz(uint32_t j) { return j + (j >> 4); }
-  static constexpr uint32_t ioff(int i, int b) { return ((uint32_t)i << b) + (((uint32_t)i << b) >> 4); }
 };
 
-// Load CNT consecutive twiddle pairs starting at a CNT-aligned node.
-template <class W, int CNT>
-__device__ __forceinline__ void load_tw(Tw<W> (&t)[CNT], const Tw<W>* p) {
-#pragma unroll
-  for (int m = 0; m < CNT; ++m) t[m] = p[m];
-}
+// Rows: RPW rows of C = 2^LOG_C contiguous words per workgroup; each row has
+// its own LDS region with a 1-in-16 pad.  swz(base | (i<<b)) =
+// swz(base) + (i<<b) + ((i<<b)>>4) because base has zero bits in [b, b+4).
+template <int LOG_C>
+struct RowGeo : PassSched<LOG_C> {
+  using S = PassSched<LOG_C>;
+  static constexpr int LOGC = LOG_C;
+  static constexpr int C = 1 << LOG_C;
+  static constexpr int PADC = C + (C >> 4);
+  static constexpr int THREADS = S::T > kRowThreads ? S::T : kRowThreads;
+  static constexpr int RPW = THREADS / S::T;  // rows per workgroup
+  static constexpr int REGION = RPW * PADC;   // LDS words per operand
+  __device__ static __forceinline__ uint32_t slot_of(uint32_t tid) { return tid >> S::LOG_T; }
+  __device__ static __forceinline__ uint32_t tau_of(uint32_t tid) { return tid & (S::T - 1); }
+  __device__ static __forceinline__ uint32_t lds_off(uint32_t slot, uint32_t j) {
+    return slot * PADC + j + (j >> 4);
+  }
+  static constexpr uint32_t lds_ioff(int i, int b) {
+    return ((uint32_t)i << b) + (((uint32_t)i << b) >> 4);
+  }
+};
 
-// CT stages on bits [bb, bb+K) for NOPS operands sharing twiddles.  `node0`
-// = (N + r*C + P0) where P0 = row-local index of register 0.
+// Column tiles: TC = 32 adjacent columns (128 B of u32 per row segment) of
+// a stride-C, length-R column transform per workgroup; LDS is [j][TC] so the
+// 32 lanes of a half-wave (consecutive columns) hit 32 distinct banks.
+constexpr int kLogTC = 5;
+template <int LOG_R>
+struct ColGeo : PassSched<LOG_R> {
+  using S = PassSched<LOG_R>;
+  static constexpr int TC = 1 << kLogTC;
+  static constexpr int THREADS = TC * S::T;
+  static constexpr int REGION = S::X * TC;
+  __device__ static __forceinline__ uint32_t slot_of(uint32_t tid) { return tid & (TC - 1); }
+  __device__ static __forceinline__ uint32_t tau_of(uint32_t tid) { return tid >> kLogTC; }
+  __device__ static __forceinline__ uint32_t lds_off(uint32_t slot, uint32_t j) {
+    return j * TC + slot;
+  }
+  static constexpr uint32_t lds_ioff(int i, int b) { return ((uint32_t)i << b) * TC; }
+};
+
+// Last-stage constants of the inverse network (n^-1 folded, optionally with
+// the Montgomery factor): x <- (u+v) c1, y <- (u-v) c2.
+template <class W>
+struct Fold {
+  W c1, c1p, c2, c2p;
+};
+
+// CT stages on bits [BB, BB+K) for NOPS operands sharing twiddles.  `node0`
+// = heap index base of register 0: (heap root of this transform) * 2^LOGX +
+// its transform-local index, so stage s's node is node0 >> (s+1) + (i >> ...).
 template <class W, int NOPS, int LOGE, int K, int BB>
-__device__ __forceinline__ void row_ct(W (&x)[NOPS][1 << LOGE], uint64_t node0,
-                                       const Tw<W>* tw, W q) {
+__device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint64_t node0,
+                                        const Tw<W>* tw, const Mod<W>& mo) {
   constexpr int E = 1 << LOGE;
 #pragma unroll
   for (int sl = K - 1; sl >= 0; --sl) {
@@ -284,50 +329,139 @@ __device__ __forceinline__ void row_ct(W (&x)[NOPS][1 << LOGE], uint64_t node0,
     for (int i = 0; i < E; ++i) {
       if (i & d) continue;
       const int m = i >> (sl + 1);
+      // inside a pass, outputs the next stage only multiplies stay unreduced
+      const bool lazy = sl > 0 && (i & (d >> 1));
 #pragma unroll
-      for (int o = 0; o < NOPS; ++o) ct_bfly<W>(x[o][i], x[o][i | d], t[m].w, t[m].p, q);
+      for (int o = 0; o < NOPS; ++o) {
+        if (lazy)
+          ct_bfly_lazy<W>(x[o][i], x[o][i | d], t[m].w, t[m].p, mo);
+        else
+          ct_bfly<W>(x[o][i], x[o][i | d], t[m].w, t[m].p, mo);
+      }
     }
   }
 }
 
-template <class W, int NOPS, int LOGE, int K, int BB>
-__device__ __forceinline__ void row_gs(W (&x)[NOPS][1 << LOGE], uint64_t node0,
-                                       const Tw<W>* itw, W q) {
+// GS stages; with FOLD the transform's top stage (bit LOGX-1, distance N/2
+// of the whole network) applies the folded n^-1 constants instead.
+template <class W, int NOPS, int LOGE, int K, int BB, int LOGX, bool FOLD>
+__device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint64_t node0,
+                                        const Tw<W>* itw, const Mod<W>& mo, const Fold<W>& f) {
+  const W q = mo.q;
   constexpr int E = 1 << LOGE;
 #pragma unroll
   for (int sl = 0; sl < K; ++sl) {
     constexpr int H = E > 1 ? E / 2 : 1;
+    const int d = 1 << sl;
+    if (FOLD && BB + sl + 1 == LOGX) {
+#pragma unroll
+      for (int i = 0; i < E; ++i) {
+        if (i & d) continue;
+#pragma unroll
+        for (int o = 0; o < NOPS; ++o) {
+          const W u = x[o][i], v = x[o][i | d];
+          x[o][i] = shoup_mul<W>(u + v, f.c1, f.c1p, mo);
+          x[o][i | d] = shoup_mul<W>(u - v + q, f.c2, f.c2p, mo);
+        }
+      }
+      continue;
+    }
     const int cnt = H >> sl;
     const uint64_t nb = node0 >> (BB + sl + 1);
     Tw<W> t[H];
 #pragma unroll
     for (int m = 0; m < H; ++m)
       if (m < cnt) t[m] = itw[nb + m];
-    const int d = 1 << sl;
 #pragma unroll
     for (int i = 0; i < E; ++i) {
       if (i & d) continue;
       const int m = i >> (sl + 1);
 #pragma unroll
-      for (int o = 0; o < NOPS; ++o) gs_bfly<W>(x[o][i], x[o][i | d], t[m].w, t[m].p, q);
+      for (int o = 0; o < NOPS; ++o) gs_bfly<W>(x[o][i], x[o][i | d], t[m].w, t[m].p, mo);
     }
   }
 }
 
-// Per-thread row coordinates.
-struct RowPos {
+// Move NOPS register sets from distribution BF to BT through LDS.
+template <class G, class W, int NOPS, int BF, int BT>
+__device__ __forceinline__ void xchg(W (&x)[NOPS][G::E], W* lds, uint32_t slot, uint32_t tau) {
+  const uint32_t wb = G::lds_off(slot, G::base(tau, BF));
+  const uint32_t rb = G::lds_off(slot, G::base(tau, BT));
+#pragma unroll
+  for (int o = 0; o < NOPS; ++o) {
+    W* reg = lds + o * G::REGION;
+#pragma unroll
+    for (int i = 0; i < G::E; ++i) reg[wb + G::lds_ioff(i, BF)] = x[o][i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < NOPS; ++o) {
+    const W* reg = lds + o * G::REGION;
+#pragma unroll
+    for (int i = 0; i < G::E; ++i) x[o][i] = reg[rb + G::lds_ioff(i, BT)];
+  }
+  __syncthreads();
+}
+
+// Per-thread transform coordinates: `slot` (which transform of the
+// workgroup), `tau` (thread within it), `heap` (heap index of the
+// transform's root times its length: node0 = heap + local index).
+struct XPos {
   uint32_t slot, tau;
+  uint64_t heap;
+};
+
+template <class G, class W, int NOPS, int PP>
+__device__ __forceinline__ void fwd_pass(W (&x)[NOPS][G::E], const XPos& xp, W* lds,
+                                         const Tw<W>* tw, const Mod<W>& q) {
+  constexpr int BB = G::bb(PP);
+  if constexpr (PP > 0) xchg<G, W, NOPS, G::bb(PP - 1), BB>(x, lds, xp.slot, xp.tau);
+  pass_ct<W, NOPS, G::LOGE, G::k(PP), BB>(x, xp.heap + G::base(xp.tau, BB), tw, q);
+}
+
+template <class G, class W, int NOPS, int PP, bool FOLD>
+__device__ __forceinline__ void inv_pass(W (&x)[NOPS][G::E], const XPos& xp, W* lds,
+                                         const Tw<W>* itw, const Mod<W>& q, const Fold<W>& f) {
+  constexpr int BB = G::bb(PP);
+  if constexpr (PP < G::P - 1) xchg<G, W, NOPS, G::bb(PP + 1), BB>(x, lds, xp.slot, xp.tau);
+  pass_gs<W, NOPS, G::LOGE, G::k(PP), BB, G::LOGX_, FOLD>(x, xp.heap + G::base(xp.tau, BB), itw, q,
+                                                          f);
+}
+
+// All forward passes (first-pass distribution in, last-pass out).
+template <class G, class W, int NOPS>
+__device__ __forceinline__ void xf_fwd(W (&x)[NOPS][G::E], const XPos& xp, W* lds,
+                                       const Tw<W>* tw, const Mod<W>& q) {
+  if constexpr (G::P > 0) fwd_pass<G, W, NOPS, 0>(x, xp, lds, tw, q);
+  if constexpr (G::P > 1) fwd_pass<G, W, NOPS, 1>(x, xp, lds, tw, q);
+  if constexpr (G::P > 2) fwd_pass<G, W, NOPS, 2>(x, xp, lds, tw, q);
+  if constexpr (G::P > 3) fwd_pass<G, W, NOPS, 3>(x, xp, lds, tw, q);
+}
+
+// All inverse passes (last-pass distribution in, first-pass out).
+template <class G, class W, int NOPS, bool FOLD = false>
+__device__ __forceinline__ void xf_inv(W (&x)[NOPS][G::E], const XPos& xp, W* lds,
+                                       const Tw<W>* itw, const Mod<W>& q,
+                                       const Fold<W>& f = Fold<W>{}) {
+  if constexpr (G::P > 3) inv_pass<G, W, NOPS, 3, FOLD>(x, xp, lds, itw, q, f);
+  if constexpr (G::P > 2) inv_pass<G, W, NOPS, 2, FOLD>(x, xp, lds, itw, q, f);
+  if constexpr (G::P > 1) inv_pass<G, W, NOPS, 1, FOLD>(x, xp, lds, itw, q, f);
+  if constexpr (G::P > 0) inv_pass<G, W, NOPS, 0, FOLD>(x, xp, lds, itw, q, f);
+}
+
+// Row coordinates of this thread.
+struct RowPos {
+  XPos xp;
   uint32_t l, p, r;
   bool active;
-  uint64_t gb;  // N + r*C: heap base of this row
 };
 
 template <class G>
 __device__ __forceinline__ RowPos row_pos(uint32_t log_n, uint32_t B, uint64_t rows_total) {
   RowPos rp;
-  rp.slot = threadIdx.x >> G::LOG_T;
-  rp.tau = threadIdx.x & (G::T - 1);
-  uint64_t row = (uint64_t)blockIdx.x * G::RPW + rp.slot;
+  rp.xp.slot = G::slot_of(threadIdx.x);
+  rp.xp.tau = G::tau_of(threadIdx.x);
+  uint64_t row = (uint64_t)blockIdx.x * G::RPW + rp.xp.slot;
   rp.active = row < rows_total;
   if (!rp.active) row = 0;
   const uint32_t log_r = log_n - G::LOGC;
@@ -335,68 +469,138 @@ __device__ __forceinline__ RowPos row_pos(uint32_t log_n, uint32_t B, uint64_t r
   rp.r = (uint32_t)(row & ((1u << log_r) - 1u));
   rp.l = (uint32_t)(lp / B);
   rp.p = (uint32_t)(lp - (uint64_t)rp.l * B);
-  rp.gb = (1ull << log_n) + (uint64_t)rp.r * G::C;
+  rp.xp.heap = (1ull << log_n) + (uint64_t)rp.r * G::C;  // (R + r) * C
   return rp;
 }
 
-// Move NOPS register sets from distribution BF to BT through LDS.
-template <class G, class W, int NOPS, int BF, int BT>
-__device__ __forceinline__ void row_exchange(W (&x)[NOPS][G::E], W* lds, uint32_t slot,
-                                             uint32_t tau) {
-  const uint32_t wb = G::swz(G::base(tau, BF));
-  const uint32_t rb = G::swz(G::base(tau, BT));
+// ---------------------------------------------------------------------------
+// tiled column passes (log2 R >= 5): a workgroup owns TC = 32 adjacent
+// columns of one (limb, poly) and runs the R-point network over the row
+// index j (stride C) through LDS.  The column transform is the top of the
+// heap: node0 = R + j.  Output stays in place (row j, column c).
+// ---------------------------------------------------------------------------
+
+struct ColPos {
+  XPos xp;
+  uint32_t l, p;
+  uint64_t col;
+};
+
+template <class G>
+__device__ __forceinline__ ColPos col_pos(uint64_t tile, uint32_t log_c, uint32_t B) {
+  ColPos cp;
+  cp.xp.slot = G::slot_of(threadIdx.x);
+  cp.xp.tau = G::tau_of(threadIdx.x);
+  const uint32_t tpp_log = log_c - kLogTC;  // column tiles per (limb, poly)
+  const uint64_t lp = tile >> tpp_log;
+  const uint64_t ct = tile & ((1ull << tpp_log) - 1);
+  cp.l = (uint32_t)(lp / B);
+  cp.p = (uint32_t)(lp - (uint64_t)cp.l * B);
+  cp.col = (ct << kLogTC) + cp.xp.slot;
+  cp.xp.heap = (uint64_t)G::X;
+  return cp;
+}
+
+template <class W, int LOG_R>
+__global__ void __launch_bounds__(ColGeo<LOG_R>::THREADS)
+k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t log_n,
+           uint32_t log_c, uint32_t B, uint64_t in_ls, uint64_t out_ls) {
+  using G = ColGeo<LOG_R>;
+  constexpr int E = G::E;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  W* lds = (W*)smem_raw;
+  const ColPos cp = col_pos<G>(blockIdx.x, log_c, B);
+  const uint64_t N = 1ull << log_n;
+  const uint64_t C = 1ull << log_c;
+  const uint64_t ib = (uint64_t)cp.l * in_ls + (uint64_t)cp.p * N + cp.col;
+  const uint64_t ob = (uint64_t)cp.l * out_ls + (uint64_t)cp.p * N + cp.col;
+  const uint32_t b0 = G::base(cp.xp.tau, G::BB0);
+  const uint32_t bl = G::base(cp.xp.tau, G::BBL);
+  const Tw<W>* tw = tp.tw + (uint64_t)cp.l * N;
+  const Mod<W> m = mod_of(tp.lc[cp.l]);
+  W x[1][E];
+  // operand 1 first: out0 may alias in1 (out = a * b with out == b)
+  if (in1 != nullptr) {
 #pragma unroll
-  for (int o = 0; o < NOPS; ++o) {
-    W* reg = lds + ((uint32_t)o * G::RPW + slot) * G::PADC;
+    for (int i = 0; i < E; ++i) x[0][i] = in1[ib + (uint64_t)(b0 | ((uint32_t)i << G::BB0)) * C];
+    xf_fwd<G, W, 1>(x, cp.xp, lds, tw, m);
 #pragma unroll
-    for (int i = 0; i < G::E; ++i) reg[wb + G::ioff(i, BF)] = x[o][i];
+    for (int i = 0; i < E; ++i) out1[ob + (uint64_t)(bl | ((uint32_t)i << G::BBL)) * C] = x[0][i];
   }
-  __syncthreads();
 #pragma unroll
-  for (int o = 0; o < NOPS; ++o) {
-    const W* reg = lds + ((uint32_t)o * G::RPW + slot) * G::PADC;
+  for (int i = 0; i < E; ++i) x[0][i] = in0[ib + (uint64_t)(b0 | ((uint32_t)i << G::BB0)) * C];
+  xf_fwd<G, W, 1>(x, cp.xp, lds, tw, m);
 #pragma unroll
-    for (int i = 0; i < G::E; ++i) x[o][i] = reg[rb + G::ioff(i, BT)];
+  for (int i = 0; i < E; ++i) out0[ob + (uint64_t)(bl | ((uint32_t)i << G::BBL)) * C] = x[0][i];
+}
+
+template <class W, int LOG_R>
+__global__ void __launch_bounds__(ColGeo<LOG_R>::THREADS)
+k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, uint32_t log_c,
+           uint32_t B, uint64_t in_ls, uint64_t out_ls, int rfold) {
+  using G = ColGeo<LOG_R>;
+  constexpr int E = G::E;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  W* lds = (W*)smem_raw;
+  const ColPos cp = col_pos<G>(blockIdx.x, log_c, B);
+  const uint64_t N = 1ull << log_n;
+  const uint64_t C = 1ull << log_c;
+  const uint64_t ib = (uint64_t)cp.l * in_ls + (uint64_t)cp.p * N + cp.col;
+  const uint64_t ob = (uint64_t)cp.l * out_ls + (uint64_t)cp.p * N + cp.col;
+  const uint32_t b0 = G::base(cp.xp.tau, G::BB0);
+  const uint32_t bl = G::base(cp.xp.tau, G::BBL);
+  const LimbConst<W> lc = tp.lc[cp.l];
+  const Tw<W>* itw = tp.itw + (uint64_t)cp.l * N;
+  const Fold<W> f = rfold ? Fold<W>{lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p}
+                          : Fold<W>{lc.c1, lc.c1_p, lc.c2, lc.c2_p};
+  W x[1][E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) x[0][i] = in[ib + (uint64_t)(bl | ((uint32_t)i << G::BBL)) * C];
+  xf_inv<G, W, 1, true>(x, cp.xp, lds, itw, mod_of(lc), f);
+  if (addend != nullptr) {
+#pragma unroll
+    for (int i = 0; i < E; ++i)
+      x[0][i] = add_mod<W>(x[0][i], addend[ob + (uint64_t)(b0 | ((uint32_t)i << G::BB0)) * C], lc.q);
   }
-  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < E; ++i) out[ob + (uint64_t)(b0 | ((uint32_t)i << G::BB0)) * C] = x[0][i];
 }
 
-// Forward pass p (with the exchange from pass p-1's distribution).
-template <class G, class W, int NOPS, int PP>
-__device__ __forceinline__ void fwd_pass(W (&x)[NOPS][G::E], const RowPos& rp, W* lds,
-                                         const Tw<W>* tw, W q) {
-  constexpr int BB = G::bb(PP);
-  if constexpr (PP > 0) row_exchange<G, W, NOPS, G::bb(PP - 1), BB>(x, lds, rp.slot, rp.tau);
-  row_ct<W, NOPS, G::LOGE, G::k(PP), BB>(x, rp.gb + G::base(rp.tau, BB), tw, q);
-}
-
-template <class G, class W, int NOPS, int PP>
-__device__ __forceinline__ void inv_pass(W (&x)[NOPS][G::E], const RowPos& rp, W* lds,
-                                         const Tw<W>* itw, W q) {
-  constexpr int BB = G::bb(PP);
-  if constexpr (PP < G::P - 1) row_exchange<G, W, NOPS, G::bb(PP + 1), BB>(x, lds, rp.slot, rp.tau);
-  row_gs<W, NOPS, G::LOGE, G::k(PP), BB>(x, rp.gb + G::base(rp.tau, BB), itw, q);
-}
-
-// All forward row passes on NOPS operands loaded in the first-pass
-// distribution; leaves the registers in the last-pass distribution.
-template <class G, class W, int NOPS>
-__device__ __forceinline__ void rows_fwd(W (&x)[NOPS][G::E], const RowPos& rp, W* lds,
-                                         const Tw<W>* tw, W q) {
-  if constexpr (G::P > 0) fwd_pass<G, W, NOPS, 0>(x, rp, lds, tw, q);
-  if constexpr (G::P > 1) fwd_pass<G, W, NOPS, 1>(x, rp, lds, tw, q);
-  if constexpr (G::P > 2) fwd_pass<G, W, NOPS, 2>(x, rp, lds, tw, q);
-  if constexpr (G::P > 3) fwd_pass<G, W, NOPS, 3>(x, rp, lds, tw, q);
-}
-
-// All inverse row passes; last-pass distribution in, first-pass out.
-template <class G, class W, int NOPS>
-__device__ __forceinline__ void rows_inv(W (&x)[NOPS][G::E], const RowPos& rp, W* lds,
-                                         const Tw<W>* itw, W q) {
-  if constexpr (G::P > 3) inv_pass<G, W, NOPS, 3>(x, rp, lds, itw, q);
-  if constexpr (G::P > 2) inv_pass<G, W, NOPS, 2>(x, rp, lds, itw, q);
-  if constexpr (G::P > 1) inv_pass<G, W, NOPS, 1>(x, rp, lds, itw, q);
-  if constexpr (G::P > 0) inv_pass<G, W, NOPS, 0>(x, rp, lds, itw, q);
+// Tiled key-switch decomposition: tile = (((j*L + i)*B + p), column tile).
+template <class W, int LOG_R>
+__global__ void __launch_bounds__(ColGeo<LOG_R>::THREADS)
+k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32_t log_n,
+                 uint32_t log_c, uint32_t L, uint32_t B, uint64_t d_ls) {
+  using G = ColGeo<LOG_R>;
+  constexpr int E = G::E;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  W* lds = (W*)smem_raw;
+  const uint64_t N = 1ull << log_n;
+  const uint64_t C = 1ull << log_c;
+  const uint32_t tpp_log = log_c - kLogTC;
+  uint64_t rest = (uint64_t)blockIdx.x >> tpp_log;  // (j*L + i)*B + p
+  const uint64_t ct = (uint64_t)blockIdx.x & ((1ull << tpp_log) - 1);
+  const uint32_t p = (uint32_t)(rest % B);
+  rest /= B;
+  const uint32_t i = (uint32_t)(rest % L);
+  const uint32_t j = (uint32_t)(rest / L);
+  XPos xp;
+  xp.slot = G::slot_of(threadIdx.x);
+  xp.tau = G::tau_of(threadIdx.x);
+  xp.heap = (uint64_t)G::X;
+  const uint64_t col = (ct << kLogTC) + xp.slot;
+  const uint64_t src = (uint64_t)i * d_ls + (uint64_t)p * N + col;
+  const uint64_t dst = (((uint64_t)j * L + i) * B + p) * N + col;
+  const uint32_t b0 = G::base(xp.tau, G::BB0);
+  const uint32_t bl = G::base(xp.tau, G::BBL);
+  const LimbConst<W> lc = tp.lc[j];
+  W x[1][E];
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    x[0][e] = shoup_mul<W>(d[src + (uint64_t)(b0 | ((uint32_t)e << G::BB0)) * C], (W)1, lc.one_p, lc.q);
+  xf_fwd<G, W, 1>(x, xp, lds, tp.tw + (uint64_t)j * N, mod_of(lc));
+#pragma unroll
+  for (int e = 0; e < E; ++e) S[dst + (uint64_t)(bl | ((uint32_t)e << G::BBL)) * C] = x[0][e];
 }
 
 // mode 0: forward rows in place; 1: inverse rows in place;
@@ -415,8 +619,8 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
   const LimbConst<W> lc = tp.lc[rp.l];
   const Tw<W>* tw = tp.tw + (uint64_t)rp.l * N;
   const Tw<W>* itw = tp.itw + (uint64_t)rp.l * N;
-  const uint32_t b0 = G::base(rp.tau, G::BB0);
-  const uint32_t bl = G::base(rp.tau, G::BBL);
+  const uint32_t b0 = G::base(rp.xp.tau, G::BB0);
+  const uint32_t bl = G::base(rp.xp.tau, G::BBL);
   if constexpr (MODE == 2) {
     W v[2][E];
 #pragma unroll
@@ -424,11 +628,11 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
       v[0][i] = xg[base + b0 + ((uint32_t)i << G::BB0)];
       v[1][i] = yg[base + b0 + ((uint32_t)i << G::BB0)];
     }
-    rows_fwd<G, W, 2>(v, rp, lds, tw, lc.q);
+    xf_fwd<G, W, 2>(v, rp.xp, lds, tw, mod_of(lc));
     W z[1][E];
 #pragma unroll
     for (int i = 0; i < E; ++i) z[0][i] = mont_mul<W>(v[0][i], v[1][i], lc.q, lc.qinv);
-    rows_inv<G, W, 1>(z, rp, lds, itw, lc.q);
+    xf_inv<G, W, 1>(z, rp.xp, lds, itw, mod_of(lc));
     if (rp.active) {
 #pragma unroll
       for (int i = 0; i < E; ++i) xg[base + b0 + ((uint32_t)i << G::BB0)] = z[0][i];
@@ -437,7 +641,7 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
     W v[1][E];
 #pragma unroll
     for (int i = 0; i < E; ++i) v[0][i] = xg[base + b0 + ((uint32_t)i << G::BB0)];
-    rows_fwd<G, W, 1>(v, rp, lds, tw, lc.q);
+    xf_fwd<G, W, 1>(v, rp.xp, lds, tw, mod_of(lc));
     if (rp.active) {
 #pragma unroll
       for (int i = 0; i < E; ++i) xg[base + bl + ((uint32_t)i << G::BBL)] = v[0][i];
@@ -446,7 +650,7 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
     W v[1][E];
 #pragma unroll
     for (int i = 0; i < E; ++i) v[0][i] = xg[base + bl + ((uint32_t)i << G::BBL)];
-    rows_inv<G, W, 1>(v, rp, lds, itw, lc.q);
+    xf_inv<G, W, 1>(v, rp.xp, lds, itw, mod_of(lc));
     if (rp.active) {
 #pragma unroll
       for (int i = 0; i < E; ++i) xg[base + b0 + ((uint32_t)i << G::BB0)] = v[0][i];
@@ -477,8 +681,8 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   const LimbConst<W> lc = tp.lc[j];
   const Tw<W>* tw = tp.tw + (uint64_t)j * N;
   const Tw<W>* itw = tp.itw + (uint64_t)j * N;
-  const uint32_t b0 = G::base(rp.tau, G::BB0);
-  const uint32_t bl = G::base(rp.tau, G::BBL);
+  const uint32_t b0 = G::base(rp.xp.tau, G::BB0);
+  const uint32_t bl = G::base(rp.xp.tau, G::BBL);
   W acc[2][E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -491,7 +695,7 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     W x[1][E];
 #pragma unroll
     for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
-    rows_fwd<G, W, 1>(x, rp, lds, tw, lc.q);
+    xf_fwd<G, W, 1>(x, rp.xp, lds, tw, mod_of(lc));
     // key poly i, limb j (key buffers hold L polys: limb stride key_ls)
     const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + rowoff;
 #pragma unroll
@@ -503,7 +707,7 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
       acc[1][e] = add_mod<W>(acc[1][e], mont_mul<W>(x[0][e], ka, lc.q, lc.qinv), lc.q);
     }
   }
-  rows_inv<G, W, 2>(acc, rp, lds, itw, lc.q);
+  xf_inv<G, W, 2>(acc, rp.xp, lds, itw, mod_of(lc));
   if (rp.active) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -535,8 +739,8 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
   const LimbConst<W> lc = tp.lc[rp.l];
   const Tw<W>* tw = tp.tw + (uint64_t)rp.l * N;
   const Tw<W>* itw = tp.itw + (uint64_t)rp.l * N;
-  const uint32_t b0 = G::base(rp.tau, G::BB0);
-  const uint32_t bl = G::base(rp.tau, G::BBL);
+  const uint32_t b0 = G::base(rp.xp.tau, G::BB0);
+  const uint32_t bl = G::base(rp.xp.tau, G::BBL);
   W a[2][E], b[2][E];
 #pragma unroll
   for (int i = 0; i < E; ++i) {
@@ -544,14 +748,14 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
     a[0][i] = c0[base + e];
     a[1][i] = c1[base + e];
   }
-  rows_fwd<G, W, 2>(a, rp, lds, tw, lc.q);
+  xf_fwd<G, W, 2>(a, rp.xp, lds, tw, mod_of(lc));
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const uint32_t e = b0 + ((uint32_t)i << G::BB0);
     b[0][i] = c0p[base + e];
     b[1][i] = c1p[base + e];
   }
-  rows_fwd<G, W, 2>(b, rp, lds, tw, lc.q);
+  xf_fwd<G, W, 2>(b, rp.xp, lds, tw, mod_of(lc));
   W d2[1][E];
 #pragma unroll
   for (int i = 0; i < E; ++i) {
@@ -566,7 +770,7 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
       d1hat[base + pos] = d1;
     }
   }
-  rows_inv<G, W, 1>(d2, rp, lds, itw, lc.q);
+  xf_inv<G, W, 1>(d2, rp.xp, lds, itw, mod_of(lc));
   if (rp.active) {
 #pragma unroll
     for (int i = 0; i < E; ++i) d2row[base + b0 + ((uint32_t)i << G::BB0)] = d2[0][i];
@@ -785,10 +989,6 @@ static hipError_t allow_lds(K kernel, size_t bytes) {
     case 7: MACRO(7);                  \
     case 8: MACRO(8);                  \
     case 9: MACRO(9);                  \
-    case 10: MACRO(10);                \
-    case 11: MACRO(11);                \
-    case 12: MACRO(12);                \
-    case 13: MACRO(13);                \
     default: return hipErrorInvalidValue; \
   }
 
@@ -798,13 +998,40 @@ static size_t row_lds(int nops) {
   return (size_t)nops * G::RPW * G::PADC * sizeof(W);
 }
 
+#define RNT_DISPATCH_LOGRT(LOGR, MACRO) \
+  switch (LOGR) {                       \
+    case 5: MACRO(5); break;            \
+    case 6: MACRO(6); break;            \
+    case 7: MACRO(7); break;            \
+    case 8: MACRO(8); break;            \
+    default: return hipErrorInvalidValue; \
+  }
+
+template <class W, int LOG_R>
+static size_t col_lds() {
+  return (size_t)ColGeo<LOG_R>::REGION * sizeof(W);
+}
+
 template <class W>
 static hipError_t col_fwd_t(const Launch& k, void* out0, const void* in0, void* out1,
                             const void* in1, uint64_t in_ls, uint64_t out_ls) {
   const Geom g = geom_for(k.t->log_n);
-  const uint64_t total = (uint64_t)k.L * k.B * g.c;
   const TabPtrs<W> tp = tab_ptrs<W>(k.t);
-  if (total == 0) return hipSuccess;
+  if ((uint64_t)k.L * k.B == 0) return hipSuccess;
+  if (g.log_r >= 5) {
+    const uint64_t tiles = ((uint64_t)k.L * k.B) << (g.log_c - kLogTC);
+    hipError_t e = hipSuccess;
+#define RNT_L(R)                                                                               \
+  e = allow_lds(k_colt_fwd<W, R>, col_lds<W, R>());                                             \
+  if (e != hipSuccess) return e;                                                               \
+  hipLaunchKernelGGL((k_colt_fwd<W, R>), dim3((unsigned)tiles), dim3(ColGeo<R>::THREADS),      \
+                     (col_lds<W, R>()), k.s, (W*)out0, (const W*)in0, (W*)out1, (const W*)in1, tp, \
+                     g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls)
+    RNT_DISPATCH_LOGRT(g.log_r, RNT_L)
+#undef RNT_L
+    return hipGetLastError();
+  }
+  const uint64_t total = (uint64_t)k.L * k.B * g.c;
 #define RNT_L(R)                                                                              \
   hipLaunchKernelGGL((k_col_fwd<W, R>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,      \
                      (W*)out0, (const W*)in0, (W*)out1, (const W*)in1, tp, g.log_n, g.log_c, \
@@ -818,9 +1045,22 @@ template <class W>
 static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const void* in,
                             uint64_t in_ls, int rfold, const void* addend) {
   const Geom g = geom_for(k.t->log_n);
-  const uint64_t total = (uint64_t)k.L * k.B * g.c;
   const TabPtrs<W> tp = tab_ptrs<W>(k.t);
-  if (total == 0) return hipSuccess;
+  if ((uint64_t)k.L * k.B == 0) return hipSuccess;
+  if (g.log_r >= 5) {
+    const uint64_t tiles = ((uint64_t)k.L * k.B) << (g.log_c - kLogTC);
+    hipError_t e = hipSuccess;
+#define RNT_L(R)                                                                            \
+  e = allow_lds(k_colt_inv<W, R>, col_lds<W, R>());                                          \
+  if (e != hipSuccess) return e;                                                            \
+  hipLaunchKernelGGL((k_colt_inv<W, R>), dim3((unsigned)tiles), dim3(ColGeo<R>::THREADS),   \
+                     (col_lds<W, R>()), k.s, (W*)out, (const W*)in, (const W*)addend, tp,      \
+                     g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls, rfold)
+    RNT_DISPATCH_LOGRT(g.log_r, RNT_L)
+#undef RNT_L
+    return hipGetLastError();
+  }
+  const uint64_t total = (uint64_t)k.L * k.B * g.c;
 #define RNT_L(R)                                                                          \
   hipLaunchKernelGGL((k_col_inv<W, R>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,  \
                      (W*)out, (const W*)in, (const W*)addend, tp, g.log_n, g.log_c,      \
@@ -955,9 +1195,22 @@ static hipError_t export_t(const Launch& k, uint64_t* stage, const void* src, in
 template <class W>
 static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64_t d_ls) {
   const Geom g = geom_for(k.t->log_n);
-  const uint64_t total = (uint64_t)k.L * k.L * k.B * g.c;
-  if (total == 0) return hipSuccess;
+  if ((uint64_t)k.L * k.B == 0) return hipSuccess;
   const TabPtrs<W> tp = tab_ptrs<W>(k.t);
+  if (g.log_r >= 5) {
+    const uint64_t tiles = ((uint64_t)k.L * k.L * k.B) << (g.log_c - kLogTC);
+    hipError_t e = hipSuccess;
+#define RNT_L(R)                                                                                \
+  e = allow_lds(k_colt_decompose<W, R>, col_lds<W, R>());                                        \
+  if (e != hipSuccess) return e;                                                                \
+  hipLaunchKernelGGL((k_colt_decompose<W, R>), dim3((unsigned)tiles), dim3(ColGeo<R>::THREADS), \
+                     (col_lds<W, R>()), k.s, (W*)S, (const W*)d, tp, g.log_n, g.log_c,            \
+                     (uint32_t)k.L, (uint32_t)k.B, d_ls)
+    RNT_DISPATCH_LOGRT(g.log_r, RNT_L)
+#undef RNT_L
+    return hipGetLastError();
+  }
+  const uint64_t total = (uint64_t)k.L * k.L * k.B * g.c;
 #define RNT_L(R)                                                                               \
   hipLaunchKernelGGL((k_ks_decompose<W, R>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,  \
                      (W*)S, (const W*)d, tp, g.log_n, g.log_c, (uint32_t)k.L, (uint32_t)k.B, \

@@ -59,6 +59,47 @@ __host__ __device__ __forceinline__ W shoup_mul(W x, W w, W wp, W q) {
   return csub<W>(r, q);
 }
 
+// Modulus bundle passed to the butterflies.  nq = 2^w - q (so q-multiples
+// can be subtracted by a multiply-add).
+template <class W>
+struct Mod {
+  W q;
+  W nq;
+};
+
+// gfx950 VALU rates measured by tools/oprate.hip (cycles per wave64
+// instruction per SIMD): add/sub/xor/and ~2; min/max, v_mul_lo/hi_u32,
+// v_mul_u32_u24, VOP3 shifts-adds and v_mad_u64_u32 ~4.  v_mad_u64_u32
+// yields a full 64-bit a*b+c for the price of one 32-bit multiply, so the
+// 32-bit path builds its products from it.
+__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t r, cy;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cy) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint64_t mul64(uint32_t a, uint32_t b) {
+  uint64_t r, cy;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cy) : "v"(a), "v"(b));
+  return r;
+}
+
+// Shoup product, result in [0, 2q) (not reduced):
+//   r = x*w - floor(x*w'/2^w)*q  (mod 2^w)
+__device__ __forceinline__ uint32_t shoup_lazy(uint32_t x, uint32_t w, uint32_t wp,
+                                               const Mod<uint32_t>& m) {
+  const uint32_t qh = mulhi(x, wp);
+  return (uint32_t)mad64(qh, m.nq, mul64(x, w));  // low word of x*w + qh*(2^32 - q)
+}
+__device__ __forceinline__ uint64_t shoup_lazy(uint64_t x, uint64_t w, uint64_t wp,
+                                               const Mod<uint64_t>& m) {
+  const uint64_t qh = mulhi(x, wp);
+  return x * w - qh * m.q;
+}
+template <class W>
+__device__ __forceinline__ W shoup_mul(W x, W w, W wp, const Mod<W>& m) {
+  return csub<W>(shoup_lazy(x, w, wp, m), m.q);
+}
+
 // Montgomery product a*b*2^-w mod q (a, b in [0, q)); qinv = q^-1 mod 2^w.
 template <class W>
 __host__ __device__ __forceinline__ W mont_mul(W a, W b, W q, W qinv);
@@ -66,11 +107,19 @@ __host__ __device__ __forceinline__ W mont_mul(W a, W b, W q, W qinv);
 template <>
 __host__ __device__ __forceinline__ uint32_t mont_mul<uint32_t>(uint32_t a, uint32_t b, uint32_t q,
                                                                  uint32_t qinv) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // m = -t q^-1 mod 2^32, so t + m q is a multiple of 2^32 and
+  // (t + m q) / 2^32 < q^2/2^32 + q < 2q; 3 half-rate ops + csub.
+  const uint64_t t = mul64(a, b);
+  const uint32_t m = (uint32_t)t * (0u - qinv);
+  return csub<uint32_t>((uint32_t)(mad64(m, q, t) >> 32), q);
+#else
   uint64_t t = (uint64_t)a * b;
   uint32_t m = (uint32_t)t * qinv;
   uint32_t hi = (uint32_t)(t >> 32);
   uint32_t mh = mulhi(m, q);
   return sub_mod<uint32_t>(hi, mh, q);  // (t - m q) / 2^32, exact; hi, mh < q
+#endif
 }
 
 template <>
@@ -83,21 +132,33 @@ __host__ __device__ __forceinline__ uint64_t mont_mul<uint64_t>(uint64_t a, uint
   return sub_mod<uint64_t>(hi, mh, q);
 }
 
-// CT butterfly (forward, merged twist): (x, y) -> (x + w y, x - w y)
+// CT butterfly (forward, merged twist): (x, y) -> (x + w y, x - w y).
+// x must be reduced; y may be anything < 2^w (it only feeds Shoup).
 template <class W>
-__device__ __forceinline__ void ct_bfly(W& x, W& y, W w, W wp, W q) {
-  W t = shoup_mul<W>(y, w, wp, q);
-  W u = x;
-  x = add_mod<W>(u, t, q);
-  y = sub_mod<W>(u, t, q);
+__device__ __forceinline__ void ct_bfly(W& x, W& y, W w, W wp, const Mod<W>& m) {
+  const W t = shoup_mul<W>(y, w, wp, m);
+  const W u = x;
+  x = add_mod<W>(u, t, m.q);
+  y = sub_mod<W>(u, t, m.q);
+}
+
+// Same butterfly with outputs left in [0, 2q]: used when both outputs next
+// feed Shoup as multiplicands (the "y" of the following stage), so their
+// reductions are dead work.
+template <class W>
+__device__ __forceinline__ void ct_bfly_lazy(W& x, W& y, W w, W wp, const Mod<W>& m) {
+  const W t = shoup_mul<W>(y, w, wp, m);
+  const W u = x;
+  x = u + t;
+  y = u + (m.q - t);
 }
 
 // GS butterfly (inverse): (x, y) -> (x + y, (x - y) w)
 template <class W>
-__device__ __forceinline__ void gs_bfly(W& x, W& y, W w, W wp, W q) {
-  W u = x, v = y;
-  x = add_mod<W>(u, v, q);
-  y = shoup_mul<W>(u - v + q, w, wp, q);  // u - v + q in (0, 2q): any x < 2^w is fine
+__device__ __forceinline__ void gs_bfly(W& x, W& y, W w, W wp, const Mod<W>& m) {
+  const W u = x, v = y;
+  x = add_mod<W>(u, v, m.q);
+  y = shoup_mul<W>(u - v + m.q, w, wp, m);  // u - v + q in (0, 2q): any x < 2^w is fine
 }
 
 }  // namespace rnt
