@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun call: GPU parity tests, smoke, short bench, rocprofv3 kernel
-# trace.  Every GPU step has its own time limit; a fault/abort/timeout stops
-# the script, plain test failures do not.
+# trace.  Every GPU step has its own time limit; any failing step stops the
+# script (a failed parity test may be a device fault: start nothing more).
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -12,7 +12,7 @@ step() {  # step <name> <seconds> <cmd...>
   local rc=$?
   echo "== $name rc=$rc" >&2
   tail -3 "gpurun_out/$name.out" >&2
-  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+  if [ $rc -ne 0 ]; then
     echo "stopping after $name (rc=$rc)" >&2
     tail -20 "gpurun_out/$name.err" >&2
     exit $rc

@@ -63,6 +63,60 @@ __device__ __forceinline__ Mod<W> mod_of(const LimbConst<W>& lc) {
   return Mod<W>{lc.q, (W)(W(0) - lc.q)};
 }
 
+// Buffer-resource view of a wave-uniform base (a (limb, poly) plane or a
+// limb's twiddle table): loads/stores take a 32-bit per-lane element offset
+// plus a wave-uniform one that lands in the instruction's SGPR soffset, so
+// strided column access costs no VALU address arithmetic.
+template <class W>
+struct BufView {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ BufView(const W* base, uint32_t elems)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(elems * sizeof(W)), 0x00020000)) {}
+  __device__ __forceinline__ W ld(uint32_t v, uint32_t s) const {
+    if constexpr (sizeof(W) == 4) {
+      return __builtin_amdgcn_raw_buffer_load_b32(r, v * 4u, s * 4u, 0);
+    } else {
+      return __builtin_bit_cast(W, __builtin_amdgcn_raw_buffer_load_b64(r, v * 8u, s * 8u, 0));
+    }
+  }
+  __device__ __forceinline__ void st(W x, uint32_t v, uint32_t s) const {
+    if constexpr (sizeof(W) == 4) {
+      __builtin_amdgcn_raw_buffer_store_b32(x, r, v * 4u, s * 4u, 0);
+    } else {
+      using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, x), r, v * 8u, s * 8u, 0);
+    }
+  }
+};
+
+// Twiddle sources for the pass templates: a plain pointer (row kernels,
+// whose limb may vary across a workgroup) or a buffer view of one limb's
+// table (column kernels: one limb per workgroup).
+template <class W>
+__device__ __forceinline__ Tw<W> tw_get(const Tw<W>* p, uint32_t i) {
+  return p[i];
+}
+template <class W>
+struct TwBuf {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ TwBuf(const Tw<W>* base, uint32_t n)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(n * sizeof(Tw<W>)), 0x00020000)) {}
+};
+template <class W>
+__device__ __forceinline__ Tw<W> tw_get(const TwBuf<W>& b, uint32_t i) {
+  Tw<W> t;
+  if constexpr (sizeof(W) == 4) {
+    const uint64_t v = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(b.r, i * 8u, 0, 0));
+    t.w = (uint32_t)v;
+    t.p = (uint32_t)(v >> 32);
+  } else {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(b.r, i * 16u, 0, 0);
+    t.w = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+    t.p = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+  }
+  return t;
+}
+
 Geom geom_for(uint32_t log_n) {
   Geom g;
   g.log_n = log_n;
@@ -311,19 +365,19 @@ struct Fold {
 // CT stages on bits [BB, BB+K) for NOPS operands sharing twiddles.  `node0`
 // = heap index base of register 0: (heap root of this transform) * 2^LOGX +
 // its transform-local index, so stage s's node is node0 >> (s+1) + (i >> ...).
-template <class W, int NOPS, int LOGE, int K, int BB>
-__device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint64_t node0,
-                                        const Tw<W>* tw, const Mod<W>& mo) {
+template <class W, int NOPS, int LOGE, int K, int BB, class TS>
+__device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0, const TS& tw,
+                                        const Mod<W>& mo) {
   constexpr int E = 1 << LOGE;
 #pragma unroll
   for (int sl = K - 1; sl >= 0; --sl) {
     constexpr int H = E > 1 ? E / 2 : 1;
     const int cnt = H >> sl;  // distinct twiddles at this stage
-    const uint64_t nb = node0 >> (BB + sl + 1);
+    const uint32_t nb = node0 >> (BB + sl + 1);
     Tw<W> t[H];
 #pragma unroll
     for (int m = 0; m < H; ++m)
-      if (m < cnt) t[m] = tw[nb + m];
+      if (m < cnt) t[m] = tw_get<W>(tw, nb + m);
     const int d = 1 << sl;
 #pragma unroll
     for (int i = 0; i < E; ++i) {
@@ -344,9 +398,9 @@ __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint64_t node0,
 
 // GS stages; with FOLD the transform's top stage (bit LOGX-1, distance N/2
 // of the whole network) applies the folded n^-1 constants instead.
-template <class W, int NOPS, int LOGE, int K, int BB, int LOGX, bool FOLD>
-__device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint64_t node0,
-                                        const Tw<W>* itw, const Mod<W>& mo, const Fold<W>& f) {
+template <class W, int NOPS, int LOGE, int K, int BB, int LOGX, bool FOLD, class TS>
+__device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0, const TS& itw,
+                                        const Mod<W>& mo, const Fold<W>& f) {
   const W q = mo.q;
   constexpr int E = 1 << LOGE;
 #pragma unroll
@@ -367,11 +421,11 @@ __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint64_t node0,
       continue;
     }
     const int cnt = H >> sl;
-    const uint64_t nb = node0 >> (BB + sl + 1);
+    const uint32_t nb = node0 >> (BB + sl + 1);
     Tw<W> t[H];
 #pragma unroll
     for (int m = 0; m < H; ++m)
-      if (m < cnt) t[m] = itw[nb + m];
+      if (m < cnt) t[m] = tw_get<W>(itw, nb + m);
 #pragma unroll
     for (int i = 0; i < E; ++i) {
       if (i & d) continue;
@@ -408,20 +462,20 @@ __device__ __forceinline__ void xchg(W (&x)[NOPS][G::E], W* lds, uint32_t slot, 
 // transform's root times its length: node0 = heap + local index).
 struct XPos {
   uint32_t slot, tau;
-  uint64_t heap;
+  uint32_t heap;
 };
 
-template <class G, class W, int NOPS, int PP>
-__device__ __forceinline__ void fwd_pass(W (&x)[NOPS][G::E], const XPos& xp, W* lds,
-                                         const Tw<W>* tw, const Mod<W>& q) {
+template <class G, class W, int NOPS, int PP, class TS>
+__device__ __forceinline__ void fwd_pass(W (&x)[NOPS][G::E], const XPos& xp, W* lds, const TS& tw,
+                                         const Mod<W>& q) {
   constexpr int BB = G::bb(PP);
   if constexpr (PP > 0) xchg<G, W, NOPS, G::bb(PP - 1), BB>(x, lds, xp.slot, xp.tau);
   pass_ct<W, NOPS, G::LOGE, G::k(PP), BB>(x, xp.heap + G::base(xp.tau, BB), tw, q);
 }
 
-template <class G, class W, int NOPS, int PP, bool FOLD>
-__device__ __forceinline__ void inv_pass(W (&x)[NOPS][G::E], const XPos& xp, W* lds,
-                                         const Tw<W>* itw, const Mod<W>& q, const Fold<W>& f) {
+template <class G, class W, int NOPS, int PP, bool FOLD, class TS>
+__device__ __forceinline__ void inv_pass(W (&x)[NOPS][G::E], const XPos& xp, W* lds, const TS& itw,
+                                         const Mod<W>& q, const Fold<W>& f) {
   constexpr int BB = G::bb(PP);
   if constexpr (PP < G::P - 1) xchg<G, W, NOPS, G::bb(PP + 1), BB>(x, lds, xp.slot, xp.tau);
   pass_gs<W, NOPS, G::LOGE, G::k(PP), BB, G::LOGX_, FOLD>(x, xp.heap + G::base(xp.tau, BB), itw, q,
@@ -429,9 +483,9 @@ __device__ __forceinline__ void inv_pass(W (&x)[NOPS][G::E], const XPos& xp, W* 
 }
 
 // All forward passes (first-pass distribution in, last-pass out).
-template <class G, class W, int NOPS>
-__device__ __forceinline__ void xf_fwd(W (&x)[NOPS][G::E], const XPos& xp, W* lds,
-                                       const Tw<W>* tw, const Mod<W>& q) {
+template <class G, class W, int NOPS, class TS>
+__device__ __forceinline__ void xf_fwd(W (&x)[NOPS][G::E], const XPos& xp, W* lds, const TS& tw,
+                                       const Mod<W>& q) {
   if constexpr (G::P > 0) fwd_pass<G, W, NOPS, 0>(x, xp, lds, tw, q);
   if constexpr (G::P > 1) fwd_pass<G, W, NOPS, 1>(x, xp, lds, tw, q);
   if constexpr (G::P > 2) fwd_pass<G, W, NOPS, 2>(x, xp, lds, tw, q);
@@ -439,10 +493,9 @@ __device__ __forceinline__ void xf_fwd(W (&x)[NOPS][G::E], const XPos& xp, W* ld
 }
 
 // All inverse passes (last-pass distribution in, first-pass out).
-template <class G, class W, int NOPS, bool FOLD = false>
-__device__ __forceinline__ void xf_inv(W (&x)[NOPS][G::E], const XPos& xp, W* lds,
-                                       const Tw<W>* itw, const Mod<W>& q,
-                                       const Fold<W>& f = Fold<W>{}) {
+template <class G, class W, int NOPS, bool FOLD = false, class TS>
+__device__ __forceinline__ void xf_inv(W (&x)[NOPS][G::E], const XPos& xp, W* lds, const TS& itw,
+                                       const Mod<W>& q, const Fold<W>& f = Fold<W>{}) {
   if constexpr (G::P > 3) inv_pass<G, W, NOPS, 3, FOLD>(x, xp, lds, itw, q, f);
   if constexpr (G::P > 2) inv_pass<G, W, NOPS, 2, FOLD>(x, xp, lds, itw, q, f);
   if constexpr (G::P > 1) inv_pass<G, W, NOPS, 1, FOLD>(x, xp, lds, itw, q, f);
@@ -469,7 +522,7 @@ __device__ __forceinline__ RowPos row_pos(uint32_t log_n, uint32_t B, uint64_t r
   rp.r = (uint32_t)(row & ((1u << log_r) - 1u));
   rp.l = (uint32_t)(lp / B);
   rp.p = (uint32_t)(lp - (uint64_t)rp.l * B);
-  rp.xp.heap = (1ull << log_n) + (uint64_t)rp.r * G::C;  // (R + r) * C
+  rp.xp.heap = (1u << log_n) + rp.r * (uint32_t)G::C;  // (R + r) * C
   return rp;
 }
 
@@ -483,23 +536,38 @@ __device__ __forceinline__ RowPos row_pos(uint32_t log_n, uint32_t B, uint64_t r
 struct ColPos {
   XPos xp;
   uint32_t l, p;
-  uint64_t col;
+  uint32_t col;
 };
 
+// Grid: x = poly * (C / TC) + column tile, y = limb (no integer division,
+// so limb and poly stay in SGPRs and the buffer descriptors built from them
+// are provably wave-uniform).
 template <class G>
-__device__ __forceinline__ ColPos col_pos(uint64_t tile, uint32_t log_c, uint32_t B) {
+__device__ __forceinline__ ColPos col_pos(uint32_t log_c) {
   ColPos cp;
   cp.xp.slot = G::slot_of(threadIdx.x);
   cp.xp.tau = G::tau_of(threadIdx.x);
   const uint32_t tpp_log = log_c - kLogTC;  // column tiles per (limb, poly)
-  const uint64_t lp = tile >> tpp_log;
-  const uint64_t ct = tile & ((1ull << tpp_log) - 1);
-  cp.l = (uint32_t)(lp / B);
-  cp.p = (uint32_t)(lp - (uint64_t)cp.l * B);
+  cp.l = blockIdx.y;
+  cp.p = blockIdx.x >> tpp_log;
+  const uint32_t ct = blockIdx.x & ((1u << tpp_log) - 1);
   cp.col = (ct << kLogTC) + cp.xp.slot;
-  cp.xp.heap = (uint64_t)G::X;
+  cp.xp.heap = (uint32_t)G::X;
   return cp;
 }
+
+// Per-lane element offset of register 0 and the wave-uniform register
+// stride of a column tile in distribution bits [BB, BB+LOGE).
+template <class G, int BB>
+struct ColAddr {
+  uint32_t v, s;
+  __device__ ColAddr(const ColPos& cp, uint32_t log_c)
+      : v(cp.col + (G::base(cp.xp.tau, BB) << log_c)), s(1u << (log_c + BB)) {}
+  // Opaque redefinition of the stride: stops the compiler from keeping all
+  // E soffsets (i * s) live across a transform, which spills them to VGPRs
+  // and turns every buffer op into a waterfall loop.
+  __device__ __forceinline__ void refresh() { asm volatile("" : "+s"(s)); }
+};
 
 template <class W, int LOG_R>
 __global__ void __launch_bounds__(ColGeo<LOG_R>::THREADS)
@@ -509,29 +577,32 @@ k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
-  const ColPos cp = col_pos<G>(blockIdx.x, log_c, B);
-  const uint64_t N = 1ull << log_n;
-  const uint64_t C = 1ull << log_c;
-  const uint64_t ib = (uint64_t)cp.l * in_ls + (uint64_t)cp.p * N + cp.col;
-  const uint64_t ob = (uint64_t)cp.l * out_ls + (uint64_t)cp.p * N + cp.col;
-  const uint32_t b0 = G::base(cp.xp.tau, G::BB0);
-  const uint32_t bl = G::base(cp.xp.tau, G::BBL);
-  const Tw<W>* tw = tp.tw + (uint64_t)cp.l * N;
+  const ColPos cp = col_pos<G>(log_c);
+  const uint32_t N = 1u << log_n;
+  const uint64_t ip = (uint64_t)cp.l * in_ls + (uint64_t)cp.p * N;
+  const uint64_t op = (uint64_t)cp.l * out_ls + (uint64_t)cp.p * N;
+  ColAddr<G, G::BB0> a0(cp, log_c);
+  ColAddr<G, G::BBL> al(cp, log_c);
+  const TwBuf<W> tw(tp.tw + (uint64_t)cp.l * N, N);
   const Mod<W> m = mod_of(tp.lc[cp.l]);
   W x[1][E];
   // operand 1 first: out0 may alias in1 (out = a * b with out == b)
   if (in1 != nullptr) {
+    const BufView<W> src(in1 + ip, N), dst(out1 + op, N);
 #pragma unroll
-    for (int i = 0; i < E; ++i) x[0][i] = in1[ib + (uint64_t)(b0 | ((uint32_t)i << G::BB0)) * C];
+    for (int i = 0; i < E; ++i) x[0][i] = src.ld(a0.v, i * a0.s);
     xf_fwd<G, W, 1>(x, cp.xp, lds, tw, m);
 #pragma unroll
-    for (int i = 0; i < E; ++i) out1[ob + (uint64_t)(bl | ((uint32_t)i << G::BBL)) * C] = x[0][i];
+    for (int i = 0; i < E; ++i) dst.st(x[0][i], al.v, i * al.s);
+    a0.refresh();
+    al.refresh();
   }
+  const BufView<W> src(in0 + ip, N), dst(out0 + op, N);
 #pragma unroll
-  for (int i = 0; i < E; ++i) x[0][i] = in0[ib + (uint64_t)(b0 | ((uint32_t)i << G::BB0)) * C];
+  for (int i = 0; i < E; ++i) x[0][i] = src.ld(a0.v, i * a0.s);
   xf_fwd<G, W, 1>(x, cp.xp, lds, tw, m);
 #pragma unroll
-  for (int i = 0; i < E; ++i) out0[ob + (uint64_t)(bl | ((uint32_t)i << G::BBL)) * C] = x[0][i];
+  for (int i = 0; i < E; ++i) dst.st(x[0][i], al.v, i * al.s);
 }
 
 template <class W, int LOG_R>
@@ -542,31 +613,34 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
-  const ColPos cp = col_pos<G>(blockIdx.x, log_c, B);
-  const uint64_t N = 1ull << log_n;
-  const uint64_t C = 1ull << log_c;
-  const uint64_t ib = (uint64_t)cp.l * in_ls + (uint64_t)cp.p * N + cp.col;
-  const uint64_t ob = (uint64_t)cp.l * out_ls + (uint64_t)cp.p * N + cp.col;
-  const uint32_t b0 = G::base(cp.xp.tau, G::BB0);
-  const uint32_t bl = G::base(cp.xp.tau, G::BBL);
+  const ColPos cp = col_pos<G>(log_c);
+  const uint32_t N = 1u << log_n;
+  const uint64_t ip = (uint64_t)cp.l * in_ls + (uint64_t)cp.p * N;
+  const uint64_t op = (uint64_t)cp.l * out_ls + (uint64_t)cp.p * N;
+  ColAddr<G, G::BB0> a0(cp, log_c);
+  const ColAddr<G, G::BBL> al(cp, log_c);
   const LimbConst<W> lc = tp.lc[cp.l];
-  const Tw<W>* itw = tp.itw + (uint64_t)cp.l * N;
+  const TwBuf<W> itw(tp.itw + (uint64_t)cp.l * N, N);
   const Fold<W> f = rfold ? Fold<W>{lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p}
                           : Fold<W>{lc.c1, lc.c1_p, lc.c2, lc.c2_p};
+  const BufView<W> src(in + ip, N), dst(out + op, N);
   W x[1][E];
 #pragma unroll
-  for (int i = 0; i < E; ++i) x[0][i] = in[ib + (uint64_t)(bl | ((uint32_t)i << G::BBL)) * C];
+  for (int i = 0; i < E; ++i) x[0][i] = src.ld(al.v, i * al.s);
   xf_inv<G, W, 1, true>(x, cp.xp, lds, itw, mod_of(lc), f);
+  a0.refresh();
   if (addend != nullptr) {
+    const BufView<W> ad(addend + op, N);
 #pragma unroll
-    for (int i = 0; i < E; ++i)
-      x[0][i] = add_mod<W>(x[0][i], addend[ob + (uint64_t)(b0 | ((uint32_t)i << G::BB0)) * C], lc.q);
+    for (int i = 0; i < E; ++i) x[0][i] = add_mod<W>(x[0][i], ad.ld(a0.v, i * a0.s), lc.q);
   }
+  a0.refresh();
 #pragma unroll
-  for (int i = 0; i < E; ++i) out[ob + (uint64_t)(b0 | ((uint32_t)i << G::BB0)) * C] = x[0][i];
+  for (int i = 0; i < E; ++i) dst.st(x[0][i], a0.v, i * a0.s);
 }
 
-// Tiled key-switch decomposition: tile = (((j*L + i)*B + p), column tile).
+// Tiled key-switch decomposition: grid x = p * (C / TC) + column tile,
+// y = source limb i, z = target limb j.
 template <class W, int LOG_R>
 __global__ void __launch_bounds__(ColGeo<LOG_R>::THREADS)
 k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32_t log_n,
@@ -575,32 +649,29 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
-  const uint64_t N = 1ull << log_n;
-  const uint64_t C = 1ull << log_c;
+  const uint32_t N = 1u << log_n;
   const uint32_t tpp_log = log_c - kLogTC;
-  uint64_t rest = (uint64_t)blockIdx.x >> tpp_log;  // (j*L + i)*B + p
-  const uint64_t ct = (uint64_t)blockIdx.x & ((1ull << tpp_log) - 1);
-  const uint32_t p = (uint32_t)(rest % B);
-  rest /= B;
-  const uint32_t i = (uint32_t)(rest % L);
-  const uint32_t j = (uint32_t)(rest / L);
-  XPos xp;
-  xp.slot = G::slot_of(threadIdx.x);
-  xp.tau = G::tau_of(threadIdx.x);
-  xp.heap = (uint64_t)G::X;
-  const uint64_t col = (ct << kLogTC) + xp.slot;
-  const uint64_t src = (uint64_t)i * d_ls + (uint64_t)p * N + col;
-  const uint64_t dst = (((uint64_t)j * L + i) * B + p) * N + col;
-  const uint32_t b0 = G::base(xp.tau, G::BB0);
-  const uint32_t bl = G::base(xp.tau, G::BBL);
+  const uint32_t p = blockIdx.x >> tpp_log;
+  const uint32_t ct = blockIdx.x & ((1u << tpp_log) - 1);
+  const uint32_t i = blockIdx.y;
+  const uint32_t j = blockIdx.z;
+  ColPos cp;
+  cp.xp.slot = G::slot_of(threadIdx.x);
+  cp.xp.tau = G::tau_of(threadIdx.x);
+  cp.xp.heap = (uint32_t)G::X;
+  cp.col = (ct << kLogTC) + cp.xp.slot;
+  const ColAddr<G, G::BB0> a0(cp, log_c);
+  ColAddr<G, G::BBL> al(cp, log_c);
+  const BufView<W> src(d + (uint64_t)i * d_ls + (uint64_t)p * N, N);
+  const BufView<W> dst(S + (((uint64_t)j * L + i) * B + p) * N, N);
   const LimbConst<W> lc = tp.lc[j];
   W x[1][E];
 #pragma unroll
-  for (int e = 0; e < E; ++e)
-    x[0][e] = shoup_mul<W>(d[src + (uint64_t)(b0 | ((uint32_t)e << G::BB0)) * C], (W)1, lc.one_p, lc.q);
-  xf_fwd<G, W, 1>(x, xp, lds, tp.tw + (uint64_t)j * N, mod_of(lc));
+  for (int e = 0; e < E; ++e) x[0][e] = shoup_mul<W>(src.ld(a0.v, e * a0.s), (W)1, lc.one_p, lc.q);
+  xf_fwd<G, W, 1>(x, cp.xp, lds, TwBuf<W>(tp.tw + (uint64_t)j * N, N), mod_of(lc));
+  al.refresh();
 #pragma unroll
-  for (int e = 0; e < E; ++e) S[dst + (uint64_t)(bl | ((uint32_t)e << G::BBL)) * C] = x[0][e];
+  for (int e = 0; e < E; ++e) dst.st(x[0][e], al.v, e * al.s);
 }
 
 // mode 0: forward rows in place; 1: inverse rows in place;
@@ -1012,6 +1083,15 @@ static size_t col_lds() {
   return (size_t)ColGeo<LOG_R>::REGION * sizeof(W);
 }
 
+// Tiled column grid: x = poly * (C / TC) + column tile, y, z as given
+// (limb; source x target limb for the key-switch decomposition).  grid.x = 0
+// flags a shape beyond the hardware grid limits.
+static dim3 col_grid(const Launch& k, const Geom& g, uint32_t y, uint32_t z) {
+  const uint64_t x = (uint64_t)k.B << (g.log_c - kLogTC);
+  if (x > 0x7fffffffull || y > 65535u || z > 65535u) return dim3(0, 1, 1);
+  return dim3((unsigned)x, y, z);
+}
+
 template <class W>
 static hipError_t col_fwd_t(const Launch& k, void* out0, const void* in0, void* out1,
                             const void* in1, uint64_t in_ls, uint64_t out_ls) {
@@ -1019,12 +1099,13 @@ static hipError_t col_fwd_t(const Launch& k, void* out0, const void* in0, void* 
   const TabPtrs<W> tp = tab_ptrs<W>(k.t);
   if ((uint64_t)k.L * k.B == 0) return hipSuccess;
   if (g.log_r >= 5) {
-    const uint64_t tiles = ((uint64_t)k.L * k.B) << (g.log_c - kLogTC);
+    const dim3 grid = col_grid(k, g, (uint32_t)k.L, 1);
+    if (grid.x == 0) return hipErrorInvalidConfiguration;
     hipError_t e = hipSuccess;
 #define RNT_L(R)                                                                               \
   e = allow_lds(k_colt_fwd<W, R>, col_lds<W, R>());                                             \
   if (e != hipSuccess) return e;                                                               \
-  hipLaunchKernelGGL((k_colt_fwd<W, R>), dim3((unsigned)tiles), dim3(ColGeo<R>::THREADS),      \
+  hipLaunchKernelGGL((k_colt_fwd<W, R>), grid, dim3(ColGeo<R>::THREADS),                       \
                      (col_lds<W, R>()), k.s, (W*)out0, (const W*)in0, (W*)out1, (const W*)in1, tp, \
                      g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls)
     RNT_DISPATCH_LOGRT(g.log_r, RNT_L)
@@ -1048,12 +1129,13 @@ static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const v
   const TabPtrs<W> tp = tab_ptrs<W>(k.t);
   if ((uint64_t)k.L * k.B == 0) return hipSuccess;
   if (g.log_r >= 5) {
-    const uint64_t tiles = ((uint64_t)k.L * k.B) << (g.log_c - kLogTC);
+    const dim3 grid = col_grid(k, g, (uint32_t)k.L, 1);
+    if (grid.x == 0) return hipErrorInvalidConfiguration;
     hipError_t e = hipSuccess;
 #define RNT_L(R)                                                                            \
   e = allow_lds(k_colt_inv<W, R>, col_lds<W, R>());                                          \
   if (e != hipSuccess) return e;                                                            \
-  hipLaunchKernelGGL((k_colt_inv<W, R>), dim3((unsigned)tiles), dim3(ColGeo<R>::THREADS),   \
+  hipLaunchKernelGGL((k_colt_inv<W, R>), grid, dim3(ColGeo<R>::THREADS),                    \
                      (col_lds<W, R>()), k.s, (W*)out, (const W*)in, (const W*)addend, tp,      \
                      g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls, rfold)
     RNT_DISPATCH_LOGRT(g.log_r, RNT_L)
@@ -1198,12 +1280,13 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
   if ((uint64_t)k.L * k.B == 0) return hipSuccess;
   const TabPtrs<W> tp = tab_ptrs<W>(k.t);
   if (g.log_r >= 5) {
-    const uint64_t tiles = ((uint64_t)k.L * k.L * k.B) << (g.log_c - kLogTC);
+    const dim3 grid = col_grid(k, g, (uint32_t)k.L, (uint32_t)k.L);
+    if (grid.x == 0) return hipErrorInvalidConfiguration;
     hipError_t e = hipSuccess;
 #define RNT_L(R)                                                                                \
   e = allow_lds(k_colt_decompose<W, R>, col_lds<W, R>());                                        \
   if (e != hipSuccess) return e;                                                                \
-  hipLaunchKernelGGL((k_colt_decompose<W, R>), dim3((unsigned)tiles), dim3(ColGeo<R>::THREADS), \
+  hipLaunchKernelGGL((k_colt_decompose<W, R>), grid, dim3(ColGeo<R>::THREADS),                  \
                      (col_lds<W, R>()), k.s, (W*)S, (const W*)d, tp, g.log_n, g.log_c,            \
                      (uint32_t)k.L, (uint32_t)k.B, d_ls)
     RNT_DISPATCH_LOGRT(g.log_r, RNT_L)

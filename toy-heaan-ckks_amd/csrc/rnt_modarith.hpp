@@ -71,16 +71,19 @@ struct Mod {
 // instruction per SIMD): add/sub/xor/and ~2; min/max, v_mul_lo/hi_u32,
 // v_mul_u32_u24, VOP3 shifts-adds and v_mad_u64_u32 ~4.  v_mad_u64_u32
 // yields a full 64-bit a*b+c for the price of one 32-bit multiply, so the
-// 32-bit path builds its products from it.
+// 32-bit path builds its products from it.  The instruction is left to the
+// compiler (it writes an SGPR carry, whose wait states hipcc only inserts
+// for its own instructions); an empty asm on the 64-bit value keeps the
+// compiler from narrowing it to mul_lo + add.
+__device__ __forceinline__ uint64_t keep64(uint64_t x) {
+  asm("" : "+v"(x));
+  return x;
+}
 __device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
-  uint64_t r, cy;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cy) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return keep64((uint64_t)a * b + c);
 }
 __device__ __forceinline__ uint64_t mul64(uint32_t a, uint32_t b) {
-  uint64_t r, cy;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(cy) : "v"(a), "v"(b));
-  return r;
+  return keep64((uint64_t)a * b);
 }
 
 // Shoup product, result in [0, 2q) (not reduced):
