@@ -94,25 +94,10 @@ def main():
     import numpy as np
 
     import rns_ntt as rn  # loads librnsntt.so (HIP runtime) before torch
+    from rns_ntt.dist import Comm, weak_throughput
 
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-
-        tdist.init_process_group("gloo", rank=rank, world_size=world)
-        dist = (torch, tdist)
-
-    def barrier():
-        if dist:
-            dist[1].barrier()
-
-    def max_over_ranks(x: float) -> float:
-        if not dist:
-            return x
-        t = dist[0].tensor([x], dtype=dist[0].float64)
-        dist[1].all_reduce(t, op=dist[1].ReduceOp.MAX)
-        return float(t.item())
+    comm = Comm.from_env()
+    barrier, max_over_ranks = comm.barrier, comm.max
 
     n = 1 << args.log_n
     L = args.limbs
@@ -155,7 +140,7 @@ def main():
     B.profile_enable(False)
 
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * batch / (elapsed / args.steps)
+    value = weak_throughput(batch, world, elapsed, args.steps)
 
     # spot parity of the timed output against the first unique pair
     if rank == 0:
@@ -238,8 +223,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    if dist:
-        dist[1].destroy_process_group()
+    comm.close()
 
 
 if __name__ == "__main__":
