@@ -172,8 +172,9 @@ def main():
         try:
             with open(tpath) as f:
                 t = json.load(f)
-            if t.get("kernel") == dom and t.get("batch") == batch and t.get("log_n") == args.log_n:
-                traffic = t.get("bytes_per_launch")
+            kt = t.get("kernels", {}).get(dom)
+            if kt and t.get("batch") == batch and t.get("log_n") == args.log_n and t.get("L") == L:
+                traffic = kt.get("bytes_per_launch")
         except Exception:
             traffic = None
     op_bytes = 3 * L * n * wb  # read a, read b, write c per poly-mul at the device word width

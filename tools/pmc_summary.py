@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""pmc_summary.py <prof_dir> <tag>: per-kernel averages from a
+tools/profile_run.sh run -> profiles/<tag>_rocprof_kernel_stats.csv (copied),
+profiles/<tag>_pmc.json and profiles/pmc_traffic.json (what bench.py reads
+for roofline.traffic).  HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE per launch
+(MI355X_MICROARCH.md § HBM: gfx950 FETCH_SIZE tallies 128-B requests at 64 B;
+checked here against this kernel's own algorithmic reads)."""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NAMES = {"k_colt_fwd<unsigned int, 8>": "col_fwd", "k_row<unsigned int, 2, 8>": "row_mul",
+         "k_colt_inv<unsigned int, 8>": "col_inv"}
+
+
+def short(kname):
+    for k, v in NAMES.items():
+        if k in kname:
+            return v
+    return None
+
+
+def counters(d):
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if k:
+                agg[k][(r["Counter_Name"], r.get("Dispatch_Id", ""))].append(float(r["Counter_Value"]))
+    out = {}
+    for k, d2 in agg.items():
+        per = collections.defaultdict(list)
+        for (c, _), vals in d2.items():
+            per[c].append(sum(vals))  # sum over XCD/SE instances within one dispatch
+        out[k] = {c: sum(v) / len(v) for c, v in per.items()}
+    return out
+
+
+def main():
+    prof, tag = sys.argv[1], sys.argv[2]
+    res = collections.defaultdict(dict)
+    for sub in ("fetch", "write", "sq", "grbm"):
+        for k, d in counters(os.path.join(prof, sub)).items():
+            res[k].update(d)
+    stats = glob.glob(os.path.join(prof, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    trace = {}
+    if stats:
+        shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_rocprof_kernel_stats.csv"))
+        for r in csv.DictReader(open(stats[0])):
+            k = short(r["Name"])
+            if k:
+                trace[k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+    kernels = {}
+    for k, d in res.items():
+        fetch = d.get("FETCH_SIZE", 0.0) * 1024  # rocprofv3 reports KB
+        write = d.get("WRITE_SIZE", 0.0) * 1024
+        e = {"fetch_size_bytes": fetch, "write_size_bytes": write,
+             "bytes_per_launch": 2 * fetch + write, **{c: v for c, v in d.items() if c.startswith(("SQ_", "GRBM"))}}
+        if k in trace:
+            e.update(trace[k])
+            if "GRBM_GUI_ACTIVE" in d:
+                e["effective_clock_ghz"] = d["GRBM_GUI_ACTIVE"] / 8 / trace[k]["avg_ns"]
+        if "SQ_WAVE_CYCLES" in d and d["SQ_WAVE_CYCLES"]:
+            w = d["SQ_WAVE_CYCLES"]
+            e["frac_active"] = d.get("SQ_ACTIVE_INST_ANY", 0) / w
+            e["frac_issue_stall"] = d.get("SQ_WAIT_INST_ANY", 0) / w
+            e["frac_waitcnt_barrier"] = d.get("SQ_WAIT_ANY", 0) / w
+        kernels[k] = e
+    meta = {"batch": 256, "log_n": 16, "L": 16, "source": f"tools/profile_run.sh {tag}", "kernels": kernels}
+    with open(os.path.join(ROOT, "profiles", f"{tag}_pmc.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    for k, e in kernels.items():
+        print(k, {x: (round(y, 3) if isinstance(y, float) else y) for x, y in e.items()})
+
+
+if __name__ == "__main__":
+    main()

@@ -337,23 +337,55 @@ struct RowGeo : PassSched<LOG_C> {
   }
 };
 
-// Column tiles: TC = 32 adjacent columns (128 B of u32 per row segment) of
-// a stride-C, length-R column transform per workgroup; LDS is [j][TC] so the
-// 32 lanes of a half-wave (consecutive columns) hit 32 distinct banks.
-constexpr int kLogTC = 5;
-template <int LOG_R>
+// Column tiles: TC = 2^LOG_TC adjacent columns of a stride-C, length-R
+// column transform per workgroup; LDS is [j][TC] so consecutive lanes hit
+// consecutive banks.  TC = 64 (C >= 64) makes a wave's 64 lanes one tau, so
+// every twiddle a wave needs is wave-uniform: they come through scalar loads
+// into SGPRs (no VGPRs, no vector memory ops); TC = 32 (C = 32) keeps them
+// per-lane.
+template <int LOG_R, int LOG_TC>
 struct ColGeo : PassSched<LOG_R> {
   using S = PassSched<LOG_R>;
-  static constexpr int TC = 1 << kLogTC;
+  static constexpr int LOGTC = LOG_TC;
+  static constexpr int TC = 1 << LOG_TC;
+  static constexpr bool UNIFORM = TC == 64;
   static constexpr int THREADS = TC * S::T;
   static constexpr int REGION = S::X * TC;
   __device__ static __forceinline__ uint32_t slot_of(uint32_t tid) { return tid & (TC - 1); }
-  __device__ static __forceinline__ uint32_t tau_of(uint32_t tid) { return tid >> kLogTC; }
+  __device__ static __forceinline__ uint32_t tau_of(uint32_t tid) {
+    if constexpr (UNIFORM) return __builtin_amdgcn_readfirstlane(tid >> LOG_TC);
+    else return tid >> LOG_TC;
+  }
   __device__ static __forceinline__ uint32_t lds_off(uint32_t slot, uint32_t j) {
     return j * TC + slot;
   }
   static constexpr uint32_t lds_ioff(int i, int b) { return ((uint32_t)i << b) * TC; }
 };
+
+// Wave-uniform twiddle source: a constant-address-space view, so uniform
+// indices become s_load into SGPRs.  (The host pass of hipcc parses the
+// kernels too and has no address space 4.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RNT_CONST_AS __attribute__((address_space(4)))
+#else
+#define RNT_CONST_AS
+#endif
+template <class W>
+struct TwScalar {
+  const RNT_CONST_AS Tw<W>* p;
+};
+template <class W>
+__device__ __forceinline__ Tw<W> tw_get(const TwScalar<W>& t, uint32_t i) {
+  return t.p[i];
+}
+template <class W, bool UNIFORM>
+__device__ __forceinline__ auto col_twiddles(const Tw<W>* base, uint32_t n) {
+  if constexpr (UNIFORM) {
+    return TwScalar<W>{(const RNT_CONST_AS Tw<W>*)base};
+  } else {
+    return TwBuf<W>(base, n);
+  }
+}
 
 // Last-stage constants of the inverse network (n^-1 folded, optionally with
 // the Montgomery factor): x <- (u+v) c1, y <- (u-v) c2.
@@ -547,11 +579,11 @@ __device__ __forceinline__ ColPos col_pos(uint32_t log_c) {
   ColPos cp;
   cp.xp.slot = G::slot_of(threadIdx.x);
   cp.xp.tau = G::tau_of(threadIdx.x);
-  const uint32_t tpp_log = log_c - kLogTC;  // column tiles per (limb, poly)
+  const uint32_t tpp_log = log_c - G::LOGTC;  // column tiles per (limb, poly)
   cp.l = blockIdx.y;
   cp.p = blockIdx.x >> tpp_log;
   const uint32_t ct = blockIdx.x & ((1u << tpp_log) - 1);
-  cp.col = (ct << kLogTC) + cp.xp.slot;
+  cp.col = (ct << G::LOGTC) + cp.xp.slot;
   cp.xp.heap = (uint32_t)G::X;
   return cp;
 }
@@ -569,11 +601,11 @@ struct ColAddr {
   __device__ __forceinline__ void refresh() { asm volatile("" : "+s"(s)); }
 };
 
-template <class W, int LOG_R>
-__global__ void __launch_bounds__(ColGeo<LOG_R>::THREADS)
+template <class W, int LOG_R, int LOG_TC>
+__global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t log_n,
            uint32_t log_c, uint32_t B, uint64_t in_ls, uint64_t out_ls) {
-  using G = ColGeo<LOG_R>;
+  using G = ColGeo<LOG_R, LOG_TC>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
@@ -583,7 +615,7 @@ k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t
   const uint64_t op = (uint64_t)cp.l * out_ls + (uint64_t)cp.p * N;
   ColAddr<G, G::BB0> a0(cp, log_c);
   ColAddr<G, G::BBL> al(cp, log_c);
-  const TwBuf<W> tw(tp.tw + (uint64_t)cp.l * N, N);
+  const auto tw = col_twiddles<W, G::UNIFORM>(tp.tw + (uint64_t)cp.l * N, N);
   const Mod<W> m = mod_of(tp.lc[cp.l]);
   W x[1][E];
   // operand 1 first: out0 may alias in1 (out = a * b with out == b)
@@ -605,11 +637,11 @@ k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t
   for (int i = 0; i < E; ++i) dst.st(x[0][i], al.v, i * al.s);
 }
 
-template <class W, int LOG_R>
-__global__ void __launch_bounds__(ColGeo<LOG_R>::THREADS)
+template <class W, int LOG_R, int LOG_TC>
+__global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, uint32_t log_c,
            uint32_t B, uint64_t in_ls, uint64_t out_ls, int rfold) {
-  using G = ColGeo<LOG_R>;
+  using G = ColGeo<LOG_R, LOG_TC>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
@@ -620,7 +652,7 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
   ColAddr<G, G::BB0> a0(cp, log_c);
   const ColAddr<G, G::BBL> al(cp, log_c);
   const LimbConst<W> lc = tp.lc[cp.l];
-  const TwBuf<W> itw(tp.itw + (uint64_t)cp.l * N, N);
+  const auto itw = col_twiddles<W, G::UNIFORM>(tp.itw + (uint64_t)cp.l * N, N);
   const Fold<W> f = rfold ? Fold<W>{lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p}
                           : Fold<W>{lc.c1, lc.c1_p, lc.c2, lc.c2_p};
   const BufView<W> src(in + ip, N), dst(out + op, N);
@@ -641,16 +673,16 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
 
 // Tiled key-switch decomposition: grid x = p * (C / TC) + column tile,
 // y = source limb i, z = target limb j.
-template <class W, int LOG_R>
-__global__ void __launch_bounds__(ColGeo<LOG_R>::THREADS)
+template <class W, int LOG_R, int LOG_TC>
+__global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32_t log_n,
                  uint32_t log_c, uint32_t L, uint32_t B, uint64_t d_ls) {
-  using G = ColGeo<LOG_R>;
+  using G = ColGeo<LOG_R, LOG_TC>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
   const uint32_t N = 1u << log_n;
-  const uint32_t tpp_log = log_c - kLogTC;
+  const uint32_t tpp_log = log_c - G::LOGTC;
   const uint32_t p = blockIdx.x >> tpp_log;
   const uint32_t ct = blockIdx.x & ((1u << tpp_log) - 1);
   const uint32_t i = blockIdx.y;
@@ -659,7 +691,7 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
   cp.xp.slot = G::slot_of(threadIdx.x);
   cp.xp.tau = G::tau_of(threadIdx.x);
   cp.xp.heap = (uint32_t)G::X;
-  cp.col = (ct << kLogTC) + cp.xp.slot;
+  cp.col = (ct << G::LOGTC) + cp.xp.slot;
   const ColAddr<G, G::BB0> a0(cp, log_c);
   ColAddr<G, G::BBL> al(cp, log_c);
   const BufView<W> src(d + (uint64_t)i * d_ls + (uint64_t)p * N, N);
@@ -668,7 +700,8 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
   W x[1][E];
 #pragma unroll
   for (int e = 0; e < E; ++e) x[0][e] = shoup_mul<W>(src.ld(a0.v, e * a0.s), (W)1, lc.one_p, lc.q);
-  xf_fwd<G, W, 1>(x, cp.xp, lds, TwBuf<W>(tp.tw + (uint64_t)j * N, N), mod_of(lc));
+  xf_fwd<G, W, 1>(x, cp.xp, lds, col_twiddles<W, G::UNIFORM>(tp.tw + (uint64_t)j * N, N),
+                  mod_of(lc));
   al.refresh();
 #pragma unroll
   for (int e = 0; e < E; ++e) dst.st(x[0][e], al.v, e * al.s);
@@ -1078,16 +1111,17 @@ static size_t row_lds(int nops) {
     default: return hipErrorInvalidValue; \
   }
 
-template <class W, int LOG_R>
+template <class W, int LOG_R, int LOG_TC>
 static size_t col_lds() {
-  return (size_t)ColGeo<LOG_R>::REGION * sizeof(W);
+  return (size_t)ColGeo<LOG_R, LOG_TC>::REGION * sizeof(W);
 }
 
 // Tiled column grid: x = poly * (C / TC) + column tile, y, z as given
 // (limb; source x target limb for the key-switch decomposition).  grid.x = 0
 // flags a shape beyond the hardware grid limits.
+static int col_log_tc(const Geom& g) { return g.log_c >= 6 ? 6 : 5; }
 static dim3 col_grid(const Launch& k, const Geom& g, uint32_t y, uint32_t z) {
-  const uint64_t x = (uint64_t)k.B << (g.log_c - kLogTC);
+  const uint64_t x = (uint64_t)k.B << (g.log_c - col_log_tc(g));
   if (x > 0x7fffffffull || y > 65535u || z > 65535u) return dim3(0, 1, 1);
   return dim3((unsigned)x, y, z);
 }
@@ -1102,14 +1136,21 @@ static hipError_t col_fwd_t(const Launch& k, void* out0, const void* in0, void* 
     const dim3 grid = col_grid(k, g, (uint32_t)k.L, 1);
     if (grid.x == 0) return hipErrorInvalidConfiguration;
     hipError_t e = hipSuccess;
-#define RNT_L(R)                                                                               \
-  e = allow_lds(k_colt_fwd<W, R>, col_lds<W, R>());                                             \
-  if (e != hipSuccess) return e;                                                               \
-  hipLaunchKernelGGL((k_colt_fwd<W, R>), grid, dim3(ColGeo<R>::THREADS),                       \
-                     (col_lds<W, R>()), k.s, (W*)out0, (const W*)in0, (W*)out1, (const W*)in1, tp, \
-                     g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls)
+#define RNT_L2(R, TC)                                                                           \
+  e = allow_lds(k_colt_fwd<W, R, TC>, col_lds<W, R, TC>());                                     \
+  if (e != hipSuccess) return e;                                                                \
+  hipLaunchKernelGGL((k_colt_fwd<W, R, TC>), grid, dim3(ColGeo<R, TC>::THREADS),                \
+                     (col_lds<W, R, TC>()), k.s, (W*)out0, (const W*)in0, (W*)out1, (const W*)in1, \
+                     tp, g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls)
+#define RNT_L(R)                          \
+  if (col_log_tc(g) == 6) {               \
+    RNT_L2(R, 6);                         \
+  } else {                                \
+    RNT_L2(R, 5);                         \
+  }
     RNT_DISPATCH_LOGRT(g.log_r, RNT_L)
 #undef RNT_L
+#undef RNT_L2
     return hipGetLastError();
   }
   const uint64_t total = (uint64_t)k.L * k.B * g.c;
@@ -1132,14 +1173,21 @@ static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const v
     const dim3 grid = col_grid(k, g, (uint32_t)k.L, 1);
     if (grid.x == 0) return hipErrorInvalidConfiguration;
     hipError_t e = hipSuccess;
-#define RNT_L(R)                                                                            \
-  e = allow_lds(k_colt_inv<W, R>, col_lds<W, R>());                                          \
-  if (e != hipSuccess) return e;                                                            \
-  hipLaunchKernelGGL((k_colt_inv<W, R>), grid, dim3(ColGeo<R>::THREADS),                    \
-                     (col_lds<W, R>()), k.s, (W*)out, (const W*)in, (const W*)addend, tp,      \
+#define RNT_L2(R, TC)                                                                        \
+  e = allow_lds(k_colt_inv<W, R, TC>, col_lds<W, R, TC>());                                  \
+  if (e != hipSuccess) return e;                                                             \
+  hipLaunchKernelGGL((k_colt_inv<W, R, TC>), grid, dim3(ColGeo<R, TC>::THREADS),             \
+                     (col_lds<W, R, TC>()), k.s, (W*)out, (const W*)in, (const W*)addend, tp, \
                      g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls, rfold)
+#define RNT_L(R)                          \
+  if (col_log_tc(g) == 6) {               \
+    RNT_L2(R, 6);                         \
+  } else {                                \
+    RNT_L2(R, 5);                         \
+  }
     RNT_DISPATCH_LOGRT(g.log_r, RNT_L)
 #undef RNT_L
+#undef RNT_L2
     return hipGetLastError();
   }
   const uint64_t total = (uint64_t)k.L * k.B * g.c;
@@ -1283,14 +1331,21 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
     const dim3 grid = col_grid(k, g, (uint32_t)k.L, (uint32_t)k.L);
     if (grid.x == 0) return hipErrorInvalidConfiguration;
     hipError_t e = hipSuccess;
-#define RNT_L(R)                                                                                \
-  e = allow_lds(k_colt_decompose<W, R>, col_lds<W, R>());                                        \
-  if (e != hipSuccess) return e;                                                                \
-  hipLaunchKernelGGL((k_colt_decompose<W, R>), grid, dim3(ColGeo<R>::THREADS),                  \
-                     (col_lds<W, R>()), k.s, (W*)S, (const W*)d, tp, g.log_n, g.log_c,            \
+#define RNT_L2(R, TC)                                                                         \
+  e = allow_lds(k_colt_decompose<W, R, TC>, col_lds<W, R, TC>());                             \
+  if (e != hipSuccess) return e;                                                              \
+  hipLaunchKernelGGL((k_colt_decompose<W, R, TC>), grid, dim3(ColGeo<R, TC>::THREADS),        \
+                     (col_lds<W, R, TC>()), k.s, (W*)S, (const W*)d, tp, g.log_n, g.log_c,      \
                      (uint32_t)k.L, (uint32_t)k.B, d_ls)
+#define RNT_L(R)                          \
+  if (col_log_tc(g) == 6) {               \
+    RNT_L2(R, 6);                         \
+  } else {                                \
+    RNT_L2(R, 5);                         \
+  }
     RNT_DISPATCH_LOGRT(g.log_r, RNT_L)
 #undef RNT_L
+#undef RNT_L2
     return hipGetLastError();
   }
   const uint64_t total = (uint64_t)k.L * k.L * k.B * g.c;
