@@ -468,11 +468,37 @@ __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0,
   }
 }
 
+// Row kernels with several operands exchange them one after the other
+// through a single LDS region: half (or a third) of the LDS per workgroup,
+// so occupancy is bounded by VGPRs rather than LDS, at two extra barriers.
+#ifndef RNT_SEQ_XCHG
+#define RNT_SEQ_XCHG 1
+#endif
+constexpr bool kSeqXchg = RNT_SEQ_XCHG;
+// Minimum resident waves per SIMD requested for the row kernels (caps their
+// VGPR budget at 512 / kRowMinWaves).
+#ifndef RNT_ROW_MIN_WAVES
+#define RNT_ROW_MIN_WAVES 6
+#endif
+constexpr int kRowMinWaves = RNT_ROW_MIN_WAVES;
+
 // Move NOPS register sets from distribution BF to BT through LDS.
 template <class G, class W, int NOPS, int BF, int BT>
 __device__ __forceinline__ void xchg(W (&x)[NOPS][G::E], W* lds, uint32_t slot, uint32_t tau) {
   const uint32_t wb = G::lds_off(slot, G::base(tau, BF));
   const uint32_t rb = G::lds_off(slot, G::base(tau, BT));
+  if constexpr (kSeqXchg && NOPS > 1) {
+#pragma unroll
+    for (int o = 0; o < NOPS; ++o) {
+#pragma unroll
+      for (int i = 0; i < G::E; ++i) lds[wb + G::lds_ioff(i, BF)] = x[o][i];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < G::E; ++i) x[o][i] = lds[rb + G::lds_ioff(i, BT)];
+      __syncthreads();
+    }
+    return;
+  }
 #pragma unroll
   for (int o = 0; o < NOPS; ++o) {
     W* reg = lds + o * G::REGION;
@@ -710,7 +736,7 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
 // mode 0: forward rows in place; 1: inverse rows in place;
 // 2: poly-mul rows: x <- INV(FWD(x) (.) FWD(y)) with Montgomery pointwise.
 template <class W, int MODE, int LOG_C>
-__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS)
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kRowMinWaves : 1)
 k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_n, uint32_t B,
       uint64_t ls, uint64_t rows_total) {
   using G = RowGeo<LOG_C>;
@@ -1099,7 +1125,7 @@ static hipError_t allow_lds(K kernel, size_t bytes) {
 template <class W, int LOG_C>
 static size_t row_lds(int nops) {
   using G = RowGeo<LOG_C>;
-  return (size_t)nops * G::RPW * G::PADC * sizeof(W);
+  return (size_t)(kSeqXchg ? 1 : nops) * G::RPW * G::PADC * sizeof(W);
 }
 
 #define RNT_DISPATCH_LOGRT(LOGR, MACRO) \

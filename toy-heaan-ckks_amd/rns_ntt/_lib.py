@@ -105,11 +105,14 @@ SIGNATURES = {
 _lib = None
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load librnsntt.so once; raise loudly if it was not built."""
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load librnsntt.so once; raise loudly if it was not built.  RNSNTT_LIB
+    overrides the path (tools/ab.sh compares build variants of the same
+    library on one box)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("RNSNTT_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(
             f"librnsntt.so not found at {path}: build it with `make` or "
