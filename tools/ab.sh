@@ -1,15 +1,20 @@
 #!/bin/bash
-# ab.sh <reps> <variant...>: interleaved short bench runs of build variants
-# (lib/variants/librnsntt_<v>.so; "base" = lib/librnsntt.so) on one box ->
-# gpurun_out/ab_<v>_<i>.json, summarised per variant by tools/ab_summary.py.
+# ab.sh <reps> <variant...>: interleaved short bench runs on one box.
+# A variant is <lib>[+VAR=VAL...]: <lib> = "base" (lib/librnsntt.so) or a
+# name from tools/build_variant.sh; the +VAR=VAL pairs are exported for that
+# run (e.g. base+RNT_MUL_CHUNKS=4+RNT_MUL_STREAMS=2).  Results ->
+# gpurun_out/ab_<variant>_<i>.json, summarised by tools/ab_summary.py.
 set -o pipefail
 mkdir -p gpurun_out
 REPS=$1; shift
 VARS=${@:-base}
 for i in $(seq 1 $REPS); do
   for v in $VARS; do
-    if [ "$v" = base ]; then lib=toy-heaan-ckks_amd/lib/librnsntt.so; else lib=toy-heaan-ckks_amd/lib/variants/librnsntt_$v.so; fi
-    RNSNTT_LIB=$lib timeout -k 10 300 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline > gpurun_out/ab_${v}_$i.json 2> gpurun_out/ab_${v}_$i.err || exit $?
+    IFS='+' read -ra parts <<< "$v"
+    libname=${parts[0]}
+    if [ "$libname" = base ]; then lib=toy-heaan-ckks_amd/lib/librnsntt.so; else lib=toy-heaan-ckks_amd/lib/variants/librnsntt_$libname.so; fi
+    tag=$(echo "$v" | tr '+=' '__')
+    env RNSNTT_LIB=$lib "${parts[@]:1}" timeout -k 10 300 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline $BENCH_ARGS > gpurun_out/ab_${tag}_$i.json 2> gpurun_out/ab_${tag}_$i.err || exit $?
   done
 done
-for v in $VARS; do echo "== $v" >&2; python3 tools/ab_summary.py gpurun_out/ab_${v}_*.json >&2; done
+for v in $VARS; do tag=$(echo "$v" | tr '+=' '__'); echo "== $v" >&2; python3 tools/ab_summary.py gpurun_out/ab_${tag}_[0-9]*.json >&2; done

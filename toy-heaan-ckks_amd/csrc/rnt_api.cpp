@@ -63,20 +63,24 @@ hipEvent_t prof_event(rnt::Prof* p) {
 
 // Bracket one launch with events when profiling is on.
 template <class F>
-hipError_t prof_launch(const rnt::Tables* t, int id, F&& f) {
+hipError_t prof_launch(const rnt::Tables* t, hipStream_t s, int id, F&& f) {
   rnt::Prof* p = t->prof;
   if (p == nullptr || !p->on) return f();
   std::lock_guard<std::mutex> g(p->mu);
   hipEvent_t a = prof_event(p), b = prof_event(p);
-  if (a) (void)hipEventRecord(a, t->stream);
+  if (a) (void)hipEventRecord(a, s);
   hipError_t e = f();
-  if (b) (void)hipEventRecord(b, t->stream);
+  if (b) (void)hipEventRecord(b, s);
   if (a && b) p->pending.push_back({id, a, b});
   return e;
 }
 
+// Launch on the context's stream, or (LAUNCH_ON) on an explicit one; with
+// profiling on, the launch is bracketed by events on that same stream.
 #define LAUNCH(T, ID, EXPR, WHERE) \
-  HIP_TRY(prof_launch((T), (ID), [&]() { return (EXPR); }), WHERE)
+  HIP_TRY(prof_launch((T), (T)->stream, (ID), [&]() { return (EXPR); }), WHERE)
+#define LAUNCH_ON(T, S, ID, EXPR, WHERE) \
+  HIP_TRY(prof_launch((T), (S), (ID), [&]() { return (EXPR); }), WHERE)
 
 
 
@@ -171,6 +175,14 @@ rnt::Tables::~Tables() {
     (void)hipStreamSynchronize(stream);
     (void)hipStreamDestroy(stream);
   }
+  for (int i = 0; i < kAux; ++i) {
+    if (aux[i]) {
+      (void)hipStreamSynchronize(aux[i]);
+      (void)hipStreamDestroy(aux[i]);
+    }
+    if (join_ev[i]) (void)hipEventDestroy(join_ev[i]);
+  }
+  if (fork_ev) (void)hipEventDestroy(fork_ev);
   (void)hipFree(tw_fwd);
   (void)hipFree(tw_inv);
   (void)hipFree(lconst);
@@ -621,16 +633,50 @@ extern "C" int rnt_ntt_inv(rnt_buf* b) {
 // Polys per launch chunk of the coefficient-domain product.  0 / unset
 // RNT_MUL_CHUNK_MB: whole batch; otherwise chunks of about that many MiB of
 // a-operand data (experiment knob for Infinity-Cache residency).
-static size_t mul_chunk(const rnt::Tables* t, size_t L, size_t B) {
-  static const long mb = [] {
-    const char* e = getenv("RNT_MUL_CHUNK_MB");
-    return e ? atol(e) : 0L;
-  }();
-  if (mb <= 0) return B;
-  const size_t per = L * t->n * (t->wide ? 8 : 4);
-  size_t c = ((size_t)mb << 20) / (per ? per : 1);
-  if (c < 1) c = 1;
-  return std::min(c, B);
+// Batch pipelining of rnt_mul: the batch is cut into `chunks` slices whose
+// three launches go round-robin onto `streams` streams, so one slice's
+// HBM-bound column passes can overlap another's VALU-bound row pass.
+// RNT_MUL_CHUNKS / RNT_MUL_STREAMS override the defaults (A/B tuning).
+struct MulPlan {
+  size_t chunk;  // polys per slice
+  int streams;   // 1 = the context stream only
+};
+static long env_long(const char* name, long dflt) {
+  const char* e = getenv(name);
+  return e ? atol(e) : dflt;
+}
+static MulPlan mul_plan(size_t B) {
+  static const long chunks = env_long("RNT_MUL_CHUNKS", 1);
+  static const long streams = env_long("RNT_MUL_STREAMS", 1);
+  MulPlan p;
+  const size_t c = chunks > 1 ? (size_t)chunks : 1;
+  p.chunk = std::max<size_t>(1, (B + c - 1) / c);
+  p.streams = (int)std::max(1L, std::min<long>(streams, rnt::Tables::kAux));
+  if (p.chunk >= B) p.streams = 1;
+  return p;
+}
+
+// Auxiliary streams forked from the context stream (created on first use).
+static hipError_t aux_fork(rnt::Tables* t, int n) {
+  std::lock_guard<std::mutex> g(t->aux_mu);
+  hipError_t e = hipSuccess;
+  if (!t->fork_ev) e = hipEventCreateWithFlags(&t->fork_ev, hipEventDisableTiming);
+  for (int i = 0; i < n && e == hipSuccess; ++i) {
+    if (!t->aux[i]) e = hipStreamCreateWithFlags(&t->aux[i], hipStreamNonBlocking);
+    if (e == hipSuccess && !t->join_ev[i])
+      e = hipEventCreateWithFlags(&t->join_ev[i], hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipEventRecord(t->fork_ev, t->stream);
+  for (int i = 0; i < n && e == hipSuccess; ++i) e = hipStreamWaitEvent(t->aux[i], t->fork_ev, 0);
+  return e;
+}
+static hipError_t aux_join(rnt::Tables* t, int n) {
+  hipError_t e = hipSuccess;
+  for (int i = 0; i < n && e == hipSuccess; ++i) {
+    e = hipEventRecord(t->join_ev[i], t->aux[i]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(t->stream, t->join_ev[i], 0);
+  }
+  return e;
 }
 
 extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
@@ -655,20 +701,27 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   const size_t wb = word_bytes(k.t);
   if (int rc = ensure_ws(out, poly_words(out) * wb)) return rc;
   const size_t B = out->n_polys;
-  const size_t bc = mul_chunk(k.t, k.L, B);
+  const MulPlan plan = mul_plan(B);
   const size_t n = k.t->n;
-  for (size_t p0 = 0; p0 < B; p0 += bc) {
+  rnt::Tables* tm = const_cast<rnt::Tables*>(k.t);
+  if (plan.streams > 1) HIP_TRY(aux_fork(tm, plan.streams), "stream fork");
+  int si = 0;
+  for (size_t p0 = 0; p0 < B; p0 += plan.chunk, si = (si + 1) % plan.streams) {
     rnt::Launch kc = k;
-    kc.B = std::min(bc, B - p0);
+    kc.B = std::min(plan.chunk, B - p0);
+    kc.s = plan.streams > 1 ? tm->aux[si] : k.s;
     const size_t off = p0 * n * wb;
     char* o = (char*)out->data + off;
     char* w = (char*)out->ws + off;
     const char* pa = (const char*)a->data + off;
     const char* pb = (const char*)b->data + off;
-    LAUNCH(kc.t, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, o, pa, w, pb, ls, ls), "column forward");
-    LAUNCH(kc.t, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, o, w, ls), "row mul");
-    LAUNCH(kc.t, rnt::K_COL_INV, rnt::launch_col_inv(kc, o, ls, o, ls, 1, nullptr), "column inverse");
+    LAUNCH_ON(kc.t, kc.s, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, o, pa, w, pb, ls, ls),
+              "column forward");
+    LAUNCH_ON(kc.t, kc.s, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, o, w, ls), "row mul");
+    LAUNCH_ON(kc.t, kc.s, rnt::K_COL_INV, rnt::launch_col_inv(kc, o, ls, o, ls, 1, nullptr),
+              "column inverse");
   }
+  if (plan.streams > 1) HIP_TRY(aux_join(tm, plan.streams), "stream join");
   out->in_ntt = 0;
   return RNT_OK;
 }

@@ -73,6 +73,13 @@ struct Tables {
   void* resc = nullptr;     // [L][L]: resc[l][i] = (q_l mod q_i)^-1 mod q_i, i < l
   void* resc_p = nullptr;   // [L][L] Shoup companions
   hipStream_t stream = nullptr;
+  // Auxiliary streams for chunked pipelines (rnt_mul): created on first
+  // use, forked from / joined back into `stream` with events.
+  static constexpr int kAux = 4;
+  hipStream_t aux[kAux] = {};
+  hipEvent_t fork_ev = nullptr;
+  hipEvent_t join_ev[kAux] = {};
+  std::mutex aux_mu;
   struct Prof* prof = nullptr;  // per-kernel event timing (rnt_profile_*)
   ~Tables();
 };

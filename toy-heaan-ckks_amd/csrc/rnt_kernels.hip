@@ -644,20 +644,32 @@ k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t
   const auto tw = col_twiddles<W, G::UNIFORM>(tp.tw + (uint64_t)cp.l * N, N);
   const Mod<W> m = mod_of(tp.lc[cp.l]);
   W x[1][E];
-  // operand 1 first: out0 may alias in1 (out = a * b with out == b)
+  const BufView<W> src(in0 + ip, N), dst(out0 + op, N);
+  // operand 1 first: out0 may alias in1 (out = a * b with out == b).  With
+  // wave-uniform twiddles the registers are cheap, so operand 0's loads are
+  // issued up front and land while operand 1 is transformed.
   if (in1 != nullptr) {
-    const BufView<W> src(in1 + ip, N), dst(out1 + op, N);
+    const BufView<W> src1(in1 + ip, N), dst1(out1 + op, N);
+    W y[1][E];
 #pragma unroll
-    for (int i = 0; i < E; ++i) x[0][i] = src.ld(a0.v, i * a0.s);
-    xf_fwd<G, W, 1>(x, cp.xp, lds, tw, m);
+    for (int i = 0; i < E; ++i) y[0][i] = src1.ld(a0.v, i * a0.s);
+    if constexpr (G::UNIFORM) {
 #pragma unroll
-    for (int i = 0; i < E; ++i) dst.st(x[0][i], al.v, i * al.s);
+      for (int i = 0; i < E; ++i) x[0][i] = src.ld(a0.v, i * a0.s);
+    }
+    xf_fwd<G, W, 1>(y, cp.xp, lds, tw, m);
+#pragma unroll
+    for (int i = 0; i < E; ++i) dst1.st(y[0][i], al.v, i * al.s);
     a0.refresh();
     al.refresh();
-  }
-  const BufView<W> src(in0 + ip, N), dst(out0 + op, N);
+    if constexpr (!G::UNIFORM) {
 #pragma unroll
-  for (int i = 0; i < E; ++i) x[0][i] = src.ld(a0.v, i * a0.s);
+      for (int i = 0; i < E; ++i) x[0][i] = src.ld(a0.v, i * a0.s);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < E; ++i) x[0][i] = src.ld(a0.v, i * a0.s);
+  }
   xf_fwd<G, W, 1>(x, cp.xp, lds, tw, m);
 #pragma unroll
   for (int i = 0; i < E; ++i) dst.st(x[0][i], al.v, i * al.s);
