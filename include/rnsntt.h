@@ -127,6 +127,14 @@ int rnt_upload_coeffs(rnt_buf* buf, const int64_t* coeffs, size_t n_polys);
  * in the buffer's current domain (natural order when NTT). */
 int rnt_download(const rnt_buf* buf, uint64_t* host, size_t n_polys);
 int rnt_copy(rnt_buf* dst, const rnt_buf* src); /* Clone */
+/* Device-memory interop for multi-GPU pipelines (collectives run by the
+ * caller, e.g. RCCL through torch.distributed):
+ * rnt_buf_wrap makes a NON-owning buffer over caller device memory laid out
+ * [L][n_polys][N] in the context's word width (device-internal order when
+ * in_ntt); rnt_buf_device_ptr exposes a buffer's storage and word width. */
+int rnt_buf_wrap(const rnt_ctx* ctx, void* device_ptr, size_t n_polys, int in_ntt,
+                 rnt_buf** out);
+int rnt_buf_device_ptr(const rnt_buf* buf, void** device_ptr, size_t* word_bytes);
 
 /* ---- ring ops (batched; every poly of the buffers participates) -------- */
 /* to_ntt_domain / to_coeff_domain (poly.rs:136-166); no-ops when already
@@ -158,7 +166,9 @@ int rnt_rotate_slots(rnt_buf* out, const rnt_buf* in, int32_t k);
 
 /* ---- engine-level fused ops (src/crypto/engine.rs) -------------------- */
 /* A gadget key (RnsGadgetRelinKey / RnsGadgetRotationKey, engine.rs:224-253):
- * key_a and key_b are buffers of L polys each (poly i = a_i / b_i).  They
+ * key_a and key_b are buffers of one poly per gadget (source) limb i
+ * (poly i = a_i / b_i): L polys for rnt_keyswitch, the global limb count for
+ * a limb shard's rnt_keyswitch_ext (validated by the key-switch calls).  They
  * are kept device-resident in the NTT domain; rnt_key_prepare transforms
  * them once. */
 int rnt_key_prepare(rnt_buf* key_a, rnt_buf* key_b);
@@ -181,6 +191,32 @@ int rnt_ct_rotate(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
  * dropped basis. */
 int rnt_ct_rescale(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
                    const rnt_buf* c1);
+
+/* ---- limb-sharded building blocks ------------------------ */
+/* A rank owning a contiguous run of the global basis' limbs holds every
+ * ciphertext restricted to them (a context over those moduli).  The join
+ * steps take the other ranks' limbs as raw device arrays gathered by the
+ * caller. */
+/* Tensor product of mul_ciphertexts_gadget (engine.rs:480-493) on the local
+ * limbs: d0 = c0 c0', d1 = c0 c1' + c1 c0' (NTT domain, device order: the
+ * seeds of rnt_keyswitch_ext), d2 = c1 c1' (coefficient domain). */
+int rnt_ct_tensor(rnt_buf* d0, rnt_buf* d1, rnt_buf* d2, const rnt_buf* c0,
+                  const rnt_buf* c1, const rnt_buf* c0p, const rnt_buf* c1p);
+/* Gadget sum (engine.rs:505-528) for the local (target) limbs of acc0/acc1
+ * over `src_limbs` source limbs held at `src` ([src_limbs][B][N] words,
+ * coefficient domain, B = acc0's batch): acc = INV(seed + sum_i
+ * NTT(src_i mod q_j) key[i]); key_a/key_b hold src_limbs polys over acc's
+ * basis (prepared); init0/init1 NTT-domain seeds or NULL. */
+int rnt_keyswitch_ext(rnt_buf* acc0, rnt_buf* acc1, const void* src, size_t src_limbs,
+                      const rnt_buf* key_a, const rnt_buf* key_b, const rnt_buf* init0,
+                      const rnt_buf* init1);
+/* rescale_into (poly.rs:187-228) by an external last modulus q_last whose
+ * residues (coefficient domain, [B][N] words) are at `last_limb`: every
+ * local limb l -> (c_l - (c_last mod q_l)) (q_last mod q_l)^-1.  If q_last is
+ * the input's own last modulus (the shard that owns it) that limb is
+ * dropped, so `out` must be drop_last(1) of `in`'s context; otherwise `out`
+ * shares `in`'s context. */
+int rnt_rescale_ext(rnt_buf* out, const rnt_buf* in, const void* last_limb, uint64_t q_last);
 
 #ifdef __cplusplus
 }

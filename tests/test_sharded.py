@@ -1,0 +1,228 @@
+"""Limb-sharded ct x ct -> relin -> rescale.
+
+CPU: world_size 2/3 gloo ranks run rns_ntt.sharded.LimbShardedPipeline with
+the oracle backend (tests/shard_oracle_backend.py); the assembled per-rank
+limbs must equal the unsharded oracle pipeline (oracle/oracle.c restating
+engine.rs:473-539 and poly.rs:187-228) bit-exactly.
+
+GPU: the same pipeline on one MI355X with the ranks simulated as threads
+(ThreadComm), through librnsntt's rnt_ct_tensor / rnt_keyswitch_ext /
+rnt_rescale_ext, against the unsharded library path and the oracle.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import pyoracle as orc
+
+
+def _inputs(mods, n, B, seed):
+    rng = np.random.default_rng(seed)
+    L = len(mods)
+    cts = [orc.uniform_poly(mods, n, rng, batch=B) for _ in range(4)]  # c0 c1 c0' c1'
+    key_a = orc.uniform_poly(mods, n, rng, batch=L)
+    key_b = orc.uniform_poly(mods, n, rng, batch=L)
+    return cts, key_a, key_b
+
+
+def _oracle_reference(mods, n, cts, key_a, key_b):
+    ob = orc.Basis(mods, n)
+    r0, r1, s0, s1 = [], [], [], []
+    for p in range(cts[0].shape[0]):
+        o0, o1 = orc.mul_ciphertexts_gadget(ob, cts[0][p], cts[1][p], cts[2][p], cts[3][p], key_a, key_b)
+        r0.append(o0)
+        r1.append(o1)
+        s0.append(orc.rescale(ob, o0))
+        s1.append(orc.rescale(ob, o1))
+    return np.stack(r0), np.stack(r1), np.stack(s0), np.stack(s1)
+
+
+def _run_rank(pipe, cts, key_a, key_b):
+    c = [pipe.upload(x) for x in cts]
+    key = pipe.upload_key(key_a, key_b)
+    m0, m1 = pipe.mul_relin(c[0], c[1], c[2], c[3], key)
+    relin = (pipe.download(m0), pipe.download(m1))
+    r0, r1 = pipe.rescale(m0, m1)
+    return relin, (pipe.download(r0), pipe.download(r1))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gloo_worker(rank, world, port, mods, n, B, seed, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from rns_ntt.sharded import LimbShardedPipeline, TorchDistComm
+    from shard_oracle_backend import OracleBackend
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cts, key_a, key_b = _inputs(mods, n, B, seed)
+        pipe = LimbShardedPipeline(mods, n, TorchDistComm(), OracleBackend())
+        limbs = (pipe.limbs.start, pipe.limbs.stop)
+        relin, resc = _run_rank(pipe, cts, key_a, key_b)
+        q.put((rank, limbs, relin, resc))
+    finally:
+        dist.destroy_process_group()
+
+
+def _collect(q, procs, count, timeout=300.0):
+    """Results from the workers; fail fast if one of them dies."""
+    import queue
+    import time
+
+    out, t0 = [], time.time()
+    while len(out) < count:
+        try:
+            out.append(q.get(timeout=2))
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"worker exited with {dead}"
+            assert time.time() - t0 < timeout, "workers timed out"
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+def _assemble(results):
+    results = sorted(results, key=lambda r: r[0])
+    relin0 = np.concatenate([r[2][0] for r in results], axis=1)
+    relin1 = np.concatenate([r[2][1] for r in results], axis=1)
+    resc0 = np.concatenate([r[3][0] for r in results], axis=1)
+    resc1 = np.concatenate([r[3][1] for r in results], axis=1)
+    return relin0, relin1, resc0, resc1
+
+
+@pytest.mark.parametrize("world,L", [(2, 4), (3, 7)])
+def test_limb_sharded_gloo_matches_unsharded(world, L):
+    n, B, seed = 32, 2, 5
+    mods = orc.generate_primes(31, L, n)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, mods, n, B, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = _collect(q, procs, world)
+    # contiguous limb runs in rank order covering the basis
+    spans = [r[1] for r in sorted(results, key=lambda r: r[0])]
+    assert spans[0][0] == 0 and spans[-1][1] == L
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    cts, key_a, key_b = _inputs(mods, n, B, seed)
+    want = _oracle_reference(mods, n, cts, key_a, key_b)
+    got = _assemble(results)
+    for g, w in zip(got, want):
+        assert np.array_equal(g.astype(np.uint64), w)
+
+
+def test_sharded_layout_bookkeeping():
+    """Rescale drops the last limb only on its owner; later joins follow."""
+    from rns_ntt.sharded import LimbShardedPipeline
+
+    class _Comm:
+        def __init__(self, rank, world):
+            self.rank, self.world = rank, world
+
+    class _NullBackend:
+        def make_basis(self, moduli, degree):
+            return list(moduli)
+
+    pipes = [LimbShardedPipeline(list(range(101, 117)), 8, _Comm(r, 3), _NullBackend()) for r in range(3)]
+    assert [(p.limbs.start, p.limbs.stop) for p in pipes] == [(0, 6), (6, 11), (11, 16)]
+    assert all(p.owner_last == 2 for p in pipes)
+
+
+# ---------------------------------------------------------------------------
+# GPU: simulated ranks (threads) on one MI355X through librnsntt
+# ---------------------------------------------------------------------------
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_limb_sharded_gpu_threads_match_unsharded(gpu, world):
+    import threading
+
+    import rns_ntt as rn
+    from rns_ntt.sharded import GpuBackend, LimbShardedPipeline, ThreadComm
+
+    n, L, B, seed = 4096, 8, 2, 11
+    mods = rn.generate_primes(31, L, n)
+    cts, key_a, key_b = _inputs(mods, n, B, seed)
+    comm = ThreadComm(world)
+    results, errors = [None] * world, []
+
+    def rank_main(r):
+        try:
+            pipe = LimbShardedPipeline(mods, n, comm.rank_view(r), GpuBackend(0))
+            relin, resc = _run_rank(pipe, cts, key_a, key_b)
+            results[r] = (r, (pipe.limbs.start, pipe.limbs.stop), relin, resc)
+        except BaseException as e:  # surface thread failures in the test
+            errors.append(e)
+            comm._bar.abort()
+
+    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=600)
+    assert not errors, errors
+    got = _assemble(results)
+
+    # unsharded library path (oracle-checked elsewhere) ...
+    Bf = rn.RnsBasis(mods, n)
+    c = [rn.RnsPoly.from_channels(x, Bf) for x in cts]
+    key = rn.RnsGadgetKey.from_channels(key_a, key_b, Bf)
+    m = rn.mul_ciphertexts_gadget(rn.Ciphertext(c[0], c[1]), rn.Ciphertext(c[2], c[3]), key)
+    r = rn.rescale_ciphertext(m)
+    for g, w in zip(got, (m.c0.channels(), m.c1.channels(), r.c0.channels(), r.c1.channels())):
+        assert np.array_equal(g, w)
+    # ... and the oracle on one ciphertext
+    want = _oracle_reference(mods, n, [x[:1] for x in cts], key_a, key_b)
+    for g, w in zip(got, want):
+        assert np.array_equal(g[:1], w)
+
+
+@pytest.mark.gpu
+def test_keyswitch_ext_and_rescale_ext_match_fused(gpu):
+    """rnt_ct_tensor + rnt_keyswitch_ext (source = the local d2) equals the
+    fused rnt_ct_mul_relin; rnt_rescale_ext by the own last limb equals
+    rnt_rescale; by a foreign modulus it keeps every limb."""
+    import rns_ntt as rn
+
+    n, L, B = 1024, 4, 3
+    mods = rn.generate_primes(31, L + 1, n)
+    base, extra = mods[:L], mods[L]
+    cts, key_a, key_b = _inputs(base, n, B, 3)
+    Bf = rn.RnsBasis(base, n)
+    c = [rn.RnsPoly.from_channels(x, Bf) for x in cts]
+    key = rn.RnsGadgetKey.from_channels(key_a, key_b, Bf)
+    d0, d1, d2 = rn.ct_tensor(*c)
+    ptr, wb = d2.device_ptr()
+    assert wb == 4 and ptr != 0
+    o0, o1 = rn.keyswitch_ext(ptr, L, key, Bf, B, d0, d1)
+    m = rn.mul_ciphertexts_gadget(rn.Ciphertext(c[0], c[1]), rn.Ciphertext(c[2], c[3]), key)
+    assert np.array_equal(o0.channels(), m.c0.channels())
+    assert np.array_equal(o1.channels(), m.c1.channels())
+    # own last limb -> same as rescale
+    last_ptr = ptr + (L - 1) * B * n * wb
+    rs = rn.rescale_ext(d2, last_ptr, base[-1], Bf.drop_last(1))
+    assert np.array_equal(rs.channels(), d2.rescale().channels())
+    # a foreign modulus: every limb kept, matches the oracle formula
+    Bx = rn.RnsBasis(base + [extra], n)
+    xl = orc.uniform_poly([extra], n, np.random.default_rng(9), batch=B)[:, 0]  # [B][N] mod extra
+    full = np.concatenate([d2.channels(), xl[:, None, :]], axis=1)
+    want = rn.RnsPoly.from_channels(full, Bx).rescale().channels()
+    xdev = rn.RnsPoly.from_channels(xl[:, None, :], rn.RnsBasis([extra], n))
+    xptr, _ = xdev.device_ptr()
+    got = rn.rescale_ext(d2, xptr, extra, Bf)
+    assert np.array_equal(got.channels(), want)

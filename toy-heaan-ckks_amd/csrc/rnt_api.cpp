@@ -183,6 +183,7 @@ rnt::Tables::~Tables() {
     if (join_ev[i]) (void)hipEventDestroy(join_ev[i]);
   }
   if (fork_ev) (void)hipEventDestroy(fork_ev);
+  for (auto& e : resc_ext) (void)hipFree(e.second);
   (void)hipFree(tw_fwd);
   (void)hipFree(tw_inv);
   (void)hipFree(lconst);
@@ -394,6 +395,7 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
 static void ctx_release(const rnt_ctx* ctx) {
   if (ctx && const_cast<rnt_ctx*>(ctx)->refs.fetch_sub(1) == 1) delete ctx;
 }
+static void ctx_retain(const rnt_ctx* ctx) { const_cast<rnt_ctx*>(ctx)->refs.fetch_add(1); }
 
 extern "C" int rnt_ctx_destroy(rnt_ctx* ctx) {
   ctx_release(ctx);  // freed once its last buffer is freed too
@@ -499,11 +501,34 @@ extern "C" int rnt_buf_free(rnt_buf* b) {
     (void)hipSetDevice(b->ctx->t->device);
     (void)hipStreamSynchronize(b->ctx->t->stream);
   }
-  (void)hipFree(b->data);
+  if (b->owns) (void)hipFree(b->data);
   (void)hipFree(b->ws);
   (void)hipFree(b->stage);
   ctx_release(b->ctx);
   delete b;
+  return RNT_OK;
+}
+
+extern "C" int rnt_buf_wrap(const rnt_ctx* ctx, void* device_ptr, size_t n_polys, int in_ntt,
+                            rnt_buf** out) {
+  if (!ctx || !device_ptr || !out) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  if (n_polys == 0) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_buf_wrap: empty batch");
+  rnt_buf* b = new (std::nothrow) rnt_buf;
+  if (!b) return fail(RNT_ERR_OUT_OF_MEMORY, "rnt_buf_wrap");
+  b->ctx = ctx;
+  b->n_polys = n_polys;
+  b->data = device_ptr;
+  b->in_ntt = in_ntt ? 1 : 0;
+  b->owns = false;
+  ctx_retain(ctx);
+  *out = b;
+  return RNT_OK;
+}
+
+extern "C" int rnt_buf_device_ptr(const rnt_buf* b, void** device_ptr, size_t* word_bytes_out) {
+  if (!b || !device_ptr) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  *device_ptr = b->data;
+  if (word_bytes_out) *word_bytes_out = word_bytes(b->ctx->t.get());
   return RNT_OK;
 }
 
@@ -781,6 +806,75 @@ extern "C" int rnt_rescale(rnt_buf* out, const rnt_buf* in) {
   return RNT_OK;
 }
 
+// Device constants {inv[L], invp[L]} for rescaling by an external modulus.
+static int resc_ext_table(const rnt_ctx* ctx, uint64_t q_last, const void** inv, const void** invp) {
+  rnt::Tables* t = ctx->t.get();
+  const size_t Lr = t->L;  // table covers every limb of the root basis
+  std::lock_guard<std::mutex> g(t->resc_mu);
+  for (auto& e : t->resc_ext)
+    if (e.first == q_last) {
+      *inv = e.second;
+      *invp = (const char*)e.second + Lr * word_bytes(t);
+      return RNT_OK;
+    }
+  const unsigned wbits = t->wide ? 64 : 32;
+  std::vector<uint64_t> h(2 * Lr);
+  for (size_t l = 0; l < Lr; ++l) {
+    const uint64_t ql = t->moduli[l];
+    if (ql == q_last) {  // the limb being dropped: never read
+      h[l] = h[Lr + l] = 0;
+      continue;
+    }
+    const uint64_t v = rnt::host::invmod(q_last % ql, ql);
+    if (v == 0)
+      return fail(RNT_ERR_BAD_ARGUMENT, "rescale: modulus %" PRIu64 " is not coprime to %" PRIu64, q_last, ql);
+    h[l] = v;
+    h[Lr + l] = rnt::host::shoup_companion(v, ql, wbits);
+  }
+  void* d = nullptr;
+  const size_t wb = word_bytes(t);
+  HIP_TRY(hipMalloc(&d, 2 * Lr * wb), "hipMalloc(rescale constants)");
+  if (wb == 4) {
+    std::vector<uint32_t> h32(h.begin(), h.end());
+    HIP_TRY(hipMemcpy(d, h32.data(), 2 * Lr * 4, hipMemcpyHostToDevice), "hipMemcpy");
+  } else {
+    HIP_TRY(hipMemcpy(d, h.data(), 2 * Lr * 8, hipMemcpyHostToDevice), "hipMemcpy");
+  }
+  t->resc_ext.push_back({q_last, d});
+  *inv = d;
+  *invp = (const char*)d + Lr * wb;
+  return RNT_OK;
+}
+
+extern "C" int rnt_rescale_ext(rnt_buf* out, const rnt_buf* in, const void* last_limb,
+                               uint64_t q_last) {
+  if (int rc = check_buf(out, "rnt_rescale_ext")) return rc;
+  if (int rc = check_buf(in, "rnt_rescale_ext")) return rc;
+  if (!last_limb) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_rescale_ext: null last limb");
+  if (in->in_ntt)
+    return fail(RNT_ERR_DOMAIN_MISMATCH, "rnt_rescale_ext: input must be in coefficient domain");
+  const size_t L = in->ctx->L;
+  const rnt::Tables* t = in->ctx->t.get();
+  // the owner of q_last drops it; every other shard keeps all its limbs
+  const size_t keep = (L > 0 && t->moduli[L - 1] == q_last) ? L - 1 : L;
+  if (keep == 0)
+    return fail(RNT_ERR_INVALID_MOD_DROP, "rescale: nothing left after dropping the last limb");
+  if (out->ctx->t != in->ctx->t || out->ctx->L != keep)
+    return fail(RNT_ERR_BASIS_MISMATCH, "rnt_rescale_ext: output basis must keep %zu limbs of the input's", keep);
+  if (out->n_polys != in->n_polys)
+    return fail(RNT_ERR_BAD_ARGUMENT, "rnt_rescale_ext: batch sizes differ");
+  if (int rc = set_device(in->ctx)) return rc;
+  const void* inv = nullptr;
+  const void* invp = nullptr;
+  if (int rc = resc_ext_table(in->ctx, q_last, &inv, &invp)) return rc;
+  rnt::Launch k = launch_for(in);
+  k.L = keep;
+  LAUNCH(k.t, rnt::K_RESCALE, rnt::launch_rescale_ext(k, out->data, in->data, last_limb, inv, invp),
+         "rescale_ext");
+  out->in_ntt = 0;
+  return RNT_OK;
+}
+
 extern "C" int rnt_mod_drop_last(rnt_buf* out, const rnt_buf* in) {
   if (int rc = check_buf(out, "rnt_mod_drop_last")) return rc;
   if (int rc = check_buf(in, "rnt_mod_drop_last")) return rc;
@@ -846,9 +940,11 @@ extern "C" int rnt_key_prepare(rnt_buf* key_a, rnt_buf* key_b) {
   if (int rc = check_buf(key_a, "rnt_key_prepare")) return rc;
   if (int rc = check_buf(key_b, "rnt_key_prepare")) return rc;
   if (int rc = check_same(key_a, key_b, "rnt_key_prepare")) return rc;
-  if (key_a->n_polys != key_a->ctx->L)
-    return fail(RNT_ERR_CHANNEL_COUNT, "gadget key must hold one poly per channel: expected %zu, got %zu",
-                key_a->ctx->L, key_a->n_polys);
+  // one poly per SOURCE limb: the basis' own channel count for rnt_keyswitch,
+  // the global count for a limb shard's rnt_keyswitch_ext (checked there)
+  if (key_a->n_polys != key_b->n_polys)
+    return fail(RNT_ERR_CHANNEL_COUNT, "gadget key halves differ: %zu vs %zu polys", key_a->n_polys,
+                key_b->n_polys);
   if (int rc = rnt_ntt_fwd(key_a)) return rc;
   return rnt_ntt_fwd(key_b);
 }
@@ -926,6 +1022,93 @@ extern "C" int rnt_keyswitch(rnt_buf* acc0, rnt_buf* acc1, const rnt_buf* d, con
       return rc;
   }
   acc0->in_ntt = acc1->in_ntt = 0;
+  return RNT_OK;
+}
+
+extern "C" int rnt_keyswitch_ext(rnt_buf* acc0, rnt_buf* acc1, const void* src, size_t src_limbs,
+                                 const rnt_buf* key_a, const rnt_buf* key_b, const rnt_buf* init0,
+                                 const rnt_buf* init1) {
+  if (int rc = check_buf(acc0, "rnt_keyswitch_ext")) return rc;
+  if (int rc = check_buf(acc1, "rnt_keyswitch_ext")) return rc;
+  if (int rc = check_same(acc0, acc1, "rnt_keyswitch_ext")) return rc;
+  if (!src || src_limbs == 0) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_keyswitch_ext: empty source");
+  if (int rc = check_buf(key_a, "key")) return rc;
+  if (int rc = check_buf(key_b, "key")) return rc;
+  if (key_a->ctx != acc0->ctx || key_b->ctx != acc0->ctx)
+    return fail(RNT_ERR_BASIS_MISMATCH, "key-switch: key and accumulator belong to different bases");
+  if (key_a->n_polys != src_limbs || key_b->n_polys != src_limbs)
+    return fail(RNT_ERR_CHANNEL_COUNT, "gadget key must hold one poly per source limb (%zu)", src_limbs);
+  if (!key_a->in_ntt || !key_b->in_ntt)
+    return fail(RNT_ERR_DOMAIN_MISMATCH, "key-switch: keys must be prepared (rnt_key_prepare)");
+  const rnt_buf* seeds[2] = {init0, init1};
+  for (const rnt_buf* sd : seeds) {
+    if (!sd) continue;
+    if (int rc = check_same(acc0, sd, "rnt_keyswitch_ext")) return rc;
+    if (!sd->in_ntt) return fail(RNT_ERR_DOMAIN_MISMATCH, "key-switch seeds must be in the NTT domain");
+    if (sd->n_polys != acc0->n_polys) return fail(RNT_ERR_BAD_ARGUMENT, "key-switch seed batch differs");
+  }
+  if (acc0 == acc1) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_keyswitch_ext: outputs alias");
+  if (int rc = set_device(acc0->ctx)) return rc;
+  rnt::Launch k = launch_for(acc0);
+  const size_t Lt = k.L, Ls = src_limbs, n = k.t->n, wb = word_bytes(k.t), B = acc0->n_polys;
+  // polys per chunk: S is [Lt][Ls][Bc][N]
+  size_t bc = std::max<size_t>(1, ((size_t)1 << 30) / std::max<size_t>(1, Lt * Ls * n * wb));
+  bc = std::min(bc, B);
+  if (int rc = ensure_ws(acc0, (Lt * Ls + 2 * Lt) * bc * n * wb)) return rc;
+  const uint64_t src_ls = (uint64_t)B * n, full_ls = limb_stride(acc0);
+  for (size_t p0 = 0; p0 < B; p0 += bc) {
+    rnt::Launch kc = k;
+    kc.B = std::min(bc, B - p0);
+    kc.Ls = Ls;
+    const uint64_t cls = (uint64_t)kc.B * n;
+    char* S = (char*)acc0->ws;
+    char* U0 = S + Lt * Ls * kc.B * n * wb;
+    char* U1 = U0 + Lt * kc.B * n * wb;
+    const size_t off = p0 * n * wb;
+    LAUNCH(kc.t, rnt::K_KS_DECOMPOSE,
+           rnt::launch_ks_decompose(kc, S, (const char*)src + off, src_ls), "ks decompose");
+    const char* i0 = init0 ? (const char*)init0->data + off : nullptr;
+    const char* i1 = init1 ? (const char*)init1->data + off : nullptr;
+    LAUNCH(kc.t, rnt::K_KS_ROWS,
+           rnt::launch_ks_rows(kc, U0, U1, cls, S, key_a->data, key_b->data, limb_stride(key_a), i0,
+                               i1, full_ls),
+           "ks rows");
+    LAUNCH(kc.t, rnt::K_COL_INV,
+           rnt::launch_col_inv(kc, (char*)acc0->data + off, full_ls, U0, cls, 1, nullptr), "ks inverse");
+    LAUNCH(kc.t, rnt::K_COL_INV,
+           rnt::launch_col_inv(kc, (char*)acc1->data + off, full_ls, U1, cls, 1, nullptr), "ks inverse");
+  }
+  acc0->in_ntt = acc1->in_ntt = 0;
+  return RNT_OK;
+}
+
+extern "C" int rnt_ct_tensor(rnt_buf* d0, rnt_buf* d1, rnt_buf* d2, const rnt_buf* c0,
+                             const rnt_buf* c1, const rnt_buf* c0p, const rnt_buf* c1p) {
+  const rnt_buf* all[7] = {d0, d1, d2, c0, c1, c0p, c1p};
+  for (const rnt_buf* b : all)
+    if (int rc = check_buf(b, "rnt_ct_tensor")) return rc;
+  for (int i = 1; i < 7; ++i)
+    if (int rc = check_same(all[0], all[i], "rnt_ct_tensor")) return rc;
+  if (c0->in_ntt || c1->in_ntt || c0p->in_ntt || c1p->in_ntt)
+    return fail(RNT_ERR_DOMAIN_MISMATCH, "rnt_ct_tensor: inputs must be in coefficient domain");
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 7; ++j)
+      if (i != j && all[i] == all[j])
+        return fail(RNT_ERR_BAD_ARGUMENT, "rnt_ct_tensor: outputs must not alias other operands");
+  if (int rc = set_device(c0->ctx)) return rc;
+  rnt::Launch k = launch_for(c0);
+  const size_t L = k.L, n = k.t->n, wb = word_bytes(k.t);
+  if (int rc = ensure_ws(d0, 4 * L * c0->n_polys * n * wb)) return rc;
+  char* T[4];
+  for (int i = 0; i < 4; ++i) T[i] = (char*)d0->ws + i * L * c0->n_polys * n * wb;
+  const uint64_t ls = limb_stride(c0);
+  LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, T[0], c0->data, T[1], c1->data, ls, ls), "tensor column");
+  LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, T[2], c0p->data, T[3], c1p->data, ls, ls), "tensor column");
+  LAUNCH(k.t, rnt::K_TENSOR_ROWS,
+         rnt::launch_tensor_rows(k, d0->data, d1->data, d2->data, T[0], T[1], T[2], T[3], ls), "tensor rows");
+  LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, d2->data, ls, d2->data, ls, 1, nullptr), "d2 inverse");
+  d0->in_ntt = d1->in_ntt = 1;
+  d2->in_ntt = 0;
   return RNT_OK;
 }
 

@@ -80,6 +80,10 @@ struct Tables {
   hipEvent_t fork_ev = nullptr;
   hipEvent_t join_ev[kAux] = {};
   std::mutex aux_mu;
+  // rnt_rescale_ext constants per external last modulus: device arrays
+  // {inv[L], invp[L]} with inv[l] = (q_last mod q_l)^-1 mod q_l.
+  std::mutex resc_mu;
+  std::vector<std::pair<uint64_t, void*>> resc_ext;
   struct Prof* prof = nullptr;  // per-kernel event timing (rnt_profile_*)
   ~Tables();
 };
@@ -125,6 +129,7 @@ struct rnt_buf {
   size_t ws_bytes = 0;
   void* stage = nullptr;      // u64 host-format staging for upload/download
   size_t stage_bytes = 0;
+  bool owns = true;           // false: rnt_buf_wrap view of caller memory
 };
 
 namespace rnt {
@@ -142,6 +147,8 @@ struct Launch {
   size_t L;            // limbs processed (prefix of the root basis)
   size_t B;            // polys per buffer
   hipStream_t s;
+  size_t Ls = 0;       // key-switch source limbs (0: same as L)
+  size_t src_limbs() const { return Ls ? Ls : L; }
 };
 
 // ---- launchers (rnt_kernels.hip), W-dispatched by t->wide ---------------
@@ -163,6 +170,10 @@ hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a,
                               const void* b);
 // k.L = limbs of the input; output has k.L - 1 (same poly count / stride B*N).
 hipError_t launch_rescale(const Launch& k, void* out, const void* in);
+// out limb l = (in_l - (last mod q_l)) * inv[l] (Shoup pair inv/invp, device
+// arrays of k.L words); `last` is a [B][N] plane of residues mod q_last.
+hipError_t launch_rescale_ext(const Launch& k, void* out, const void* in, const void* last,
+                              const void* inv, const void* invp);
 hipError_t launch_automorphism(const Launch& k, void* out, const void* in, uint64_t g);
 // host u64 [B][L][N] staging <-> device; err_index receives the smallest
 // offending flat index (UINT64_MAX if none) for non-reduced input.

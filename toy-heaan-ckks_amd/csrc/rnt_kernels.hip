@@ -267,7 +267,7 @@ k_ks_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32
   const uint32_t C = 1u << log_c;
   const uint64_t N = 1ull << log_n;
   const uint32_t j1 = (uint32_t)(gid & (C - 1));
-  uint64_t rest = gid >> log_c;  // ((j*L + i)*B + p)
+  uint64_t rest = gid >> log_c;  // ((j*L + i)*B + p), L = source limbs
   const uint32_t p = (uint32_t)(rest % B);
   rest /= B;
   const uint32_t i = (uint32_t)(rest % L);
@@ -950,17 +950,18 @@ k_elementwise(W* __restrict__ out, const W* __restrict__ a, const W* __restrict_
 // rescale_into (poly.rs:212-225): out[l] = (c_l - (c_last mod q_l)) * q_last^-1.
 template <class W>
 __global__ void __launch_bounds__(256)
-k_rescale(W* __restrict__ out, const W* __restrict__ in, TabPtrs<W> tp, uint32_t last,
+k_rescale(W* __restrict__ out, const W* __restrict__ in, const W* __restrict__ lastp,
+          const W* __restrict__ inv_t, const W* __restrict__ invp_t, TabPtrs<W> tp,
           uint64_t ls_in, uint64_t ls_out, uint64_t poly_words, uint64_t total) {
   const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= total) return;
   const uint32_t l = (uint32_t)(gid / poly_words);
   const uint64_t off = gid - (uint64_t)l * poly_words;
   const LimbConst<W> lc = tp.lc[l];
-  const W inv = tp.resc[(uint64_t)last * tp.Lroot + l];
-  const W invp = tp.rescp[(uint64_t)last * tp.Lroot + l];
+  const W inv = inv_t[l];    // (q_last mod q_l)^-1 mod q_l
+  const W invp = invp_t[l];
   const W ci = in[(uint64_t)l * ls_in + off];
-  const W cl = shoup_mul<W>(in[(uint64_t)last * ls_in + off], (W)1, lc.one_p, lc.q);
+  const W cl = shoup_mul<W>(lastp[off], (W)1, lc.one_p, lc.q);  // canonical c_last mod q_l (R5)
   out[(uint64_t)l * ls_out + off] = shoup_mul<W>(sub_mod<W>(ci, cl, lc.q), inv, invp, lc.q);
 }
 
@@ -1289,8 +1290,25 @@ static hipError_t rescale_t(const Launch& k, void* out, const void* in) {
   const uint64_t pw = (uint64_t)k.B << k.t->log_n;
   const uint64_t total = pw * (k.L - 1);
   if (total == 0) return hipSuccess;
+  const TabPtrs<W> tp = tab_ptrs<W>(k.t);
+  const uint64_t last = k.L - 1;
   hipLaunchKernelGGL((k_rescale<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, (W*)out,
-                     (const W*)in, tab_ptrs<W>(k.t), (uint32_t)(k.L - 1), pw, pw, pw, total);
+                     (const W*)in, (const W*)in + last * pw, tp.resc + last * tp.Lroot,
+                     tp.rescp + last * tp.Lroot, tp, pw, pw, pw, total);
+  return hipGetLastError();
+}
+
+// Rescale by a limb held outside the buffer (limb-sharded pipelines: the
+// broadcast last limb of the global basis): out limbs 0..k.L-1 from in's.
+template <class W>
+static hipError_t rescale_ext_t(const Launch& k, void* out, const void* in, const void* lastp,
+                                const void* inv, const void* invp) {
+  const uint64_t pw = (uint64_t)k.B << k.t->log_n;
+  const uint64_t total = pw * k.L;
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_rescale<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, (W*)out,
+                     (const W*)in, (const W*)lastp, (const W*)inv, (const W*)invp, tab_ptrs<W>(k.t),
+                     pw, pw, pw, total);
   return hipGetLastError();
 }
 
@@ -1365,8 +1383,9 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
   const Geom g = geom_for(k.t->log_n);
   if ((uint64_t)k.L * k.B == 0) return hipSuccess;
   const TabPtrs<W> tp = tab_ptrs<W>(k.t);
+  const uint32_t Ls = (uint32_t)k.src_limbs();  // source limbs i; target limbs j = k.L
   if (g.log_r >= 5) {
-    const dim3 grid = col_grid(k, g, (uint32_t)k.L, (uint32_t)k.L);
+    const dim3 grid = col_grid(k, g, Ls, (uint32_t)k.L);
     if (grid.x == 0) return hipErrorInvalidConfiguration;
     hipError_t e = hipSuccess;
 #define RNT_L2(R, TC)                                                                         \
@@ -1374,7 +1393,7 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
   if (e != hipSuccess) return e;                                                              \
   hipLaunchKernelGGL((k_colt_decompose<W, R, TC>), grid, dim3(ColGeo<R, TC>::THREADS),        \
                      (col_lds<W, R, TC>()), k.s, (W*)S, (const W*)d, tp, g.log_n, g.log_c,      \
-                     (uint32_t)k.L, (uint32_t)k.B, d_ls)
+                     Ls, (uint32_t)k.B, d_ls)
 #define RNT_L(R)                          \
   if (col_log_tc(g) == 6) {               \
     RNT_L2(R, 6);                         \
@@ -1386,11 +1405,10 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
 #undef RNT_L2
     return hipGetLastError();
   }
-  const uint64_t total = (uint64_t)k.L * k.L * k.B * g.c;
+  const uint64_t total = (uint64_t)k.L * Ls * k.B * g.c;
 #define RNT_L(R)                                                                               \
   hipLaunchKernelGGL((k_ks_decompose<W, R>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,  \
-                     (W*)S, (const W*)d, tp, g.log_n, g.log_c, (uint32_t)k.L, (uint32_t)k.B, \
-                     d_ls, total)
+                     (W*)S, (const W*)d, tp, g.log_n, g.log_c, Ls, (uint32_t)k.B, d_ls, total)
   RNT_DISPATCH_LOGR(g.log_r, RNT_L)
 #undef RNT_L
   return hipGetLastError();
@@ -1411,7 +1429,7 @@ static hipError_t ks_rows_launch(const Launch& k, void* u0, void* u1, uint64_t l
   hipLaunchKernelGGL((k_ks_rows<W, LOG_C>), dim3(blocks), dim3(G::THREADS), lds, k.s, (W*)u0,
                      (W*)u1, (const W*)S, (const W*)key_a, (const W*)key_b, key_ls,
                      (const W*)init0, (const W*)init1, init_ls, tab_ptrs<W>(k.t), g.log_n,
-                     (uint32_t)k.L, (uint32_t)k.B, ls, rows);
+                     (uint32_t)k.src_limbs(), (uint32_t)k.B, ls, rows);
   return hipGetLastError();
 }
 
@@ -1478,6 +1496,11 @@ hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a,
 }
 hipError_t launch_rescale(const Launch& k, void* out, const void* in) {
   RNT_WIDE(rescale_t<uint32_t>(k, out, in), rescale_t<uint64_t>(k, out, in));
+}
+hipError_t launch_rescale_ext(const Launch& k, void* out, const void* in, const void* last,
+                              const void* inv, const void* invp) {
+  RNT_WIDE(rescale_ext_t<uint32_t>(k, out, in, last, inv, invp),
+           rescale_ext_t<uint64_t>(k, out, in, last, inv, invp));
 }
 hipError_t launch_automorphism(const Launch& k, void* out, const void* in, uint64_t g) {
   RNT_WIDE(automorphism_t<uint32_t>(k, out, in, g), automorphism_t<uint64_t>(k, out, in, g));

@@ -244,6 +244,30 @@ class RnsPoly:
         check(load().rnt_upload(p._h, _u64p(ch), ch.shape[0], ch.shape[1], 1 if in_ntt_domain else 0))
         return p
 
+    @classmethod
+    def wrap(cls, basis: RnsBasis, device_ptr: int, n_polys: int, in_ntt_domain: bool = False,
+             owner=None) -> "RnsPoly":
+        """A non-owning view of caller device memory laid out [L][n_polys][N]
+        in the basis' device word width (``word_bytes``); ``owner`` (e.g. the
+        torch tensor holding the memory) is kept alive with the view.  Used
+        by the limb-sharded pipeline to hand buffers to RCCL collectives."""
+        p = cls.__new__(cls)
+        h = ctypes.c_void_p()
+        check(load().rnt_buf_wrap(basis.handle, ctypes.c_void_p(device_ptr), n_polys,
+                                  1 if in_ntt_domain else 0, ctypes.byref(h)))
+        p._h = h
+        p.basis = basis
+        p.n_polys = n_polys
+        p._owner = owner
+        return p
+
+    def device_ptr(self) -> tuple[int, int]:
+        """(device address of the [L][B][N] storage, word bytes)."""
+        ptr = ctypes.c_void_p()
+        wb = ctypes.c_size_t()
+        check(load().rnt_buf_device_ptr(self._h, ctypes.byref(ptr), ctypes.byref(wb)))
+        return int(ptr.value or 0), int(wb.value)
+
     # -- accessors (poly.rs:118-129) ----------------------------------------
     @property
     def handle(self):
@@ -425,3 +449,46 @@ def rescale_ciphertext(ct: Ciphertext) -> Ciphertext:
     out1 = RnsPoly(new_basis, ct.c0.n_polys)
     check(load().rnt_ct_rescale(out0.handle, out1.handle, ct.c0.handle, ct.c1.handle))
     return Ciphertext(out0, out1, ct.logp - bits_dropped, ct.logq - bits_dropped)
+
+
+# ---------------------------------------------------------------------------
+# limb-sharded building blocks (include/rnsntt.h)
+# ---------------------------------------------------------------------------
+
+
+def ct_tensor(c0: RnsPoly, c1: RnsPoly, c0p: RnsPoly, c1p: RnsPoly,
+              d2_out: Optional[RnsPoly] = None) -> tuple[RnsPoly, RnsPoly, RnsPoly]:
+    """Tensor product (engine.rs:480-493) on this basis' limbs: d0, d1 in the
+    NTT domain (key-switch seeds), d2 in the coefficient domain (written into
+    ``d2_out`` when given, e.g. a wrapped collective buffer)."""
+    basis, B = c0.basis, c0.n_polys
+    d0, d1 = RnsPoly(basis, B), RnsPoly(basis, B)
+    d2 = d2_out if d2_out is not None else RnsPoly(basis, B)
+    check(load().rnt_ct_tensor(d0.handle, d1.handle, d2.handle, c0.handle, c1.handle,
+                               c0p.handle, c1p.handle))
+    return d0, d1, d2
+
+
+def keyswitch_ext(src_ptr: int, src_limbs: int, key: RnsGadgetKey, basis: RnsBasis, n_polys: int,
+                  init0: Optional[RnsPoly] = None, init1: Optional[RnsPoly] = None,
+                  out0: Optional[RnsPoly] = None, out1: Optional[RnsPoly] = None
+                  ) -> tuple[RnsPoly, RnsPoly]:
+    """Gadget sum (engine.rs:505-528) for this basis' (target) limbs over
+    ``src_limbs`` coefficient-domain source limbs at device address
+    ``src_ptr`` ([src_limbs][n_polys][N] words); seeds in the NTT domain."""
+    acc0 = out0 if out0 is not None else RnsPoly(basis, n_polys)
+    acc1 = out1 if out1 is not None else RnsPoly(basis, n_polys)
+    check(load().rnt_keyswitch_ext(acc0.handle, acc1.handle, ctypes.c_void_p(src_ptr), src_limbs,
+                                   key.a.handle, key.b.handle,
+                                   init0.handle if init0 is not None else None,
+                                   init1.handle if init1 is not None else None))
+    return acc0, acc1
+
+
+def rescale_ext(x: RnsPoly, last_ptr: int, q_last: int, out_basis: RnsBasis,
+                out: Optional[RnsPoly] = None) -> RnsPoly:
+    """rescale_into (poly.rs:187-228) by an external last limb: residues mod
+    ``q_last`` ([n_polys][N] words, coefficient domain) at ``last_ptr``."""
+    o = out if out is not None else RnsPoly(out_basis, x.n_polys)
+    check(load().rnt_rescale_ext(o.handle, x.handle, ctypes.c_void_p(last_ptr), int(q_last)))
+    return o

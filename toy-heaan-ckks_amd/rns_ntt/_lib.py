@@ -85,6 +85,11 @@ SIGNATURES = {
     "rnt_upload_coeffs": (c_int, [_P, _I64P, c_size_t]),
     "rnt_download": (c_int, [_P, _U64P, c_size_t]),
     "rnt_copy": (c_int, [_P, _P]),
+    "rnt_buf_wrap": (c_int, [_P, c_void_p, c_size_t, c_int, POINTER(c_void_p)]),
+    "rnt_buf_device_ptr": (c_int, [_P, POINTER(c_void_p), POINTER(c_size_t)]),
+    "rnt_ct_tensor": (c_int, [_P, _P, _P, _P, _P, _P, _P]),
+    "rnt_keyswitch_ext": (c_int, [_P, _P, c_void_p, c_size_t, _P, _P, _P, _P]),
+    "rnt_rescale_ext": (c_int, [_P, _P, c_void_p, c_uint64]),
     "rnt_ntt_fwd": (c_int, [_P]),
     "rnt_ntt_inv": (c_int, [_P]),
     "rnt_mul": (c_int, [_P, _P, _P]),
