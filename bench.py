@@ -1,14 +1,22 @@
 #!/usr/bin/env python3
 """RNS-NTT poly-mul throughput on MI355X (BASELINE.json metric).
 
-Workload (BASELINE configs[3] ring, the metric's quoted shape): N = 2^16,
+Default workload (the metric's shape, BASELINE configs[3] ring): N = 2^16,
 16 RNS primes from the reference's generate_primes(31, 16, N) rule.  One
 step = one batched coefficient-domain poly-mul c = a * b (poly.rs:307-329,
-the `a *= &b` of every CkksEngine call site) over `--batch` pairs per GPU,
-inputs resident in HBM.  Multi-GPU: one process per GPU (torchrun); the
-batch is sharded across ranks with no data-path collective (each rank owns
-its own pairs), so scaling is weak; only the timing barrier / max-reduce
-crosses ranks (gloo control plane).
+the `a *= &b` of every CkksEngine call site) over `--batch` pairs' worth of
+work per GPU, inputs resident in HBM.
+
+Multi-GPU: one process per GPU (torchrun).  `--shard limb`
+(default) gives rank r a contiguous run of the 16 limbs of a global batch of
+batch * N_gpus pairs -- the north star's limb sharding; `--shard batch`
+gives each rank its own `--batch` pairs over all limbs.  Both keep the work
+per GPU fixed (weak scaling) and need no data-path collective for poly-mul;
+only the timing barrier / max-reduce crosses ranks (gloo control plane).
+
+`--workload ctmul` times BASELINE config 4's pipeline instead: ct x ct ->
+gadget relinearisation -> rescale, limb-sharded with the RCCL all-gather of
+d2 and broadcast of the last limb (rns_ntt.sharded).
 
 Prints ONE JSON line on rank 0.
 """
@@ -26,7 +34,8 @@ PKG = os.path.join(REPO, "toy-heaan-ckks_amd")
 sys.path.insert(0, PKG)
 
 METRIC = "RNS-NTT poly-muls/sec (N=2^16, 16 primes) at 1/2/4/8 GPUs; % HBM roofline"
-HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); 6.29 TB/s measured copy
+CT_METRIC = "ct x ct -> relin -> rescale ciphertexts/sec (N=2^16, 16 primes, limb-sharded)"
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); ~6.3 TB/s achievable
 
 
 def log(*a):
@@ -38,7 +47,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--workload", choices=("polymul", "ctmul"), default="polymul")
+    p.add_argument("--shard", choices=("limb", "batch"), default="limb")
     p.add_argument("--batch", type=int, default=256, help="poly-mul pairs per GPU per step")
+    p.add_argument("--ct-batch", type=int, default=128, help="ciphertext pairs per GPU per step (ctmul)")
     p.add_argument("--log-n", type=int, default=16)
     p.add_argument("--limbs", type=int, default=16)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
@@ -55,14 +67,19 @@ def relaunch_with_torchrun(args) -> int:
     return subprocess.call(cmd)
 
 
+def oracle():
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle as orc
+
+    return orc
+
+
 def cpu_baseline(mod, n, budget_s):
     """The oracle (reference-faithful C restatement, u128 `%`) on this host's
     cores: a bounded sample of the same workload, timed in this run."""
     import numpy as np
 
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import pyoracle as orc
-
+    orc = oracle()
     threads = max(1, min(16, os.cpu_count() or 1))
     Bo = orc.Basis(mod, n)
     rng = np.random.default_rng(11)
@@ -83,6 +100,237 @@ def cpu_baseline(mod, n, budget_s):
     }
 
 
+def uniform(rng, mods, count, n):
+    import numpy as np
+
+    q = np.array(mods, dtype=np.uint64)[None, :, None]
+    return rng.integers(0, 1 << 62, size=(count, len(mods), n), dtype=np.uint64) % q
+
+
+def traffic_for(kernel, batch, log_n, L):
+    """HBM bytes per launch of `kernel` from the committed PMC passes
+    (profiles/pmc_traffic.json, tools/pmc_summary.py) when they were taken
+    on this exact shape; else None."""
+    tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(tpath) as f:
+            t = json.load(f)
+        kt = t.get("kernels", {}).get(kernel)
+        if kt and t.get("batch") == batch and t.get("log_n") == log_n and t.get("L") == L:
+            return kt.get("bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def run_polymul(args, comm, world, rank, local_rank):
+    import numpy as np
+
+    import rns_ntt as rn
+    from rns_ntt.dist import limb_shard, weak_throughput
+
+    n = 1 << args.log_n
+    L = args.limbs
+    mod = rn.generate_primes(31, L, n)
+    if args.shard == "limb":
+        limbs = limb_shard(L, world, rank)
+        batch = args.batch * world  # global batch, every rank holds its limbs of all of it
+    else:
+        limbs = range(L)
+        batch = args.batch
+    lmod = mod[limbs.start:limbs.stop]
+    Lr = len(lmod)
+    B = rn.RnsBasis(lmod, n, device=local_rank)
+    wb = 4 if max(lmod) < (1 << 31) else 8
+
+    # synthetic inputs: 16 seeded unique pairs tiled to the batch
+    rng = np.random.default_rng(1234 + (rank if args.shard == "batch" else 0))
+    uniq = min(16, batch)
+    a_u = uniform(rng, mod, uniq, n)[:, limbs.start:limbs.stop]
+    b_u = uniform(rng, mod, uniq, n)[:, limbs.start:limbs.stop]
+    reps = (batch + uniq - 1) // uniq
+    a = rn.RnsPoly.from_channels(np.tile(a_u, (reps, 1, 1))[:batch], B)
+    b = rn.RnsPoly.from_channels(np.tile(b_u, (reps, 1, 1))[:batch], B)
+    out = rn.RnsPoly(B, batch)
+    lib = rn.load()
+
+    for _ in range(args.warmup):
+        rn.check(lib.rnt_mul(out.handle, a.handle, b.handle))
+    B.sync()
+    comm.barrier()
+    B.profile_enable(True)
+    B.sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rn.check(lib.rnt_mul(out.handle, a.handle, b.handle))
+    B.sync()
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = comm.max(t1 - t0)
+    kernels = {}
+    for k in ("col_fwd", "row_mul", "col_inv"):
+        cnt, ms = B.profile_read(k)
+        kernels[k] = {"launches": cnt, "avg_ms": ms / cnt if cnt else None, "total_ms": ms}
+    B.profile_enable(False)
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = weak_throughput(args.batch, world, elapsed, args.steps)  # global poly-muls / s
+
+    # spot parity of the timed output (this rank's limbs of pair 0) vs the oracle
+    parity_ok = True
+    if rank == 0:
+        orc = oracle()
+        parity_ok = bool(np.array_equal(out.channels()[0], orc.mul(orc.Basis(lmod, n), a_u[0], b_u[0])))
+
+    # roofline of the dominant kernel: its algorithmic bytes per launch (at
+    # the device word width) / its average launch time, measured with HIP
+    # events on the library stream
+    elem = Lr * batch * n
+    step_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb}
+    dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
+    alg_bytes = {k: step_bytes[k] * args.steps / max(kernels[k]["launches"], 1) for k in kernels}
+    achieved = alg_bytes[dom] / (kernels[dom]["avg_ms"] * 1e-3) / 1e9
+    per_gpu = value / world
+    roofline = {
+        "bound": "hbm",
+        "kernel": dom,
+        "achieved": achieved,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": traffic_for(dom, batch, args.log_n, Lr),
+        "alg_bytes_per_launch": alg_bytes[dom],
+        # the metric's "% HBM roofline" (SURVEY §8d: 3*L*N*8 B per poly-mul)
+        "whole_op_GBs": per_gpu * 3 * L * n * wb / 1e9,
+        "whole_op_frac": per_gpu * 3 * L * n * wb / 1e9 / HBM_PEAK_GBS,
+        "whole_op_frac_u64_equiv": per_gpu * 3 * L * n * 8 / 1e9 / HBM_PEAK_GBS,
+        "kernels": kernels,
+    }
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(mod, n, args.cpu_seconds)
+    par = (f"limb-sharded x{world} ({Lr} of {L} limbs per GPU), no collective" if args.shard == "limb"
+           else f"batch-sharded x{world}, no collective")
+    return {
+        "metric": METRIC,
+        "value": value,
+        "unit": "poly-muls/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32" if wb == 4 else "u64",
+        "data": "synthetic (seeded uniform residues)",
+        "config": {
+            "workload": f"coefficient-domain RNS-NTT poly-mul c=a*b, N=2^{args.log_n}, L={L} x 31-bit primes",
+            "N": n,
+            "L": L,
+            "pairs_per_gpu_per_step": args.batch,
+            "global_batch": args.batch * world,
+            "parallelism": par,
+            "parity_spot_check": parity_ok,
+        },
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+
+
+def run_ctmul(args, comm, world, rank, local_rank):
+    """BASELINE config 4: ct x ct + gadget relin + rescale, limb-sharded."""
+    import numpy as np
+    import torch
+
+    import rns_ntt as rn
+    from rns_ntt.sharded import GpuBackend, LimbShardedPipeline, SingleComm, TorchDistComm
+
+    n = 1 << args.log_n
+    L = args.limbs
+    mod = rn.generate_primes(31, L, n)
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        import torch.distributed as dist
+
+        data_comm = TorchDistComm(dist.new_group(backend="nccl"))  # RCCL over xGMI
+    else:
+        data_comm = SingleComm()
+    B = args.ct_batch * world  # global ciphertext batch (weak scaling)
+    pipe = LimbShardedPipeline(mod, n, data_comm, GpuBackend(local_rank))
+    rng = np.random.default_rng(77)
+    uniq = min(4, B)
+    reps = (B + uniq - 1) // uniq
+    cts = [np.tile(uniform(rng, mod, uniq, n), (reps, 1, 1))[:B] for _ in range(4)]
+    key_a, key_b = uniform(rng, mod, L, n), uniform(rng, mod, L, n)
+    c = [pipe.upload(x) for x in cts]
+    key = pipe.upload_key(key_a, key_b)
+    state0 = (pipe.basis, pipe.moduli, list(pipe.counts), pipe.limbs, pipe.owner_last)
+
+    def step():
+        # every step starts from the same level (rescale drops a limb)
+        pipe.basis, pipe.moduli, counts, pipe.limbs, pipe.owner_last = state0
+        pipe.counts = list(counts)
+        m0, m1 = pipe.mul_relin(c[0], c[1], c[2], c[3], key)
+        return pipe.rescale(m0, m1)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = comm.max(t1 - t0)
+    value = B * args.steps / elapsed
+
+    parity_ok = None
+    cpu = None
+    if rank == 0 and world == 1:
+        orc = oracle()
+        ob = orc.Basis(mod, n)
+        t = time.perf_counter()
+        o0, _ = orc.mul_ciphertexts_gadget(ob, cts[0][0], cts[1][0], cts[2][0], cts[3][0], key_a, key_b)
+        want0 = orc.rescale(ob, o0)
+        cpu_s = time.perf_counter() - t
+        parity_ok = bool(np.array_equal(pipe.download(r[0])[0], want0))
+        if not args.no_cpu_baseline:
+            cpu = {"value": 1.0 / cpu_s, "unit": "ct-muls/s", "cores": 1, "kind": "port",
+                   "sample": f"1 ciphertext pair (N={n}, L={L}) through oracle mul_ciphertexts_gadget "
+                             f"+ rescale of c0, single thread, {cpu_s:.1f} s"}
+    # bytes per ciphertext (SURVEY §8d config 4): (4L + 2(L-1)) * N * 8
+    ct_bytes = (4 * L + 2 * (L - 1)) * n * 8
+    return {
+        "metric": CT_METRIC,
+        "value": value,
+        "unit": "ct-muls/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded uniform residues and key)",
+        "config": {
+            "workload": f"ct x ct + gadget relin + rescale, N=2^{args.log_n}, L={L} x 31-bit primes",
+            "ct_pairs_per_gpu_per_step": args.ct_batch,
+            "global_batch": B,
+            "parallelism": f"limb-sharded x{world}: RCCL all-gather of d2, broadcast of q_L limb",
+            "parity_spot_check": parity_ok,
+        },
+        "roofline": {"bound": "hbm", "kernel": "whole pipeline", "unit": "GB/s",
+                     "achieved": value / world * ct_bytes / 1e9, "peak": HBM_PEAK_GBS,
+                     "frac": value / world * ct_bytes / 1e9 / HBM_PEAK_GBS, "traffic": None},
+        "cpu_baseline": cpu,
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,138 +339,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
-    import numpy as np
-
-    import rns_ntt as rn  # loads librnsntt.so (HIP runtime) before torch
-    from rns_ntt.dist import Comm, weak_throughput
+    import rns_ntt  # noqa: F401  loads librnsntt.so (HIP runtime) before torch
+    from rns_ntt.dist import Comm
 
     comm = Comm.from_env()
-    barrier, max_over_ranks = comm.barrier, comm.max
-
-    n = 1 << args.log_n
-    L = args.limbs
-    mod = rn.generate_primes(31, L, n)
-    B = rn.RnsBasis(mod, n, device=local_rank)
-    batch = args.batch
-    wb = 4 if max(mod) < (1 << 31) else 8
-
-    # synthetic inputs: 16 seeded unique pairs tiled to the batch (rank-seeded)
-    rng = np.random.default_rng(1234 + rank)
-    uniq = min(16, batch)
-    qa = np.array(mod, dtype=np.uint64)[None, :, None]
-    a_u = (rng.integers(0, 1 << 62, size=(uniq, L, n), dtype=np.uint64) % qa)
-    b_u = (rng.integers(0, 1 << 62, size=(uniq, L, n), dtype=np.uint64) % qa)
-    reps = (batch + uniq - 1) // uniq
-    a = rn.RnsPoly.from_channels(np.tile(a_u, (reps, 1, 1))[:batch], B)
-    b = rn.RnsPoly.from_channels(np.tile(b_u, (reps, 1, 1))[:batch], B)
-    del a_u, b_u
-    out = rn.RnsPoly(B, batch)
-    lib = rn.load()
-
-    for _ in range(args.warmup):
-        rn.check(lib.rnt_mul(out.handle, a.handle, b.handle))
-    B.sync()
-    barrier()
-    B.profile_enable(True)
-    B.sync()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        rn.check(lib.rnt_mul(out.handle, a.handle, b.handle))
-    B.sync()
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = max_over_ranks(t1 - t0)
-    kernels = {}
-    for k in ("col_fwd", "row_mul", "col_inv"):
-        cnt, ms = B.profile_read(k)
-        kernels[k] = {"launches": cnt, "avg_ms": ms / cnt if cnt else None, "total_ms": ms}
-    B.profile_enable(False)
-
-    ms_per_step = elapsed / args.steps * 1e3
-    value = weak_throughput(batch, world, elapsed, args.steps)
-
-    # spot parity of the timed output against the first unique pair
+    run = run_ctmul if args.workload == "ctmul" else run_polymul
+    line = run(args, comm, world, rank, local_rank)
     if rank == 0:
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import pyoracle as orc
-
-        ch = out.channels()
-        Bo = orc.Basis(mod, n)
-        rng2 = np.random.default_rng(1234 + rank)
-        a_u = (rng2.integers(0, 1 << 62, size=(uniq, L, n), dtype=np.uint64) % qa)
-        b_u = (rng2.integers(0, 1 << 62, size=(uniq, L, n), dtype=np.uint64) % qa)
-        parity_ok = bool(np.array_equal(ch[0], orc.mul(Bo, a_u[0], b_u[0])))
-        del ch
-    else:
-        parity_ok = True
-
-    # roofline of the dominant kernel: algorithmic bytes per launch / average
-    # launch time (a step may issue several launches when the batch is
-    # chunked; bytes per launch = bytes per step * steps / launches)
-    elem = L * batch * n
-    step_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb}
-    dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
-    dom_ms = kernels[dom]["avg_ms"]
-    alg_bytes = {k: step_bytes[k] * args.steps / max(kernels[k]["launches"], 1) for k in kernels}
-    achieved = alg_bytes[dom] / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            with open(tpath) as f:
-                t = json.load(f)
-            kt = t.get("kernels", {}).get(dom)
-            if kt and t.get("batch") == batch and t.get("log_n") == args.log_n and t.get("L") == L:
-                traffic = kt.get("bytes_per_launch")
-        except Exception:
-            traffic = None
-    op_bytes = 3 * L * n * wb  # read a, read b, write c per poly-mul at the device word width
-    roofline = {
-        "bound": "hbm",
-        "kernel": dom,
-        "achieved": achieved,
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBS,
-        "traffic": traffic,
-        "alg_bytes_per_launch": alg_bytes[dom],
-        "whole_op_GBs": value / world * op_bytes / 1e9,
-        "whole_op_frac": value / world * op_bytes / 1e9 / HBM_PEAK_GBS,
-        "whole_op_frac_u64_equiv": value / world * 3 * L * n * 8 / 1e9 / HBM_PEAK_GBS,
-        "kernels": kernels,
-    }
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(mod, n, args.cpu_seconds)
-
-    if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "poly-muls/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32" if wb == 4 else "u64",
-            "data": "synthetic (seeded uniform residues)",
-            "config": {
-                "workload": f"coefficient-domain RNS-NTT poly-mul c=a*b, N=2^{args.log_n}, L={L} x 31-bit primes",
-                "N": n,
-                "L": L,
-                "batch_per_gpu": batch,
-                "global_batch": batch * world,
-                "parallelism": f"batch-sharded x{world}, no collective",
-                "parity_spot_check": parity_ok,
-            },
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
         print(json.dumps(line), flush=True)
     comm.close()
 

@@ -68,6 +68,19 @@ class TorchDistComm:
         return t
 
 
+class SingleComm:
+    """World of one: the joins are local."""
+
+    rank = 0
+    world = 1
+
+    def all_gather_limbs(self, local, counts: Sequence[int]):
+        return local
+
+    def broadcast(self, t, src: int):
+        return t
+
+
 class ThreadComm:
     """`world` simulated ranks as threads of one process (one GPU)."""
 
