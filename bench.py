@@ -35,6 +35,7 @@ sys.path.insert(0, PKG)
 
 METRIC = "RNS-NTT poly-muls/sec (N=2^16, 16 primes) at 1/2/4/8 GPUs; % HBM roofline"
 CT_METRIC = "ct x ct -> relin -> rescale ciphertexts/sec (N=2^16, 16 primes, limb-sharded)"
+ROT_METRIC = "rotation key-switches/sec (N=2^17, 32 primes, power-of-two Galois offsets)"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); ~6.3 TB/s achievable
 
 
@@ -47,10 +48,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=("polymul", "ctmul"), default="polymul")
+    p.add_argument("--workload", choices=("polymul", "ctmul", "rotate"), default="polymul")
     p.add_argument("--shard", choices=("limb", "batch"), default="limb")
     p.add_argument("--batch", type=int, default=256, help="poly-mul pairs per GPU per step")
     p.add_argument("--ct-batch", type=int, default=128, help="ciphertext pairs per GPU per step (ctmul)")
+    p.add_argument("--rot-batch", type=int, default=8, help="ciphertexts per rotation (rotate)")
     p.add_argument("--log-n", type=int, default=16)
     p.add_argument("--limbs", type=int, default=16)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
@@ -331,6 +333,81 @@ def run_ctmul(args, comm, world, rank, local_rank):
     }
 
 
+def run_rotate(args, comm, world, rank, local_rank):
+    """BASELINE config 5: rotate_ciphertext (engine.rs:412-463)
+    over all log2(N/2) power-of-two offsets, reusing one resident rotation
+    key (the arithmetic per offset is identical; one key per offset would be
+    2 GiB each).  Defaults to N = 2^17, L = 32 when --log-n/--limbs are the
+    poly-mul defaults."""
+    import numpy as np
+
+    import rns_ntt as rn
+
+    log_n = 17 if args.log_n == 16 else args.log_n
+    L = 32 if args.limbs == 16 else args.limbs
+    n = 1 << log_n
+    mod = rn.generate_primes(31, L, n)
+    Bs = rn.RnsBasis(mod, n, device=local_rank)
+    B = args.rot_batch
+    rng = np.random.default_rng(5 + rank)
+    c0 = rn.RnsPoly.from_channels(uniform(rng, mod, B, n), Bs)
+    c1 = rn.RnsPoly.from_channels(uniform(rng, mod, B, n), Bs)
+    key = rn.RnsGadgetKey.from_channels(uniform(rng, mod, L, n), uniform(rng, mod, L, n), Bs)
+    offsets = [1 << e for e in range(log_n - 1)]  # 1 .. N/4: all power-of-two slot offsets
+    out0, out1 = rn.RnsPoly(Bs, B), rn.RnsPoly(Bs, B)  # reused: the workspace stays allocated
+    lib = rn.load()
+
+    def step():
+        for k in offsets:
+            rn.check(lib.rnt_ct_rotate(out0.handle, out1.handle, c0.handle, c1.handle, k,
+                                       key.a.handle, key.b.handle))
+
+    for _ in range(args.warmup):
+        step()
+    Bs.sync()
+    comm.barrier()
+    Bs.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    Bs.sync()
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = comm.max(t1 - t0)
+    kernels = {}
+    for k in ("ks_decompose", "ks_rows", "col_inv", "automorphism", "col_fwd", "row_fwd"):
+        cnt, ms = Bs.profile_read(k)
+        kernels[k] = {"launches": cnt, "avg_ms": ms / cnt if cnt else None, "total_ms": ms}
+    Bs.profile_enable(False)
+    rots = B * len(offsets) * args.steps * world
+    value = rots / elapsed
+    # forward limb-NTT butterflies per key-switch: L^2 (alpha_i mod q_j) + 2L inverse
+    bfly = (L * L + 2 * L) * (n // 2) * log_n
+    return {
+        "metric": ROT_METRIC,
+        "value": value,
+        "unit": "rotations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded uniform residues and key; one key reused for every offset)",
+        "config": {
+            "workload": f"rotate_ciphertext sweep over {len(offsets)} power-of-two offsets, "
+                        f"N=2^{log_n}, L={L} x 31-bit primes, {B} ciphertexts",
+            "parallelism": f"replicas x{world} (each GPU its own ciphertexts)",
+        },
+        "roofline": {"bound": "valu", "kernel": "ks_rows", "unit": "butterflies/s",
+                     "achieved": value / world * bfly, "peak": None, "frac": None, "traffic": None,
+                     "kernels": kernels},
+        "cpu_baseline": None,
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -343,7 +420,7 @@ def main():
     from rns_ntt.dist import Comm
 
     comm = Comm.from_env()
-    run = run_ctmul if args.workload == "ctmul" else run_polymul
+    run = {"polymul": run_polymul, "ctmul": run_ctmul, "rotate": run_rotate}[args.workload]
     line = run(args, comm, world, rank, local_rank)
     if rank == 0:
         print(json.dumps(line), flush=True)
