@@ -7,6 +7,7 @@ NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/toy-heaan-ckks_amd/csrc; L=$ROOT/toy-heaan-ckks_amd/lib; V=$L/variants
 mkdir -p $V
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC "$@" -c $C/rnt_kernels.hip -o $V/k_$NAME.o
+# KSRC=<file> compiles another version of rnt_kernels.hip (e.g. from git show)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$C "$@" -c ${KSRC:-$C/rnt_kernels.hip} -o $V/k_$NAME.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $V/k_$NAME.o $L/rnt_api.o -o $V/librnsntt_$NAME.so
 echo $V/librnsntt_$NAME.so

@@ -964,9 +964,22 @@ int check_key(const rnt_buf* d, const rnt_buf* key_a, const rnt_buf* key_b) {
 }
 
 // polys per key-switch chunk so that S ([L][L][Bc][N]) stays <= ~1 GiB
+// Key-switch workspace cap: S ([L][L][Bc][N] words) of a chunk.  The key
+// rows are read once per chunk from HBM (the batch hits them in cache, see
+// row_pos_pfast), so bigger chunks cut key traffic per ciphertext; 4 GiB is
+// a small slice of the 288 GB.
+static size_t ks_ws_cap() {
+  static const size_t cap = [] {
+    const char* e = getenv("RNT_KS_WS_MB");
+    const long mb = e ? atol(e) : 4096L;
+    return (size_t)(mb > 0 ? mb : 4096L) << 20;
+  }();
+  return cap;
+}
+
 size_t ks_chunk(const rnt::Tables* t, size_t L, size_t B) {
   const size_t per = L * L * t->n * (t->wide ? 8 : 4);
-  size_t c = (size_t)1 << 30;
+  size_t c = ks_ws_cap();
   c = per ? c / per : B;
   if (c < 1) c = 1;
   return std::min(c, B);
@@ -1052,7 +1065,7 @@ extern "C" int rnt_keyswitch_ext(rnt_buf* acc0, rnt_buf* acc1, const void* src, 
   rnt::Launch k = launch_for(acc0);
   const size_t Lt = k.L, Ls = src_limbs, n = k.t->n, wb = word_bytes(k.t), B = acc0->n_polys;
   // polys per chunk: S is [Lt][Ls][Bc][N]
-  size_t bc = std::max<size_t>(1, ((size_t)1 << 30) / std::max<size_t>(1, Lt * Ls * n * wb));
+  size_t bc = std::max<size_t>(1, ks_ws_cap() / std::max<size_t>(1, Lt * Ls * n * wb));
   bc = std::min(bc, B);
   if (int rc = ensure_ws(acc0, (Lt * Ls + 2 * Lt) * bc * n * wb)) return rc;
   const uint64_t src_ls = (uint64_t)B * n, full_ls = limb_stride(acc0);

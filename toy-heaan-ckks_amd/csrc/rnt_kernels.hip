@@ -584,6 +584,27 @@ __device__ __forceinline__ RowPos row_pos(uint32_t log_n, uint32_t B, uint64_t r
   return rp;
 }
 
+// Row coordinates with the poly index fastest: row = ((l * R + r) * B + p).
+// Consecutive rows of a workgroup then share (limb, row r), so whatever they
+// read per (limb, r) -- gadget-key rows, twiddles -- is fetched from HBM once
+// and hit in cache by the rest of the batch.
+template <class G>
+__device__ __forceinline__ RowPos row_pos_pfast(uint32_t log_n, uint32_t B, uint64_t rows_total) {
+  RowPos rp;
+  rp.xp.slot = G::slot_of(threadIdx.x);
+  rp.xp.tau = G::tau_of(threadIdx.x);
+  uint64_t row = (uint64_t)blockIdx.x * G::RPW + rp.xp.slot;
+  rp.active = row < rows_total;
+  if (!rp.active) row = 0;
+  const uint32_t log_r = log_n - G::LOGC;
+  const uint64_t lr = row / B;
+  rp.p = (uint32_t)(row - lr * B);
+  rp.r = (uint32_t)(lr & ((1u << log_r) - 1u));
+  rp.l = (uint32_t)(lr >> log_r);
+  rp.xp.heap = (1u << log_n) + rp.r * (uint32_t)G::C;  // (R + r) * C
+  return rp;
+}
+
 // ---------------------------------------------------------------------------
 // tiled column passes (log2 R >= 5): a workgroup owns TC = 32 adjacent
 // columns of one (limb, poly) and runs the R-point network over the row
@@ -709,8 +730,10 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
   for (int i = 0; i < E; ++i) dst.st(x[0][i], a0.v, i * a0.s);
 }
 
-// Tiled key-switch decomposition: grid x = p * (C / TC) + column tile,
-// y = source limb i, z = target limb j.
+// Tiled key-switch decomposition: grid x = target limb j (fastest, so the
+// L workgroups that reduce one source tile of d mod every q_j run back to
+// back and read it from L2), y = p * (C / TC) + column tile, z = source
+// limb i.
 template <class W, int LOG_R, int LOG_TC>
 __global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32_t log_n,
@@ -721,10 +744,10 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
   W* lds = (W*)smem_raw;
   const uint32_t N = 1u << log_n;
   const uint32_t tpp_log = log_c - G::LOGTC;
-  const uint32_t p = blockIdx.x >> tpp_log;
-  const uint32_t ct = blockIdx.x & ((1u << tpp_log) - 1);
-  const uint32_t i = blockIdx.y;
-  const uint32_t j = blockIdx.z;
+  const uint32_t p = blockIdx.y >> tpp_log;
+  const uint32_t ct = blockIdx.y & ((1u << tpp_log) - 1);
+  const uint32_t i = blockIdx.z;
+  const uint32_t j = blockIdx.x;
   ColPos cp;
   cp.xp.slot = G::slot_of(threadIdx.x);
   cp.xp.tau = G::tau_of(threadIdx.x);
@@ -803,8 +826,11 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
 // Key-switch rows.  Row = (target limb j, poly p, row r).  For every source
 // limb i: forward rows of S[j][i][p], multiply-accumulate with the
 // NTT-resident keys; then the inverse rows of both accumulators.
+#ifndef RNT_KS_MIN_WAVES
+#define RNT_KS_MIN_WAVES 4
+#endif
 template <class W, int LOG_C>
-__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS)
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? RNT_KS_MIN_WAVES : 1)
 k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
           const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
           const W* __restrict__ init0, const W* __restrict__ init1, uint64_t init_ls,
@@ -814,7 +840,7 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
-  const RowPos rp = row_pos<G>(log_n, B, rows_total);  // rp.l == target limb j
+  const RowPos rp = row_pos_pfast<G>(log_n, B, rows_total);  // rp.l == target limb j
   const uint64_t N = 1ull << log_n;
   const uint32_t j = rp.l;
   const uint64_t rowoff = (uint64_t)rp.r * G::C;
@@ -832,30 +858,44 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     acc[0][e] = init0 ? init0[ibase + pos] : (W)0;
     acc[1][e] = init1 ? init1[ibase + pos] : (W)0;
   }
+  // one source limb per iteration; not unrolled or pipelined by the
+  // compiler (that doubles the live registers and halves occupancy)
+#pragma unroll 1
   for (uint32_t i = 0; i < L; ++i) {
     const uint64_t sbase = (((uint64_t)j * L + i) * B + rp.p) * N + rowoff;
     W x[1][E];
 #pragma unroll
     for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
     xf_fwd<G, W, 1>(x, rp.xp, lds, tw, mod_of(lc));
+    // keep the key loads below the transform: hoisted above it they stay
+    // live across all of it (the register peak that capped occupancy)
+    __builtin_amdgcn_sched_barrier(0);
     // key poly i, limb j (key buffers hold L polys: limb stride key_ls)
     const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + rowoff;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-      const uint32_t pos = bl + ((uint32_t)e << G::BBL);
-      const W kb = key_b[kbase + pos];
-      const W ka = key_a[kbase + pos];
+      const W kb = key_b[kbase + bl + ((uint32_t)e << G::BBL)];
       acc[0][e] = add_mod<W>(acc[0][e], mont_mul<W>(x[0][e], kb, lc.q, lc.qinv), lc.q);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const W ka = key_a[kbase + bl + ((uint32_t)e << G::BBL)];
       acc[1][e] = add_mod<W>(acc[1][e], mont_mul<W>(x[0][e], ka, lc.q, lc.qinv), lc.q);
     }
   }
-  xf_inv<G, W, 2>(acc, rp.xp, lds, itw, mod_of(lc));
-  if (rp.active) {
+  // the two accumulators' inverse rows one after the other (half the live
+  // registers of a two-operand pass)
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const uint32_t pos = b0 + ((uint32_t)e << G::BB0);
-      u0[obase + pos] = acc[0][e];
-      u1[obase + pos] = acc[1][e];
+  for (int o = 0; o < 2; ++o) {
+    W v[1][E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[0][e] = acc[o][e];
+    xf_inv<G, W, 1>(v, rp.xp, lds, itw, mod_of(lc));
+    W* uo = o == 0 ? u0 : u1;
+    if (rp.active) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) uo[obase + b0 + ((uint32_t)e << G::BB0)] = v[0][e];
     }
   }
 }
@@ -1385,8 +1425,9 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
   const TabPtrs<W> tp = tab_ptrs<W>(k.t);
   const uint32_t Ls = (uint32_t)k.src_limbs();  // source limbs i; target limbs j = k.L
   if (g.log_r >= 5) {
-    const dim3 grid = col_grid(k, g, Ls, (uint32_t)k.L);
-    if (grid.x == 0) return hipErrorInvalidConfiguration;
+    const dim3 g0 = col_grid(k, g, Ls, (uint32_t)k.L);
+    if (g0.x == 0 || g0.x > 65535u) return hipErrorInvalidConfiguration;
+    const dim3 grid((uint32_t)k.L, g0.x, Ls);
     hipError_t e = hipSuccess;
 #define RNT_L2(R, TC)                                                                         \
   e = allow_lds(k_colt_decompose<W, R, TC>, col_lds<W, R, TC>());                             \
