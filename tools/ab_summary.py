@@ -7,6 +7,8 @@ import sys
 runs = [json.loads(open(f).read().strip().splitlines()[-1]) for f in sys.argv[1:]]
 print("value  median %.1f  (%s)" % (statistics.median(r["value"] for r in runs),
                                    ", ".join("%.1f" % r["value"] for r in runs)))
-for k in runs[0]["roofline"]["kernels"]:
+for k in runs[0]["roofline"].get("kernels", {}):
     v = [r["roofline"]["kernels"][k]["avg_ms"] for r in runs]
+    if any(x is None for x in v):
+        continue
     print("%-8s median %.4f ms  (%s)" % (k, statistics.median(v), ", ".join("%.4f" % x for x in v)))

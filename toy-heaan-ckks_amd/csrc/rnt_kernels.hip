@@ -79,6 +79,24 @@ struct BufView {
       return __builtin_bit_cast(W, __builtin_amdgcn_raw_buffer_load_b64(r, v * 8u, s * 8u, 0));
     }
   }
+  // four consecutive words (the compiler does not merge the raw buffer
+  // builtins into wide loads by itself)
+  __device__ __forceinline__ void ld4(W (&o)[4], uint32_t v, uint32_t s) const {
+    if constexpr (sizeof(W) == 4) {
+      const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, v * 4u, s * 4u, 0);
+      o[0] = q[0];
+      o[1] = q[1];
+      o[2] = q[2];
+      o[3] = q[3];
+    } else {
+      const auto a = __builtin_amdgcn_raw_buffer_load_b128(r, v * 8u, s * 8u, 0);
+      const auto b = __builtin_amdgcn_raw_buffer_load_b128(r, v * 8u + 16u, s * 8u, 0);
+      o[0] = (uint64_t)a[0] | ((uint64_t)a[1] << 32);
+      o[1] = (uint64_t)a[2] | ((uint64_t)a[3] << 32);
+      o[2] = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
+      o[3] = (uint64_t)b[2] | ((uint64_t)b[3] << 32);
+    }
+  }
   __device__ __forceinline__ void st(W x, uint32_t v, uint32_t s) const {
     if constexpr (sizeof(W) == 4) {
       __builtin_amdgcn_raw_buffer_store_b32(x, r, v * 4u, s * 4u, 0);
@@ -92,9 +110,13 @@ struct BufView {
 // Twiddle sources for the pass templates: a plain pointer (row kernels,
 // whose limb may vary across a workgroup) or a buffer view of one limb's
 // table (column kernels: one limb per workgroup).
+// tw_get(src, nb, m): twiddle nb + m where nb is the stage's (per-lane or
+// uniform) heap base and m a compile-time index -- kept apart so the buffer
+// form puts m into the instruction (inline-constant soffset) and holds ONE
+// offset register per stage instead of one per twiddle.
 template <class W>
-__device__ __forceinline__ Tw<W> tw_get(const Tw<W>* p, uint32_t i) {
-  return p[i];
+__device__ __forceinline__ Tw<W> tw_get(const Tw<W>* p, uint32_t nb, uint32_t m) {
+  return p[nb + m];
 }
 template <class W>
 struct TwBuf {
@@ -103,14 +125,15 @@ struct TwBuf {
       : r(__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(n * sizeof(Tw<W>)), 0x00020000)) {}
 };
 template <class W>
-__device__ __forceinline__ Tw<W> tw_get(const TwBuf<W>& b, uint32_t i) {
+__device__ __forceinline__ Tw<W> tw_get(const TwBuf<W>& b, uint32_t nb, uint32_t m) {
   Tw<W> t;
   if constexpr (sizeof(W) == 4) {
-    const uint64_t v = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(b.r, i * 8u, 0, 0));
+    const uint64_t v =
+        __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(b.r, nb * 8u, m * 8u, 0));
     t.w = (uint32_t)v;
     t.p = (uint32_t)(v >> 32);
   } else {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(b.r, i * 16u, 0, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(b.r, nb * 16u, m * 16u, 0);
     t.w = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
     t.p = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
   }
@@ -375,8 +398,8 @@ struct TwScalar {
   const RNT_CONST_AS Tw<W>* p;
 };
 template <class W>
-__device__ __forceinline__ Tw<W> tw_get(const TwScalar<W>& t, uint32_t i) {
-  return t.p[i];
+__device__ __forceinline__ Tw<W> tw_get(const TwScalar<W>& t, uint32_t nb, uint32_t m) {
+  return t.p[nb + m];
 }
 template <class W, bool UNIFORM>
 __device__ __forceinline__ auto col_twiddles(const Tw<W>* base, uint32_t n) {
@@ -409,7 +432,7 @@ __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0,
     Tw<W> t[H];
 #pragma unroll
     for (int m = 0; m < H; ++m)
-      if (m < cnt) t[m] = tw_get<W>(tw, nb + m);
+      if (m < cnt) t[m] = tw_get<W>(tw, nb, (uint32_t)m);
     const int d = 1 << sl;
 #pragma unroll
     for (int i = 0; i < E; ++i) {
@@ -457,7 +480,7 @@ __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0,
     Tw<W> t[H];
 #pragma unroll
     for (int m = 0; m < H; ++m)
-      if (m < cnt) t[m] = tw_get<W>(itw, nb + m);
+      if (m < cnt) t[m] = tw_get<W>(itw, nb, (uint32_t)m);
 #pragma unroll
     for (int i = 0; i < E; ++i) {
       if (i & d) continue;
@@ -900,11 +923,6 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   }
 }
 
-// Tensor-product rows (engine.rs:480-493): inputs are the column-pass
-// outputs of c0, c1, c0', c1'.  d0 = c0 c0', d1 = c0 c1' + c1 c0',
-// d2 = c1 c1' (pointwise, Montgomery-scaled by 2^-w).  d0hat / d1hat are
-// written as NTT-domain rows (last-pass distribution) for the key-switch
-// accumulators; d2 goes through the inverse rows into d2row.
 template <class W, int LOG_C>
 __global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS)
 k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2row,
