@@ -127,6 +127,17 @@ int rnt_upload_coeffs(rnt_buf* buf, const int64_t* coeffs, size_t n_polys);
  * in the buffer's current domain (natural order when NTT). */
 int rnt_download(const rnt_buf* buf, uint64_t* host, size_t n_polys);
 int rnt_copy(rnt_buf* dst, const rnt_buf* src); /* Clone */
+/* PolyRing::to_coeffs (poly.rs:404-427) for a batch: per coefficient the CRT
+ * value centred in (-Q/2, Q/2] (reconstruct_centered_coeff, basis.rs:158-180)
+ * as int64_t[n_polys][N] -- the value's low 64 bits in two's complement,
+ * exactly the reference's result wherever it is defined (Q < 2^128).  An
+ * NTT-domain buffer is converted on a temporary copy. */
+int rnt_to_coeffs(const rnt_buf* buf, int64_t* host, size_t n_polys);
+/* The same centred CRT value without truncation: `words` 64-bit
+ * little-endian two's-complement words per coefficient,
+ * uint64_t[n_polys][N][words] (the reference's u128 path
+ * cannot represent Q >= 2^128).  1 <= words <= 64. */
+int rnt_crt_centered(const rnt_buf* buf, uint64_t* host, size_t n_polys, size_t words);
 /* Device-memory interop for multi-GPU pipelines (collectives run by the
  * caller, e.g. RCCL through torch.distributed):
  * rnt_buf_wrap makes a NON-owning buffer over caller device memory laid out

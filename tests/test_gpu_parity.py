@@ -424,3 +424,68 @@ def test_config5_full_limbs_ntt_roundtrip(gpu, vectors):
     assert np.array_equal(th[1][:2], orc.to_ntt(orc.Basis(mod[:2], n), a_h[1][:2]))
     t.to_coeff_domain()
     assert np.array_equal(t.channels(), a_h)
+
+
+# ---------------------------------------------------------------------------
+# decode-side CRT (basis.rs:158-180, poly.rs:404-427)
+# ---------------------------------------------------------------------------
+
+
+def _centered_crt(mods, residues):
+    """Exact centred CRT in Python ints (the reference's math without its
+    u128 limit)."""
+    Q = 1
+    for q in mods:
+        Q *= q
+    x = 0
+    for r, q in zip(residues, mods):
+        Qi = Q // q
+        x += (int(r) * pow(Qi % q, -1, q) % q) * Qi
+    x %= Q
+    return x - Q if x > Q // 2 else x
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log_n,bits,L", [(3, 20, 2), (4, 31, 3), (6, 40, 3), (8, 61, 2), (10, 31, 4)])
+def test_to_coeffs_matches_oracle(gpu, log_n, bits, L):
+    """Q < 2^128: bit-exact against the oracle's restatement of to_coeffs."""
+    rn = gpu
+    n = 1 << log_n
+    mods = rn.generate_primes(bits, L, n)
+    Bo = orc.Basis(mods, n)
+    rng = np.random.default_rng(log_n * 7 + L)
+    a = orc.uniform_poly(mods, n, rng, batch=3)
+    p = rn.RnsPoly.from_channels(a, rn.RnsBasis(mods, n))
+    got = p.to_coeffs()
+    for i in range(3):
+        assert np.array_equal(got[i], orc.to_coeffs(Bo, a[i])), i
+    # NTT-domain input decodes through a temporary copy, unchanged
+    p.to_ntt_domain()
+    assert np.array_equal(p.to_coeffs(), got)
+    assert p.is_ntt_domain()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log_n,L", [(16, 16), (17, 32)])
+def test_crt_centered_large_q(gpu, log_n, L):
+    """Q >= 2^128 (configs 4, 5): exact centred values against Python ints
+    on sampled coefficients, and small signed coefficients round-trip."""
+    rn = gpu
+    n = 1 << log_n
+    mods = rn.generate_primes(31, L, n)
+    B = rn.RnsBasis(mods, n)
+    rng = np.random.default_rng(L)
+    a = orc.uniform_poly(mods, n, rng, batch=1)
+    p = rn.RnsPoly.from_channels(a, B)
+    exact = p.to_coeffs_exact()
+    for i in rng.integers(0, n, size=64):
+        assert exact[i] == _centered_crt(mods, a[0, :, i]), i
+    # i64 path = the low 64 bits of the same values
+    low = p.to_coeffs()
+    for i in rng.integers(0, n, size=64):
+        v = exact[i] & ((1 << 64) - 1)
+        assert int(low[i]) == (v - (1 << 64) if v >> 63 else v)
+    # from_coeffs -> to_coeffs is the identity on i64 inputs
+    c = rng.integers(-(1 << 62), 1 << 62, size=n, dtype=np.int64)
+    c[:4] = [0, 1, -1, (1 << 62) - 1]
+    assert np.array_equal(rn.RnsPoly.from_coeffs(c, B).to_coeffs(), c)

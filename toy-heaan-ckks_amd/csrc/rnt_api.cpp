@@ -48,7 +48,7 @@ inline size_t word_bytes(const rnt::Tables* t) { return t->wide ? 8 : 4; }
 
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
-    "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export"};
+    "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -184,6 +184,7 @@ rnt::Tables::~Tables() {
   }
   if (fork_ev) (void)hipEventDestroy(fork_ev);
   for (auto& e : resc_ext) (void)hipFree(e.second);
+  for (auto& e : crt_cache) (void)hipFree(e.second.dev);
   (void)hipFree(tw_fwd);
   (void)hipFree(tw_inv);
   (void)hipFree(lconst);
@@ -873,6 +874,146 @@ extern "C" int rnt_rescale_ext(rnt_buf* out, const rnt_buf* in, const void* last
          "rescale_ext");
   out->in_ntt = 0;
   return RNT_OK;
+}
+
+// ---- decode-side CRT (basis.rs:158-180, poly.rs:404-427) ----------------
+
+namespace {
+
+// Little-endian 32-bit-word big integers for the host-side constants.
+using Big = std::vector<uint32_t>;
+void big_mul_small(Big& a, uint64_t m) {
+  // a *= m (m < 2^64), growing a
+  const uint32_t mlo = (uint32_t)m, mhi = (uint32_t)(m >> 32);
+  Big r(a.size() + 2, 0);
+  for (int half = 0; half < 2; ++half) {
+    const uint64_t f = half ? mhi : mlo;
+    if (!f) continue;
+    uint64_t carry = 0;
+    for (size_t w = 0; w < a.size(); ++w) {
+      const uint64_t t = (uint64_t)a[w] * f + r[w + half] + carry;
+      r[w + half] = (uint32_t)t;
+      carry = t >> 32;
+    }
+    for (size_t w = a.size() + half; carry && w < r.size(); ++w) {
+      const uint64_t t = (uint64_t)r[w] + carry;
+      r[w] = (uint32_t)t;
+      carry = t >> 32;
+    }
+  }
+  while (r.size() > 1 && r.back() == 0) r.pop_back();
+  a.swap(r);
+}
+
+}  // namespace
+
+// Constants of the centred CRT for the first L limbs of a basis, cached per
+// (tables, L): device block {qi_words[L][MW], q[MW], qh[MW], inv[L],
+// inv_p[L], rq[L]} and the CrtConsts pointing into it.
+static int crt_tables(const rnt_ctx* ctx, const void** consts, uint32_t* mw_out) {
+  rnt::Tables* t = ctx->t.get();
+  const size_t L = ctx->L;
+  std::lock_guard<std::mutex> g(t->resc_mu);
+  for (auto& e : t->crt_cache)
+    if (e.first == L) {
+      *consts = &e.second.cc;
+      *mw_out = e.second.mw;
+      return RNT_OK;
+    }
+  Big Q{1};
+  for (size_t l = 0; l < L; ++l) big_mul_small(Q, t->moduli[l]);
+  uint32_t mw = 4;
+  while (mw < Q.size()) mw *= 2;
+  if (mw > 128) return fail(RNT_ERR_BAD_ARGUMENT, "CRT: Q has %zu 32-bit words (max 128)", Q.size());
+  std::vector<uint32_t> qi(L * mw, 0), qw(mw, 0), qh(mw, 0);
+  std::vector<uint64_t> inv(L), invp(L);
+  std::vector<double> rq(L);
+  const unsigned wbits = t->wide ? 64 : 32;
+  for (size_t l = 0; l < L; ++l) {
+    Big Ql{1};
+    uint64_t ql_mod = 1;  // (Q/q_l) mod q_l
+    for (size_t m = 0; m < L; ++m) {
+      if (m == l) continue;
+      big_mul_small(Ql, t->moduli[m]);
+      ql_mod = rnt::host::mulmod(ql_mod, t->moduli[m] % t->moduli[l], t->moduli[l]);
+    }
+    for (size_t w = 0; w < Ql.size() && w < mw; ++w) qi[l * mw + w] = Ql[w];
+    inv[l] = rnt::host::invmod(ql_mod, t->moduli[l]);
+    if (inv[l] == 0 && L > 1)
+      return fail(RNT_ERR_BAD_ARGUMENT, "CRT: moduli are not pairwise coprime");
+    if (L == 1) inv[l] = 1;
+    invp[l] = rnt::host::shoup_companion(inv[l], t->moduli[l], wbits);
+    rq[l] = 1.0 / (double)t->moduli[l];
+  }
+  for (size_t w = 0; w < Q.size(); ++w) qw[w] = Q[w];
+  for (size_t w = 0; w < mw; ++w) qh[w] = (qw[w] >> 1) | (w + 1 < mw ? qw[w + 1] << 31 : 0);
+  const size_t bytes = (L * mw + 2 * mw) * 4 + L * 8 * 2 + L * 8;
+  void* d = nullptr;
+  HIP_TRY(hipMalloc(&d, bytes), "hipMalloc(CRT constants)");
+  std::vector<unsigned char> h(bytes);
+  size_t off = 0;
+  auto put = [&](const void* src, size_t n) {
+    memcpy(h.data() + off, src, n);
+    off += n;
+  };
+  rnt::CrtDev cd;
+  cd.dev = d;
+  cd.mw = mw;
+  cd.cc.qi_words = (const uint32_t*)((char*)d + off);
+  put(qi.data(), qi.size() * 4);
+  cd.cc.q_words = (const uint32_t*)((char*)d + off);
+  put(qw.data(), mw * 4);
+  cd.cc.qh_words = (const uint32_t*)((char*)d + off);
+  put(qh.data(), mw * 4);
+  cd.cc.inv = (const uint64_t*)((char*)d + off);
+  put(inv.data(), L * 8);
+  cd.cc.inv_p = (const uint64_t*)((char*)d + off);
+  put(invp.data(), L * 8);
+  cd.cc.rq = (const double*)((char*)d + off);
+  put(rq.data(), L * 8);
+  HIP_TRY(hipMemcpy(d, h.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy(CRT constants)");
+  t->crt_cache.push_back({L, cd});
+  *consts = &t->crt_cache.back().second.cc;
+  *mw_out = mw;
+  return RNT_OK;
+}
+
+static int crt_download(const rnt_buf* cb, uint64_t* host, size_t n_polys, size_t out_words,
+                        const char* name) {
+  rnt_buf* b = const_cast<rnt_buf*>(cb);  // workspace / staging only
+  if (int rc = check_buf(b, name)) return rc;
+  if (!host) return fail(RNT_ERR_BAD_ARGUMENT, "%s: null host pointer", name);
+  if (n_polys != b->n_polys)
+    return fail(RNT_ERR_BAD_ARGUMENT, "%s: buffer holds %zu polys, got %zu", name, b->n_polys, n_polys);
+  if (out_words == 0 || out_words > 64) return fail(RNT_ERR_BAD_ARGUMENT, "%s: 1..64 words", name);
+  if (int rc = set_device(b->ctx)) return rc;
+  const void* consts = nullptr;
+  uint32_t mw = 0;
+  if (int rc = crt_tables(b->ctx, &consts, &mw)) return rc;
+  rnt::Launch k = launch_for(b);
+  const void* src = b->data;
+  if (b->in_ntt) {  // poly.rs:408-417: a coefficient-domain clone
+    if (int rc = ensure_ws(b, poly_words(b) * word_bytes(k.t))) return rc;
+    if (int rc = to_coeff_into(b, b->ws)) return rc;
+    src = b->ws;
+  }
+  const size_t coeffs = b->n_polys * k.t->n;
+  if (int rc = ensure_stage(b, coeffs * out_words * 8)) return rc;
+  LAUNCH(k.t, rnt::K_CRT, rnt::launch_crt(k, (uint64_t*)b->stage, src, consts, mw, (uint32_t)out_words),
+         "crt");
+  HIP_TRY(hipMemcpyAsync(host, b->stage, coeffs * out_words * 8, hipMemcpyDeviceToHost, k.s),
+          "hipMemcpy D2H");
+  HIP_TRY(hipStreamSynchronize(k.s), "hipStreamSynchronize");
+  trim_stage(b);
+  return RNT_OK;
+}
+
+extern "C" int rnt_to_coeffs(const rnt_buf* buf, int64_t* host, size_t n_polys) {
+  return crt_download(buf, (uint64_t*)host, n_polys, 1, "rnt_to_coeffs");
+}
+
+extern "C" int rnt_crt_centered(const rnt_buf* buf, uint64_t* host, size_t n_polys, size_t words) {
+  return crt_download(buf, host, n_polys, words, "rnt_crt_centered");
 }
 
 extern "C" int rnt_mod_drop_last(rnt_buf* out, const rnt_buf* in) {

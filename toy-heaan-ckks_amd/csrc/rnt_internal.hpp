@@ -59,6 +59,21 @@ struct alignas(2 * sizeof(W)) Tw {
 
 // Shared, immutable device tables of a root basis.  drop_last views hold a
 // shared_ptr to the same tables (no copy, unlike basis.rs:130-133).
+// Device pointers of the centred-CRT constants (rnt_kernels.hip k_crt).
+struct CrtConsts {
+  const uint32_t* qi_words;  // [L][MW]  Q / q_l
+  const uint32_t* q_words;   // [MW]     Q
+  const uint32_t* qh_words;  // [MW]     floor(Q / 2)
+  const uint64_t* inv;       // [L]      (Q/q_l)^-1 mod q_l
+  const uint64_t* inv_p;     // [L]      its Shoup companion (device word width)
+  const double* rq;          // [L]      1 / q_l
+};
+struct CrtDev {
+  void* dev = nullptr;
+  uint32_t mw = 0;
+  CrtConsts cc{};
+};
+
 struct Tables {
   int device = 0;
   int wide = 0;            // 0: W = u32, 1: W = u64
@@ -84,6 +99,8 @@ struct Tables {
   // {inv[L], invp[L]} with inv[l] = (q_last mod q_l)^-1 mod q_l.
   std::mutex resc_mu;
   std::vector<std::pair<uint64_t, void*>> resc_ext;
+  // centred-CRT constants per limb count (rnt_to_coeffs / rnt_crt_centered)
+  std::vector<std::pair<size_t, struct CrtDev>> crt_cache;
   struct Prof* prof = nullptr;  // per-kernel event timing (rnt_profile_*)
   ~Tables();
 };
@@ -91,7 +108,7 @@ struct Tables {
 // Kernel ids for rnt_profile_read.
 enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
-  K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_COUNT
+  K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT, K_COUNT
 };
 
 struct Prof {
@@ -170,6 +187,11 @@ hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a,
                               const void* b);
 // k.L = limbs of the input; output has k.L - 1 (same poly count / stride B*N).
 hipError_t launch_rescale(const Launch& k, void* out, const void* in);
+// Centred CRT of every coefficient (coefficient-domain `in`, k.L limbs) into
+// `out_words` 64-bit two's-complement words each ([B][N][out_words]);
+// `consts` points to a host CrtConsts of device arrays, mw = 32-bit words of Q.
+hipError_t launch_crt(const Launch& k, uint64_t* out, const void* in, const void* consts,
+                      uint32_t mw, uint32_t out_words);
 // out limb l = (in_l - (last mod q_l)) * inv[l] (Shoup pair inv/invp, device
 // arrays of k.L words); `last` is a [B][N] plane of residues mod q_last.
 hipError_t launch_rescale_ext(const Launch& k, void* out, const void* in, const void* last,

@@ -1553,8 +1553,157 @@ hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const voi
 hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a, const void* b) {
   RNT_WIDE(elementwise_t<uint32_t>(k, op, out, a, b), elementwise_t<uint64_t>(k, op, out, a, b));
 }
+// ---------------------------------------------------------------------------
+// decode-side CRT (basis.rs:158-180, poly.rs:404-427)
+// ---------------------------------------------------------------------------
+
+// Per coefficient, with residues r_l (coefficient domain):
+//   s_l = r_l * (Q/q_l)^-1 mod q_l,   x = sum_l s_l * (Q/q_l) - k * Q,
+//   k = floor(sum_l s_l / q_l)  (double precision, then a +-Q correction),
+// centred into (-Q/2, Q/2] and written as `out_words` little-endian 64-bit
+// two's-complement words.  Multi-word values are MW 32-bit words; the
+// constants (Q/q_l words, Q, floor(Q/2)) are wave-uniform scalar loads.
+// (CrtConsts: rnt_internal.hpp)
+
+template <int MW>
+__device__ __forceinline__ bool mw_ge(const uint32_t (&a)[MW + 1], const RNT_CONST_AS uint32_t* b) {
+  if (a[MW] != 0) return true;
+#pragma unroll
+  for (int w = MW - 1; w >= 0; --w) {
+    if (a[w] != b[w]) return a[w] > b[w];
+  }
+  return true;
+}
+template <int MW>
+__device__ __forceinline__ void mw_sub(uint32_t (&a)[MW + 1], const RNT_CONST_AS uint32_t* b) {
+  uint64_t borrow = 0;
+#pragma unroll
+  for (int w = 0; w < MW; ++w) {
+    const uint64_t d = (uint64_t)a[w] - b[w] - borrow;
+    a[w] = (uint32_t)d;
+    borrow = (d >> 32) & 1;
+  }
+  a[MW] -= (uint32_t)borrow;
+}
+template <int MW>
+__device__ __forceinline__ void mw_add(uint32_t (&a)[MW + 1], const RNT_CONST_AS uint32_t* b) {
+  uint64_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < MW; ++w) {
+    const uint64_t t = (uint64_t)a[w] + b[w] + carry;
+    a[w] = (uint32_t)t;
+    carry = t >> 32;
+  }
+  a[MW] += (uint32_t)carry;
+}
+
+template <class W, int MW>
+__global__ void __launch_bounds__(256)
+k_crt(uint64_t* __restrict__ out, const W* __restrict__ in, CrtConsts cc, TabPtrs<W> tp,
+      uint32_t L, uint64_t ls, uint32_t out_words, uint64_t total) {
+  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= total) return;
+  const RNT_CONST_AS uint32_t* qi = (const RNT_CONST_AS uint32_t*)cc.qi_words;
+  const RNT_CONST_AS uint32_t* qw = (const RNT_CONST_AS uint32_t*)cc.q_words;
+  const RNT_CONST_AS uint32_t* qh = (const RNT_CONST_AS uint32_t*)cc.qh_words;
+  uint32_t acc[MW + 1];
+#pragma unroll
+  for (int w = 0; w <= MW; ++w) acc[w] = 0;
+  double f = 0.0;
+  for (uint32_t l = 0; l < L; ++l) {
+    const LimbConst<W> lc = tp.lc[l];
+    const W s = shoup_mul<W>(in[(uint64_t)l * ls + gid], (W)cc.inv[l], (W)cc.inv_p[l], lc.q);
+    f += (double)s * cc.rq[l];
+    // acc += s * (Q/q_l), s split into 32-bit halves
+    const RNT_CONST_AS uint32_t* row = qi + (uint64_t)l * MW;
+#pragma unroll
+    for (int half = 0; half < (sizeof(W) == 8 ? 2 : 1); ++half) {
+      const uint32_t sh = (uint32_t)((uint64_t)s >> (32 * half));
+      uint64_t carry = 0;
+#pragma unroll
+      for (int w = 0; w + half < MW; ++w) {
+        const uint64_t t = (uint64_t)sh * row[w] + acc[w + half] + carry;
+        acc[w + half] = (uint32_t)t;
+        carry = t >> 32;
+      }
+#pragma unroll
+      for (int w = MW - half; w <= MW; ++w) {  // propagate into the top word(s)
+        const uint64_t t = (uint64_t)acc[w] + carry;
+        acc[w] = (uint32_t)t;
+        carry = t >> 32;
+      }
+    }
+  }
+  // subtract k*Q, k = floor(f) < L; then correct by at most one Q either way
+  const uint32_t k = (uint32_t)f;
+  {
+    uint64_t borrow = 0;
+    uint64_t carry = 0;
+#pragma unroll
+    for (int w = 0; w < MW; ++w) {
+      const uint64_t kq = (uint64_t)k * qw[w] + carry;
+      carry = kq >> 32;
+      const uint64_t d = (uint64_t)acc[w] - (uint32_t)kq - borrow;
+      acc[w] = (uint32_t)d;
+      borrow = (d >> 32) & 1;
+    }
+    acc[MW] = acc[MW] - (uint32_t)carry - (uint32_t)borrow;
+  }
+  if ((int32_t)acc[MW] < 0) mw_add<MW>(acc, qw);
+  if (mw_ge<MW>(acc, qw)) mw_sub<MW>(acc, qw);
+  // centre: x > floor(Q/2)  <=>  x > Q/2 (Q odd)  ->  x - Q
+  uint32_t t2[MW + 1];
+#pragma unroll
+  for (int w = 0; w <= MW; ++w) t2[w] = acc[w];
+  bool gt = false;
+  {
+    bool decided = false;
+#pragma unroll
+    for (int w = MW - 1; w >= 0; --w) {
+      if (!decided && t2[w] != qh[w]) {
+        gt = t2[w] > qh[w];
+        decided = true;
+      }
+    }
+  }
+  if (gt) mw_sub<MW>(acc, qw);  // negative: two's complement with sign in acc[MW]
+  const uint32_t sign = (int32_t)acc[MW] < 0 ? 0xffffffffu : 0u;
+  uint64_t* o = out + gid * out_words;
+  for (uint32_t w = 0; w < out_words; ++w) {
+    const uint32_t lo = 2 * w < (uint32_t)MW ? acc[2 * w] : sign;
+    const uint32_t hi = 2 * w + 1 < (uint32_t)MW ? acc[2 * w + 1] : sign;
+    o[w] = (uint64_t)lo | ((uint64_t)hi << 32);
+  }
+}
+
+template <class W>
+static hipError_t crt_t(const Launch& k, uint64_t* out, const void* in, const CrtConsts& cc,
+                        uint32_t mw, uint32_t out_words) {
+  const uint64_t total = (uint64_t)k.B << k.t->log_n;
+  if (total == 0) return hipSuccess;
+  const uint64_t ls = total;
+#define RNT_L(MW)                                                                                \
+  hipLaunchKernelGGL((k_crt<W, MW>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, out,       \
+                     (const W*)in, cc, tab_ptrs<W>(k.t), (uint32_t)k.L, ls, out_words, total); \
+  return hipGetLastError()
+  if (mw <= 4) { RNT_L(4); }
+  if (mw <= 8) { RNT_L(8); }
+  if (mw <= 16) { RNT_L(16); }
+  if (mw <= 32) { RNT_L(32); }
+  if (mw <= 64) { RNT_L(64); }
+  if (mw <= 128) { RNT_L(128); }
+#undef RNT_L
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_rescale(const Launch& k, void* out, const void* in) {
   RNT_WIDE(rescale_t<uint32_t>(k, out, in), rescale_t<uint64_t>(k, out, in));
+}
+hipError_t launch_crt(const Launch& k, uint64_t* out, const void* in, const void* consts,
+                      uint32_t mw, uint32_t out_words) {
+  const CrtConsts cc = *(const CrtConsts*)consts;
+  RNT_WIDE(crt_t<uint32_t>(k, out, in, cc, mw, out_words),
+           crt_t<uint64_t>(k, out, in, cc, mw, out_words));
 }
 hipError_t launch_rescale_ext(const Launch& k, void* out, const void* in, const void* last,
                               const void* inv, const void* invp) {

@@ -355,19 +355,31 @@ class RnsPoly:
 
     # -- PolyRing::to_coeffs (poly.rs:404-427) ------------------------------
     def to_coeffs(self) -> np.ndarray:
-        """Centered CRT of each coefficient (host u128 decode, Q < 2^128)."""
-        tmp = self
-        if self.is_ntt_domain():
-            tmp = self.clone()
-            tmp.to_coeff_domain()
-        ch = tmp.channels()
-        if ch.ndim == 2:
-            ch = ch[None]
-        out = np.zeros((ch.shape[0], ch.shape[2]), dtype=object)
-        for b in range(ch.shape[0]):
-            for i in range(ch.shape[2]):
-                out[b, i] = self.basis.reconstruct_centered_coeff([int(v) for v in ch[b, :, i]])
-        out = out.astype(np.int64)
+        """PolyRing::to_coeffs (poly.rs:404-427): the centred CRT value of each
+        coefficient as i64 (its low 64 bits, like the reference), computed on
+        the device (rnt_to_coeffs)."""
+        out = np.zeros((self.n_polys, self.basis.degree), dtype=np.int64)
+        check(load().rnt_to_coeffs(self._h, out.ctypes.data_as(ctypes.c_void_p), self.n_polys))
+        return out[0] if self.n_polys == 1 else out
+
+    def to_coeffs_exact(self) -> list:
+        """The centred CRT values as Python ints for any Q (rnt_crt_centered):
+        [N] for one polynomial, [B][N] nested lists for a batch."""
+        bits = sum(int(q).bit_length() for q in self.basis.moduli())
+        words = max(1, (bits + 1 + 63) // 64)
+        raw = np.zeros((self.n_polys, self.basis.degree, words), dtype=np.uint64)
+        check(load().rnt_crt_centered(self._h, raw.ctypes.data_as(ctypes.c_void_p), self.n_polys, words))
+        out = []
+        for b in range(self.n_polys):
+            row = []
+            for i in range(self.basis.degree):
+                v = 0
+                for w in range(words - 1, -1, -1):
+                    v = (v << 64) | int(raw[b, i, w])
+                if v >> (64 * words - 1):  # two's complement sign
+                    v -= 1 << (64 * words)
+                row.append(v)
+            out.append(row)
         return out[0] if self.n_polys == 1 else out
 
     def __del__(self):

@@ -85,6 +85,8 @@ SIGNATURES = {
     "rnt_upload_coeffs": (c_int, [_P, _I64P, c_size_t]),
     "rnt_download": (c_int, [_P, _U64P, c_size_t]),
     "rnt_copy": (c_int, [_P, _P]),
+    "rnt_to_coeffs": (c_int, [_P, c_void_p, c_size_t]),
+    "rnt_crt_centered": (c_int, [_P, c_void_p, c_size_t, c_size_t]),
     "rnt_buf_wrap": (c_int, [_P, c_void_p, c_size_t, c_int, POINTER(c_void_p)]),
     "rnt_buf_device_ptr": (c_int, [_P, POINTER(c_void_p), POINTER(c_size_t)]),
     "rnt_ct_tensor": (c_int, [_P, _P, _P, _P, _P, _P, _P]),
