@@ -319,6 +319,11 @@ class RnsPoly:
         check(load().rnt_add(out._h, self._h, rhs._h))
         return out
 
+    def __sub__(self, rhs: "RnsPoly") -> "RnsPoly":
+        out = RnsPoly(self.basis, self.n_polys)
+        check(load().rnt_sub(out._h, self._h, rhs._h))
+        return out
+
     def __neg__(self) -> "RnsPoly":
         out = RnsPoly(self.basis, self.n_polys)
         check(load().rnt_neg(out._h, self._h))
