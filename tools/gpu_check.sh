@@ -19,7 +19,7 @@ step() {  # step <name> <seconds> <cmd...>
   fi
   return 0
 }
-step pytest_gpu 1200 python -m pytest tests -m gpu -x -q
+step pytest_gpu 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 3
 step bench_ctmul 900 python bench.py --workload ctmul --ct-batch ${CT_BATCH:-32} --steps 3 --warmup 1

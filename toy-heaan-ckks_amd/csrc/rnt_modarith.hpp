@@ -31,8 +31,23 @@ __host__ __device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) {
 }
 
 // x in [0, 2q) -> [0, q)
+//
+// On the device the 32-bit form is a borrow-select: v_sub_co_u32 (borrow
+// into VCC / an SGPR pair) + v_cndmask_b32, two full-rate instructions
+// (tools/oprate2.hip: 2.1 cycles each per wave64 on one SIMD), where the
+// min(x, x - q) form costs v_sub (2.2) + v_min_u32 (4.1, half rate).
+#ifndef RNT_BORROW_SELECT
+#define RNT_BORROW_SELECT 1
+#endif
 template <class W>
 __host__ __device__ __forceinline__ W csub(W x, W q) {
+#if defined(__HIP_DEVICE_COMPILE__) && RNT_BORROW_SELECT
+  if constexpr (sizeof(W) == 4) {
+    W y;
+    const bool borrow = __builtin_sub_overflow(x, q, &y);
+    return borrow ? x : y;
+  }
+#endif
   W y = x - q;
   return y < x ? y : x;  // min(x, x - q) as unsigned
 }
@@ -45,6 +60,13 @@ __host__ __device__ __forceinline__ W add_mod(W a, W b, W q) {
 // a, b in [0, q) -> a - b mod q
 template <class W>
 __host__ __device__ __forceinline__ W sub_mod(W a, W b, W q) {
+#if defined(__HIP_DEVICE_COMPILE__) && RNT_BORROW_SELECT
+  if constexpr (sizeof(W) == 4) {
+    W d;
+    const bool borrow = __builtin_sub_overflow(a, b, &d);
+    return borrow ? d + q : d;
+  }
+#endif
   W d = a - b;
   W e = d + q;
   return e < d ? e : d;  // min(d, d + q)
