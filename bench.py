@@ -171,9 +171,12 @@ def run_polymul(args, comm, world, rank, local_rank):
     comm.barrier()
     elapsed = comm.max(t1 - t0)
     kernels = {}
-    for k in ("col_fwd", "row_mul", "col_inv"):
+    # whole-plane path (N=2^16, u32: plane_fwd + plane_mul) or the
+    # three-launch column/row/column path (any other shape, RNT_PLANE=0)
+    for k in ("plane_fwd", "plane_mul", "col_fwd", "row_mul", "col_inv"):
         cnt, ms = B.profile_read(k)
-        kernels[k] = {"launches": cnt, "avg_ms": ms / cnt if cnt else None, "total_ms": ms}
+        if cnt:
+            kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
     B.profile_enable(False)
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -189,7 +192,8 @@ def run_polymul(args, comm, world, rank, local_rank):
     # the device word width) / its average launch time, measured with HIP
     # events on the library stream
     elem = Lr * batch * n
-    step_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb}
+    step_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb,
+                  "plane_fwd": 2 * elem * wb, "plane_mul": 3 * elem * wb}
     dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
     alg_bytes = {k: step_bytes[k] * args.steps / max(kernels[k]["launches"], 1) for k in kernels}
     achieved = alg_bytes[dom] / (kernels[dom]["avg_ms"] * 1e-3) / 1e9
@@ -347,6 +351,8 @@ def run_rotate(args, comm, world, rank, local_rank):
     L = 32 if args.limbs == 16 else args.limbs
     n = 1 << log_n
     mod = rn.generate_primes(31, L, n)
+    if world > 1 and args.shard == "limb":
+        return run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod)
     Bs = rn.RnsBasis(mod, n, device=local_rank)
     B = args.rot_batch
     rng = np.random.default_rng(5 + rank)
@@ -404,6 +410,70 @@ def run_rotate(args, comm, world, rank, local_rank):
         "roofline": {"bound": "valu", "kernel": "ks_rows", "unit": "butterflies/s",
                      "achieved": value / world * bfly, "peak": None, "frac": None, "traffic": None,
                      "kernels": kernels},
+        "cpu_baseline": None,
+    }
+
+
+def run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod):
+    """Config 5 limb-sharded: each rank owns L/world limbs of a
+    global batch of rot_batch * world ciphertexts and a [L][L_r][N] slice of
+    the rotation key; per offset: limb-local slot rotation, RCCL all-gather
+    of sigma(c1), key-switch of the local target limbs."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from rns_ntt.sharded import GpuBackend, LimbShardedPipeline, TorchDistComm
+
+    n = 1 << log_n
+    torch.cuda.set_device(local_rank)
+    pipe = LimbShardedPipeline(mod, n, TorchDistComm(dist.new_group(backend="nccl")), GpuBackend(local_rank))
+    B = args.rot_batch * world
+    rng = np.random.default_rng(5)
+    uniq = min(2, B)
+    reps = (B + uniq - 1) // uniq
+    c0 = pipe.upload(np.tile(uniform(rng, mod, uniq, n), (reps, 1, 1))[:B])
+    c1 = pipe.upload(np.tile(uniform(rng, mod, uniq, n), (reps, 1, 1))[:B])
+    key = pipe.upload_key(uniform(rng, mod, L, n), uniform(rng, mod, L, n))
+    offsets = [1 << e for e in range(log_n - 1)]
+
+    def step():
+        for k in offsets:
+            pipe.rotate(c0, c1, k, key)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = comm.max(t1 - t0)
+    value = B * len(offsets) * args.steps / elapsed
+    bfly = (L * L + 2 * L) * (n // 2) * log_n
+    return {
+        "metric": ROT_METRIC,
+        "value": value,
+        "unit": "rotations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded uniform residues and key; one key reused for every offset)",
+        "config": {
+            "workload": f"rotate_ciphertext sweep over {len(offsets)} power-of-two offsets, "
+                        f"N=2^{log_n}, L={L} x 31-bit primes, {B} ciphertexts (global)",
+            "parallelism": f"limb-sharded x{world}: RCCL all-gather of sigma(c1) per offset",
+        },
+        "roofline": {"bound": "valu", "kernel": "ks_rows", "unit": "butterflies/s",
+                     "achieved": value / world * bfly, "peak": None, "frac": None, "traffic": None},
         "cpu_baseline": None,
     }
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define RNT_ABI_VERSION 1
+#define RNT_ABI_VERSION 2
 
 /* Status codes.  1..6 mirror RnsNttError in order
  * (src/rings/backends/rns_ntt/errors.rs:4-20). */
@@ -174,6 +174,22 @@ int rnt_automorphism(rnt_buf* out, const rnt_buf* in, uint64_t g);
 /* rotate_slots (poly.rs:546-569): g = 5^k mod 2N (k >= 0); for k < 0 the
  * reference's automorphism(5^|k|) then automorphism(2N-1). */
 int rnt_rotate_slots(rnt_buf* out, const rnt_buf* in, int32_t k);
+
+/* ---- CKKS encoder / decoder (src/encoding) ---------- */
+/* CkksEncoder::encode_complex (ckks_encoder.rs:85-122) for every poly of
+ * `out`: values = [n_polys][n_values] complex slots as interleaved (re, im)
+ * doubles, n_values <= N/2 (zero-padded to N/2, build_conjugate_slots,
+ * special_fft.rs:158-178); slots times 2^scale_bits -> the inverse canonical
+ * embedding (special_idft, special_fft.rs:194-220, as an O(N log N) special
+ * FFT) -> coefficients rounded like f64::round -> residues like from_coeffs
+ * (poly.rs:49-67).  `out` becomes coefficient domain.  n_values > N/2 or
+ * scale_bits == 0 -> RNT_ERR_BAD_ARGUMENT (the reference panics). */
+int rnt_encode(rnt_buf* out, const double* values, size_t n_values, uint32_t scale_bits);
+/* CkksEncoder::decode_complex (ckks_encoder.rs:134-156): centred CRT
+ * coefficients (to_coeffs, poly.rs:404-427, its i64 result) -> the canonical
+ * embedding (special_dft, special_fft.rs:224-242) -> the first n_values
+ * slots / 2^scale_bits into values ([n_polys][n_values] (re, im) pairs). */
+int rnt_decode(const rnt_buf* in, double* values, size_t n_values, uint32_t scale_bits);
 
 /* ---- engine-level fused ops (src/crypto/engine.rs) -------------------- */
 /* A gadget key (RnsGadgetRelinKey / RnsGadgetRotationKey, engine.rs:224-253):

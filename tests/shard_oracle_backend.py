@@ -65,13 +65,27 @@ class OracleBackend:
         ka, kb = key
         src = src_full.numpy().astype(np.uint64)  # [L][B][N]
         ob = basis.ob
-        o0, o1 = _to_bln(d0), _to_bln(d1)
-        for p in range(src.shape[1]):
+        B = src.shape[1]
+        zero = np.zeros((B, len(basis.mods), basis.n), dtype=np.uint64)
+        o0 = _to_bln(d0) if d0 is not None else zero.copy()
+        o1 = _to_bln(d1) if d1 is not None else zero.copy()
+        for p in range(B):
             for i in range(src.shape[0]):
                 alpha = np.stack([src[i, p] % np.uint64(q) for q in basis.mods])
                 o0[p] = orc.add(ob, o0[p], orc.mul(ob, alpha, kb[i]))
                 o1[p] = orc.add(ob, o1[p], orc.mul(ob, alpha, ka[i]))
         return _from_bln(o0), _from_bln(o1)
+
+    def rotate(self, basis, poly, k):
+        """poly.rs:546-569 per poly on this rank's limbs."""
+        x = _to_bln(poly)
+        return _from_bln(np.stack([orc.rotate_slots(basis.ob, x[p], k)[0] for p in range(x.shape[0])]))
+
+    rotate_planes = rotate
+
+    def add(self, basis, a, b):
+        x, y = _to_bln(a), _to_bln(b)
+        return _from_bln(np.stack([orc.add(basis.ob, x[p], y[p]) for p in range(x.shape[0])]))
 
     def last_limb(self, poly):
         return poly[-1]

@@ -26,7 +26,7 @@ def declared_functions():
 
 def test_library_loads_and_exports_every_declared_symbol():
     lib = rns_ntt.load()
-    assert lib.rnt_abi_version() == 1
+    assert lib.rnt_abi_version() == 2
     names = declared_functions()
     assert len(names) >= 35
     for n in names:

@@ -1,4 +1,5 @@
-"""Limb-sharded ct x ct -> relin -> rescale.
+"""Limb-sharded ct x ct -> relin -> rescale and
+limb-sharded rotation key-switch.
 
 CPU: world_size 2/3 gloo ranks run rns_ntt.sharded.LimbShardedPipeline with
 the oracle backend (tests/shard_oracle_backend.py); the assembled per-rank
@@ -125,6 +126,73 @@ def test_limb_sharded_gloo_matches_unsharded(world, L):
         assert np.array_equal(g.astype(np.uint64), w)
 
 
+ROT_K = (1, -3, 0)  # slot offsets; negative = rotate_slots(k < 0), 0 = identity
+
+
+def _rot_inputs(mods, n, B, seed):
+    rng = np.random.default_rng(seed)
+    L = len(mods)
+    c0 = orc.uniform_poly(mods, n, rng, batch=B)
+    c1 = orc.uniform_poly(mods, n, rng, batch=B)
+    key_a = orc.uniform_poly(mods, n, rng, batch=L)
+    key_b = orc.uniform_poly(mods, n, rng, batch=L)
+    return c0, c1, key_a, key_b
+
+
+def _rot_oracle(mods, n, c0, c1, key_a, key_b, k):
+    """engine.rs:412-463 restated (oracle/oracle.c or_rotate_ciphertext)."""
+    ob = orc.Basis(mods, n)
+    r = [orc.rotate_ciphertext(ob, c0[p], c1[p], k, key_a, key_b) for p in range(c0.shape[0])]
+    return np.stack([x[0] for x in r]), np.stack([x[1] for x in r])
+
+
+def _run_rank_rotate(pipe, c0, c1, key_a, key_b):
+    x0, x1 = pipe.upload(c0), pipe.upload(c1)
+    key = pipe.upload_key(key_a, key_b)
+    outs = []
+    for k in ROT_K:
+        o0, o1 = pipe.rotate(x0, x1, k, key)
+        outs.append((pipe.download(o0), pipe.download(o1)))
+    return outs
+
+
+def _gloo_rot_worker(rank, world, port, mods, n, B, seed, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from rns_ntt.sharded import LimbShardedPipeline, TorchDistComm
+    from shard_oracle_backend import OracleBackend
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c0, c1, key_a, key_b = _rot_inputs(mods, n, B, seed)
+        pipe = LimbShardedPipeline(mods, n, TorchDistComm(), OracleBackend())
+        q.put((rank, _run_rank_rotate(pipe, c0, c1, key_a, key_b)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,L", [(2, 4), (3, 5)])
+def test_limb_sharded_rotation_gloo_matches_unsharded(world, L):
+    n, B, seed = 32, 2, 21
+    mods = orc.generate_primes(31, L, n)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_rot_worker, args=(r, world, port, mods, n, B, seed, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    results = sorted(_collect(q, procs, world), key=lambda r: r[0])
+    c0, c1, key_a, key_b = _rot_inputs(mods, n, B, seed)
+    for ki, k in enumerate(ROT_K):
+        want0, want1 = _rot_oracle(mods, n, c0, c1, key_a, key_b, k)
+        got0 = np.concatenate([r[1][ki][0] for r in results], axis=1)
+        got1 = np.concatenate([r[1][ki][1] for r in results], axis=1)
+        assert np.array_equal(got0.astype(np.uint64), want0), k
+        assert np.array_equal(got1.astype(np.uint64), want1), k
+
+
 def test_sharded_layout_bookkeeping():
     """Rescale drops the last limb only on its owner; later joins follow."""
     from rns_ntt.sharded import LimbShardedPipeline
@@ -190,6 +258,49 @@ def test_limb_sharded_gpu_threads_match_unsharded(gpu, world):
     want = _oracle_reference(mods, n, [x[:1] for x in cts], key_a, key_b)
     for g, w in zip(got, want):
         assert np.array_equal(g[:1], w)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_limb_sharded_rotation_gpu_threads_match_unsharded(gpu, world):
+    """Config 5's limb-sharded rotation on simulated ranks (threads) vs the
+    fused unsharded rnt_ct_rotate and the oracle."""
+    import threading
+
+    import rns_ntt as rn
+    from rns_ntt.sharded import GpuBackend, LimbShardedPipeline, ThreadComm
+
+    n, L, B, seed = 2048, 6, 2, 31
+    mods = rn.generate_primes(31, L, n)
+    c0, c1, key_a, key_b = _rot_inputs(mods, n, B, seed)
+    comm = ThreadComm(world)
+    results, errors = [None] * world, []
+
+    def rank_main(r):
+        try:
+            pipe = LimbShardedPipeline(mods, n, comm.rank_view(r), GpuBackend(0))
+            results[r] = _run_rank_rotate(pipe, c0, c1, key_a, key_b)
+        except BaseException as e:  # surface thread failures in the test
+            errors.append(e)
+            comm._bar.abort()
+
+    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=600)
+    assert not errors, errors
+    Bf = rn.RnsBasis(mods, n)
+    x0, x1 = rn.RnsPoly.from_channels(c0, Bf), rn.RnsPoly.from_channels(c1, Bf)
+    for ki, k in enumerate(ROT_K):
+        got0 = np.concatenate([results[r][ki][0] for r in range(world)], axis=1)
+        got1 = np.concatenate([results[r][ki][1] for r in range(world)], axis=1)
+        key = rn.RnsGadgetKey.from_channels(key_a, key_b, Bf, rotation=k)
+        ref = rn.rotate_ciphertext(rn.Ciphertext(x0, x1), key)
+        assert np.array_equal(got0, ref.c0.channels()), k
+        assert np.array_equal(got1, ref.c1.channels()), k
+        want0, want1 = _rot_oracle(mods, n, c0[:1], c1[:1], key_a, key_b, k)
+        assert np.array_equal(got0[:1], want0) and np.array_equal(got1[:1], want1), k
 
 
 @pytest.mark.gpu

@@ -12,12 +12,12 @@ keys = sys.argv[2:]
 
 
 def short(n):
-    n = n.replace("void rnt::", "").split("(")[0]
+    n = n.replace("void rnt::", "").replace("(anonymous namespace)::", "").split("(")[0]
     return n
 
 
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
-for sub in ("fetch", "write", "sq", "grbm"):
+for sub in ("fetch", "write", "sq", "grbm", "ic"):
     for f in glob.glob(os.path.join(d, sub, "**", "*counter_collection*.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             vals[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -38,3 +38,6 @@ for k, c in sorted(vals.items(), key=lambda kv: -trace.get(kv[0], (0, 0))[1] * t
     print(f"{k[:48]:48s} calls {calls:4d} avg {ns/1e3:9.1f} us  HBM {hbm/1e6:9.1f} MB ({hbm/ns:6.2f} TB/s)  "
           f"clk {clk:4.2f}  active {avg.get('SQ_ACTIVE_INST_ANY',0)/w:4.2f} issue-stall {avg.get('SQ_WAIT_INST_ANY',0)/w:4.2f} "
           f"wait {avg.get('SQ_WAIT_ANY',0)/w:4.2f}  VALU/wave {avg.get('SQ_INSTS_VALU',0)/max(avg.get('SQ_WAVES',1),1):7.0f}")
+    if "SQC_ICACHE_MISSES" in avg:
+        print(f"{'':48s} icache misses {avg['SQC_ICACHE_MISSES']:.0f} hits {avg.get('SQC_ICACHE_HITS',0):.0f} "
+              f"lds-issue-stall {avg.get('SQ_WAIT_INST_LDS',0)/w:4.2f} smem {avg.get('SQ_INSTS_SMEM',0)/max(avg.get('SQ_WAVES',1),1):.0f}/wave")

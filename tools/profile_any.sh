@@ -18,3 +18,6 @@ step fetch --pmc FETCH_SIZE
 step write --pmc WRITE_SIZE
 step sq --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
 step grbm --pmc GRBM_GUI_ACTIVE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU
+if [ -n "$ICACHE" ]; then
+  step ic --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_WAIT_INST_LDS SQ_INSTS_SMEM
+fi

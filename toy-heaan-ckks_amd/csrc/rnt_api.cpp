@@ -48,7 +48,8 @@ inline size_t word_bytes(const rnt::Tables* t) { return t->wide ? 8 : 4; }
 
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
-    "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt"};
+    "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
+    "plane_fwd", "plane_mul", "sfft"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -187,6 +188,9 @@ rnt::Tables::~Tables() {
   for (auto& e : crt_cache) (void)hipFree(e.second.dev);
   (void)hipFree(tw_fwd);
   (void)hipFree(tw_inv);
+  (void)hipFree(mtw_fwd);
+  (void)hipFree(mtw_inv);
+  (void)hipFree(sfft_tw);
   (void)hipFree(lconst);
   (void)hipFree(resc);
   (void)hipFree(resc_p);
@@ -269,6 +273,9 @@ int build_tables(rnt::Tables* t) {
   std::vector<rnt::LimbConst<W>> lc(L);
   std::vector<W> resc(L * L, 0), rescp(L * L, 0);
   std::vector<uint64_t> pw(n), ipw(n);
+  // Montgomery-form twiddles for the whole-plane kernels (rnt_plane.hip)
+  const bool mont_tabs = wbits == 32;
+  std::vector<uint32_t> mtw(mont_tabs ? L * n : 0), mitw(mont_tabs ? L * n : 0);
   for (size_t l = 0; l < L; ++l) {
     const uint64_t q = t->moduli[l];
     const uint64_t psi = find_psi(q, n);
@@ -291,6 +298,13 @@ int build_tables(rnt::Tables* t) {
       T[g] = {(W)pw[e], (W)shoup_companion(pw[e], q, wbits)};
       I[g] = {(W)ipw[e], (W)shoup_companion(ipw[e], q, wbits)};
     }
+    if (mont_tabs) {
+      const uint64_t r32 = (uint64_t)((((u128)1) << 32) % q);
+      for (size_t g = 0; g < n; ++g) {
+        mtw[l * n + g] = (uint32_t)mulmod((uint64_t)T[g].w, r32, q);
+        mitw[l * n + g] = (uint32_t)mulmod((uint64_t)I[g].w, r32, q);
+      }
+    }
     rnt::LimbConst<W>& c = lc[l];
     c.q = (W)q;
     c.qinv = (W)neg_free_qinv(q, wbits);
@@ -309,6 +323,10 @@ int build_tables(rnt::Tables* t) {
     c.c1r_p = (W)shoup_companion(ninvr, q, wbits);
     c.c2r = (W)mulmod(w1, ninvr, q);
     c.c2r_p = (W)shoup_companion(c.c2r, q, wbits);
+    c.qneg = (W)(W(0) - c.qinv);
+    const uint64_t ninvrr = mulmod(ninvr, r, q);
+    c.mc1 = (W)ninvrr;
+    c.mc2 = (W)mulmod(w1, ninvrr, q);
     {
       // q = k * 2^s + 1; the 32-bit path uses s capped so that 32 - s <= 24
       unsigned sh = (unsigned)__builtin_ctzll(q - 1);
@@ -333,6 +351,13 @@ int build_tables(rnt::Tables* t) {
   HIP_TRY(hipMalloc(&t->resc_p, L * L * sizeof(W)), "hipMalloc(tables)");
   HIP_TRY(hipMemcpy(t->tw_fwd, tw.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
   HIP_TRY(hipMemcpy(t->tw_inv, itw.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
+  if (mont_tabs) {
+    const size_t mb = L * n * sizeof(uint32_t);
+    HIP_TRY(hipMalloc(&t->mtw_fwd, mb), "hipMalloc(tables)");
+    HIP_TRY(hipMalloc(&t->mtw_inv, mb), "hipMalloc(tables)");
+    HIP_TRY(hipMemcpy(t->mtw_fwd, mtw.data(), mb, hipMemcpyHostToDevice), "hipMemcpy");
+    HIP_TRY(hipMemcpy(t->mtw_inv, mitw.data(), mb, hipMemcpyHostToDevice), "hipMemcpy");
+  }
   HIP_TRY(hipMemcpy(t->lconst, lc.data(), L * sizeof(rnt::LimbConst<W>), hipMemcpyHostToDevice),
           "hipMemcpy");
   HIP_TRY(hipMemcpy(t->resc, resc.data(), L * L * sizeof(W), hipMemcpyHostToDevice), "hipMemcpy");
@@ -664,8 +689,9 @@ extern "C" int rnt_ntt_inv(rnt_buf* b) {
 // HBM-bound column passes can overlap another's VALU-bound row pass.
 // RNT_MUL_CHUNKS / RNT_MUL_STREAMS override the defaults (A/B tuning).
 struct MulPlan {
-  size_t chunk;  // polys per slice
-  int streams;   // 1 = the context stream only
+  size_t chunk;   // polys per slice
+  int streams;    // 1 = the context stream only
+  bool resident;  // slices go through a reused per-stream scratch
 };
 static long env_long(const char* name, long dflt) {
   const char* e = getenv(name);
@@ -674,9 +700,12 @@ static long env_long(const char* name, long dflt) {
 static MulPlan mul_plan(size_t B) {
   static const long chunks = env_long("RNT_MUL_CHUNKS", 1);
   static const long streams = env_long("RNT_MUL_STREAMS", 1);
+  static const long resident = env_long("RNT_MUL_RESIDENT", 0);
   MulPlan p;
   const size_t c = chunks > 1 ? (size_t)chunks : 1;
   p.chunk = std::max<size_t>(1, (B + c - 1) / c);
+  p.resident = resident > 0;
+  if (p.resident) p.chunk = std::min<size_t>(B, (size_t)resident);
   p.streams = (int)std::max(1L, std::min<long>(streams, rnt::Tables::kAux));
   if (p.chunk >= B) p.streams = 1;
   return p;
@@ -705,6 +734,14 @@ static hipError_t aux_join(rnt::Tables* t, int n) {
   return e;
 }
 
+// RNT_PLANE=1 enables the whole-plane product path (rnt_plane.hip).  It is
+// off by default: measured 92k vs 112k poly-muls/s for the three-launch path
+// ("whole-plane experiment").
+static bool plane_enabled() {
+  static const bool on = env_long("RNT_PLANE", 0) != 0;
+  return on;
+}
+
 extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   if (int rc = check_buf(out, "rnt_mul")) return rc;
   if (int rc = check_buf(a, "rnt_mul")) return rc;
@@ -725,10 +762,26 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   // in the Infinity Cache between the launches.
   const uint64_t ls = limb_stride(out);
   const size_t wb = word_bytes(k.t);
-  if (int rc = ensure_ws(out, poly_words(out) * wb)) return rc;
   const size_t B = out->n_polys;
+  if (plane_enabled() && rnt::plane_supported(k.t)) {
+    // whole-plane path (rnt_plane.hip): b^ into the workspace, then a * b^
+    if (int rc = ensure_ws(out, poly_words(out) * wb)) return rc;
+    LAUNCH(k.t, rnt::K_PLANE_FWD, rnt::launch_plane_fwd(k, out->ws, ls, b->data, ls), "plane forward");
+    LAUNCH(k.t, rnt::K_PLANE_MUL, rnt::launch_plane_mul(k, out->data, ls, a->data, ls, out->ws, ls),
+           "plane mul");
+    out->in_ntt = 0;
+    return RNT_OK;
+  }
   const MulPlan plan = mul_plan(B);
   const size_t n = k.t->n;
+  // resident: per stream a [2][L][chunk][N] scratch that every slice reuses,
+  // so the intermediates are rewritten in place in the Infinity Cache
+  const size_t scratch_words = 2 * k.L * plan.chunk * n;
+  if (plan.resident) {
+    if (int rc = ensure_ws(out, scratch_words * plan.streams * wb)) return rc;
+  } else if (int rc = ensure_ws(out, poly_words(out) * wb)) {
+    return rc;
+  }
   rnt::Tables* tm = const_cast<rnt::Tables*>(k.t);
   if (plan.streams > 1) HIP_TRY(aux_fork(tm, plan.streams), "stream fork");
   int si = 0;
@@ -741,6 +794,17 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
     char* w = (char*)out->ws + off;
     const char* pa = (const char*)a->data + off;
     const char* pb = (const char*)b->data + off;
+    if (plan.resident) {
+      char* s0 = (char*)out->ws + (size_t)si * scratch_words * wb;
+      char* s1 = s0 + scratch_words / 2 * wb;
+      const uint64_t sls = (uint64_t)kc.B * n;
+      LAUNCH_ON(kc.t, kc.s, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, s0, pa, s1, pb, ls, sls),
+                "column forward");
+      LAUNCH_ON(kc.t, kc.s, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, s0, s1, sls), "row mul");
+      LAUNCH_ON(kc.t, kc.s, rnt::K_COL_INV, rnt::launch_col_inv(kc, o, ls, s0, sls, 1, nullptr),
+                "column inverse");
+      continue;
+    }
     LAUNCH_ON(kc.t, kc.s, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, o, pa, w, pb, ls, ls),
               "column forward");
     LAUNCH_ON(kc.t, kc.s, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, o, w, ls), "row mul");
@@ -1014,6 +1078,107 @@ extern "C" int rnt_to_coeffs(const rnt_buf* buf, int64_t* host, size_t n_polys) 
 
 extern "C" int rnt_crt_centered(const rnt_buf* buf, uint64_t* host, size_t n_polys, size_t words) {
   return crt_download(buf, host, n_polys, words, "rnt_crt_centered");
+}
+
+// ---------------------------------------------------------------------------
+// CKKS encoder / decoder (ckks_encoder.rs:85-156, special_fft.rs; the
+// special FFT in rnt_encode.hip)
+// ---------------------------------------------------------------------------
+static int sfft_table(const rnt_ctx* ctx, const void** tab) {
+  rnt::Tables* t = ctx->t.get();
+  std::lock_guard<std::mutex> g(t->sfft_mu);
+  if (!t->sfft_tw) {
+    const std::vector<double> h = rnt::sfft_twiddles(t->log_n);
+    void* d = nullptr;
+    HIP_TRY(hipMalloc(&d, h.size() * sizeof(double)), "hipMalloc(sfft twiddles)");
+    const hipError_t e = hipMemcpy(d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(d);
+      return hip_fail(e, "hipMemcpy(sfft twiddles)");
+    }
+    t->sfft_tw = d;
+  }
+  *tab = t->sfft_tw;
+  return RNT_OK;
+}
+
+static int sfft_check(const rnt_buf* b, const double* values, size_t n_values,
+                      uint32_t scale_bits, const char* name) {
+  if (int rc = check_buf(b, name)) return rc;
+  const size_t n = b->ctx->t->n;
+  if (!rnt::sfft_supported(b->ctx->t->log_n))
+    return fail(RNT_ERR_BAD_ARGUMENT, "%s: degree %zu has no slots", name, n);
+  // ckks_encoder.rs:70-75 (a panic in the reference)
+  if (n_values > n / 2)
+    return fail(RNT_ERR_BAD_ARGUMENT, "%s: %zu values exceed max slots %zu", name, n_values, n / 2);
+  if (n_values && b->n_polys && !values) return fail(RNT_ERR_BAD_ARGUMENT, "%s: null values", name);
+  // ckks_encoder.rs:43 asserts scale_bits > 0; 2^scale_bits must be a finite f64
+  if (scale_bits == 0 || scale_bits > 1000)
+    return fail(RNT_ERR_BAD_ARGUMENT, "%s: scale_bits must be in [1, 1000], got %u", name, scale_bits);
+  return RNT_OK;
+}
+
+extern "C" int rnt_encode(rnt_buf* out, const double* values, size_t n_values, uint32_t scale_bits) {
+  if (int rc = sfft_check(out, values, n_values, scale_bits, "rnt_encode")) return rc;
+  if (int rc = set_device(out->ctx)) return rc;
+  const void* tw = nullptr;
+  if (int rc = sfft_table(out->ctx, &tw)) return rc;
+  rnt::Launch k = launch_for(out);
+  const size_t B = out->n_polys, n = k.t->n;
+  if (B == 0) {
+    out->in_ntt = 0;
+    return RNT_OK;
+  }
+  // stage: the slot values in, then the rounded i64 coefficients;
+  // ws: [B][N/2] complex working planes
+  if (int rc = ensure_stage(out, B * n * 8)) return rc;
+  if (int rc = ensure_ws(out, B * n * 8)) return rc;
+  if (n_values)
+    HIP_TRY(hipMemcpyAsync(out->stage, values, B * n_values * 16, hipMemcpyHostToDevice, k.s),
+            "hipMemcpy H2D");
+  LAUNCH(k.t, rnt::K_SFFT,
+         rnt::launch_sfft_encode(k, (int64_t*)out->stage, out->ws, out->stage, (uint32_t)n_values,
+                                 scale_bits, tw),
+         "special fft (encode)");
+  LAUNCH(k.t, rnt::K_IMPORT, rnt::launch_import_coeffs(k, out->data, (const int64_t*)out->stage),
+         "import_coeffs");
+  HIP_TRY(hipStreamSynchronize(k.s), "hipStreamSynchronize");
+  out->in_ntt = 0;
+  trim_stage(out);
+  return RNT_OK;
+}
+
+extern "C" int rnt_decode(const rnt_buf* cb, double* values, size_t n_values, uint32_t scale_bits) {
+  rnt_buf* b = const_cast<rnt_buf*>(cb);  // workspace / staging only
+  if (int rc = sfft_check(b, values, n_values, scale_bits, "rnt_decode")) return rc;
+  if (int rc = set_device(b->ctx)) return rc;
+  const void* tw = nullptr;
+  if (int rc = sfft_table(b->ctx, &tw)) return rc;
+  const void* consts = nullptr;
+  uint32_t mw = 0;
+  if (int rc = crt_tables(b->ctx, &consts, &mw)) return rc;
+  rnt::Launch k = launch_for(b);
+  const size_t B = b->n_polys, n = k.t->n;
+  if (B == 0 || n_values == 0) return RNT_OK;
+  // ws holds the coefficient-domain clone of an NTT-domain input, then the
+  // complex planes; stage the centred i64 coefficients (to_coeffs)
+  if (int rc = ensure_ws(b, std::max(poly_words(b) * word_bytes(k.t), B * n * 8))) return rc;
+  if (int rc = ensure_stage(b, B * n * 8)) return rc;
+  const void* src = b->data;
+  if (b->in_ntt) {  // poly.rs:408-417: a coefficient-domain clone
+    if (int rc = to_coeff_into(b, b->ws)) return rc;
+    src = b->ws;
+  }
+  LAUNCH(k.t, rnt::K_CRT, rnt::launch_crt(k, (uint64_t*)b->stage, src, consts, mw, 1), "crt");
+  LAUNCH(k.t, rnt::K_SFFT,
+         rnt::launch_sfft_decode(k, b->ws, (const int64_t*)b->stage, scale_bits, tw),
+         "special fft (decode)");
+  HIP_TRY(hipMemcpy2DAsync(values, n_values * 16, b->ws, (n / 2) * 16, n_values * 16, B,
+                           hipMemcpyDeviceToHost, k.s),
+          "hipMemcpy2D D2H");
+  HIP_TRY(hipStreamSynchronize(k.s), "hipStreamSynchronize");
+  trim_stage(b);
+  return RNT_OK;
 }
 
 extern "C" int rnt_mod_drop_last(rnt_buf* out, const rnt_buf* in) {

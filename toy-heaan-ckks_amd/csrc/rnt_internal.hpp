@@ -48,6 +48,10 @@ struct LimbConst {
   W c2r_p;
   W k;       // q = k * 2^s + 1 (32-bit path: s >= 8, see rnt_modarith.hpp)
   W s;
+  // whole-plane kernels (rnt_plane.hip, u32 only): Montgomery constants
+  W qneg;    // -q^-1 mod 2^w
+  W mc1;     // n^-1 * 2^2w mod q: last inverse stage after a Montgomery product
+  W mc2;     // psi_inv_rev[1] * n^-1 * 2^2w mod q
 };
 
 // A twiddle and its Shoup companion, interleaved so one load fetches both.
@@ -85,6 +89,9 @@ struct Tables {
   void* tw_fwd = nullptr;   // [L][N] Tw<W>{psi^{brv(g)}, companion}, heap order g in [1, N)
   void* tw_inv = nullptr;   // [L][N] Tw<W>{psi^{-brv(g)}, companion}
   void* lconst = nullptr;   // [L] LimbConst<W>
+  // [L][N] u32 psi^{+-brv(g)} * 2^32 mod q (Montgomery form; u32 bases only)
+  void* mtw_fwd = nullptr;
+  void* mtw_inv = nullptr;
   void* resc = nullptr;     // [L][L]: resc[l][i] = (q_l mod q_i)^-1 mod q_i, i < l
   void* resc_p = nullptr;   // [L][L] Shoup companions
   hipStream_t stream = nullptr;
@@ -101,6 +108,10 @@ struct Tables {
   std::vector<std::pair<uint64_t, void*>> resc_ext;
   // centred-CRT constants per limb count (rnt_to_coeffs / rnt_crt_centered)
   std::vector<std::pair<size_t, struct CrtDev>> crt_cache;
+  // CKKS special-FFT twiddles (rnt_encode.hip), [N/2] double2, built on
+  // first encode/decode
+  std::mutex sfft_mu;
+  void* sfft_tw = nullptr;
   struct Prof* prof = nullptr;  // per-kernel event timing (rnt_profile_*)
   ~Tables();
 };
@@ -108,7 +119,8 @@ struct Tables {
 // Kernel ids for rnt_profile_read.
 enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
-  K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT, K_COUNT
+  K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
+  K_PLANE_FWD, K_PLANE_MUL, K_SFFT, K_COUNT
 };
 
 struct Prof {
@@ -181,6 +193,13 @@ hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_
 // Montgomery factor 2^w.  addend (optional, coefficient domain, out layout).
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
                           uint64_t in_ls, int rfold, const void* addend);
+// Whole-plane product path (rnt_plane.hip; u32 bases at N = 2^16):
+// bhat <- forward transform of b in a private order; out <- a * b.
+bool plane_supported(const Tables* t);
+hipError_t launch_plane_fwd(const Launch& k, void* bhat, uint64_t bhat_ls, const void* b,
+                            uint64_t b_ls);
+hipError_t launch_plane_mul(const Launch& k, void* out, uint64_t out_ls, const void* a,
+                            uint64_t a_ls, const void* bhat, uint64_t bhat_ls);
 // Elementwise over k.L*k.B*N contiguous words: op 0 add, 1 sub, 2 neg,
 // 3 pointwise mul (canonical a*b mod q), 4 Montgomery product (a*b*2^-w).
 hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a,
@@ -216,5 +235,15 @@ hipError_t launch_ks_rows(const Launch& k, void* u0, void* u1, uint64_t u_ls, co
 hipError_t launch_tensor_rows(const Launch& k, void* d0hat, void* d1hat, void* d2row,
                               const void* c0, const void* c1, const void* c0p,
                               const void* c1p, uint64_t ls);
+// CKKS canonical embedding (rnt_encode.hip).  Twiddle table: N/2 complex
+// doubles (interleaved re, im).  encode: values [B][n_values] double2 ->
+// coeffs [B][N] i64 (work: [B][N/2] double2); decode: centred i64 coeffs
+// [B][N] -> work [B][N/2] double2 slots / 2^scale_bits.
+bool sfft_supported(uint32_t log_n);
+std::vector<double> sfft_twiddles(uint32_t log_n);
+hipError_t launch_sfft_encode(const Launch& k, int64_t* coeffs, void* work, const void* values,
+                              uint32_t n_values, uint32_t scale_bits, const void* tw);
+hipError_t launch_sfft_decode(const Launch& k, void* work, const int64_t* coeffs,
+                              uint32_t scale_bits, const void* tw);
 
 }  // namespace rnt

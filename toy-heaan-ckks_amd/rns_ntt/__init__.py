@@ -41,6 +41,8 @@ __all__ = [
     "mul_ciphertexts_gadget",
     "rotate_ciphertext",
     "rescale_ciphertext",
+    "Plaintext",
+    "CkksEncoder",
 ]
 
 
@@ -466,6 +468,73 @@ def rescale_ciphertext(ct: Ciphertext) -> Ciphertext:
     out1 = RnsPoly(new_basis, ct.c0.n_polys)
     check(load().rnt_ct_rescale(out0.handle, out1.handle, ct.c0.handle, ct.c1.handle))
     return Ciphertext(out0, out1, ct.logp - bits_dropped, ct.logq - bits_dropped)
+
+
+# ---------------------------------------------------------------------------
+# CKKS encoder (src/encoding/ckks_encoder.rs)
+# ---------------------------------------------------------------------------
+
+
+@dataclass
+class Plaintext:
+    """types.rs Plaintext: an encoded RnsPoly batch (one row of slots per
+    poly), its scale and slot count."""
+
+    poly: RnsPoly
+    scale_bits: int
+    slots: int
+
+
+class CkksEncoder:
+    """``CkksEncoder<DEGREE>`` (ckks_encoder.rs:32-157).  The canonical
+    embedding runs on the device as an O(N log N) special FFT
+    (rnt_encode / rnt_decode) instead of the reference's O(N^2) Vandermonde
+    evaluation; a 2-D ``values`` encodes one poly per row."""
+
+    def __init__(self, degree: int, scale_bits: int):
+        if degree <= 0 or degree & (degree - 1):
+            raise ValueError("CkksEncoder: DEGREE must be a power of two")
+        if scale_bits <= 0:
+            raise ValueError("CkksEncoder: scale_bits must be positive")
+        self.degree = degree
+        self.scale_bits = scale_bits
+
+    def scale_factor(self) -> float:
+        return 2.0 ** self.scale_bits
+
+    def max_slots(self) -> int:
+        return self.degree // 2
+
+    def encode(self, values, basis: RnsBasis) -> Plaintext:
+        """ckks_encoder.rs:65-82: real values, imaginary parts zero."""
+        return self.encode_complex(np.asarray(values, dtype=np.float64), basis, _name="encode")
+
+    def encode_complex(self, values, basis: RnsBasis, _name: str = "encode_complex") -> Plaintext:
+        """ckks_encoder.rs:85-99."""
+        if basis.degree != self.degree:
+            raise ValueError(f"{_name}: basis degree {basis.degree} != encoder degree {self.degree}")
+        v = np.asarray(values, dtype=np.complex128)
+        rows = v.reshape(1, -1) if v.ndim <= 1 else v
+        if rows.ndim != 2:
+            raise ValueError(f"{_name}: values must be 1-D (one poly) or 2-D (one row per poly)")
+        n_values = rows.shape[1]
+        if n_values > self.degree // 2:
+            raise ValueError(f"{_name}: {n_values} values exceed max slots {self.degree // 2}")
+        buf = np.ascontiguousarray(rows)
+        poly = RnsPoly(basis, rows.shape[0])
+        check(load().rnt_encode(poly.handle, buf.ctypes.data_as(ctypes.c_void_p), n_values, self.scale_bits))
+        return Plaintext(poly, self.scale_bits, n_values)
+
+    def decode(self, pt: Plaintext) -> np.ndarray:
+        """ckks_encoder.rs:129-131."""
+        return self.decode_complex(pt).real
+
+    def decode_complex(self, pt: Plaintext) -> np.ndarray:
+        """ckks_encoder.rs:134-156 (rows for a batch of polys)."""
+        B = pt.poly.n_polys
+        out = np.zeros((B, pt.slots), dtype=np.complex128)
+        check(load().rnt_decode(pt.poly.handle, out.ctypes.data_as(ctypes.c_void_p), pt.slots, pt.scale_bits))
+        return out[0] if B == 1 else out
 
 
 # ---------------------------------------------------------------------------

@@ -107,6 +107,8 @@ SIGNATURES = {
     "rnt_ct_mul_relin": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "rnt_ct_rotate": (c_int, [_P, _P, _P, _P, c_int32, _P, _P]),
     "rnt_ct_rescale": (c_int, [_P, _P, _P, _P]),
+    "rnt_encode": (c_int, [_P, c_void_p, c_size_t, c_uint32]),
+    "rnt_decode": (c_int, [_P, c_void_p, c_size_t, c_uint32]),
 }
 
 _lib = None

@@ -1,4 +1,4 @@
-"""Limb-sharded ciphertext pipeline (BASELINE config 4).
+"""Limb-sharded ciphertext pipeline (BASELINE configs 4 and 5).
 
 One process (rank) per GPU owns a contiguous run of the global RNS basis'
 limbs and holds every ciphertext of the batch restricted to them.  Every
@@ -13,6 +13,11 @@ ring op is limb-local; the two joins of ct x ct -> relin -> rescale are:
   limb of c0 and c1, so its owner BROADCASTS those two [B][N] planes and
   every rank rescales its limbs by them (rnt_rescale_ext); the owner also
   drops the limb.
+* rotation (engine.rs:412-463): the slot rotation X -> X^g permutes the
+  coefficients of each limb, so it is limb-local; the gadget sum over
+  sigma(c1) needs every source limb, so sigma(c1) is ALL-GATHERED (the
+  rotation join) and each rank forms its own target limbs of
+  c0' = sigma(c0) + acc0, c1' = acc1 with its slice of the rotation key.
 
 The collectives run on torch tensors: over RCCL (backend "nccl") between
 GPUs on xGMI, over gloo between CPU processes (tests), or between threads
@@ -187,15 +192,37 @@ class GpuBackend:
         return d0, d1, d2_t
 
     def keyswitch(self, basis, src_full, key, d0, d1):
+        """Gadget sum for this rank's limbs over the gathered source limbs
+        ([L][B][N] torch tensor); d0/d1 are NTT-domain seeds or None."""
         from . import keyswitch_ext
 
-        B, N, L = d0.n_polys, basis.degree, basis.channel_count()
+        B, N, L = int(src_full.shape[1]), basis.degree, basis.channel_count()
         self._sync_torch()
         out_t = self._empty(basis, (2, L, B, N))
         o0, o1 = self._wrap(basis, out_t[0], B), self._wrap(basis, out_t[1], B)
         keyswitch_ext(src_full.data_ptr(), src_full.shape[0], key, basis, B, d0, d1, o0, o1)
         basis.sync()
         return o0, o1
+
+    def rotate(self, basis, poly, k: int):
+        """rotate_slots (poly.rs:546-569) on this rank's limbs."""
+        return poly.rotate_slots(k)
+
+    def rotate_planes(self, basis, poly, k: int):
+        """rotate_slots into a torch-owned [L_r][B][N] tensor (the source of
+        the rotation join's all-gather)."""
+        from . import check, load
+
+        B = poly.n_polys
+        self._sync_torch()
+        t = self._empty(basis, (basis.channel_count(), B, basis.degree))
+        out = self._wrap(basis, t, B)
+        check(load().rnt_rotate_slots(out.handle, poly.handle, int(k)))
+        basis.sync()
+        return t
+
+    def add(self, basis, a, b):
+        return a + b
 
     def last_limb(self, poly):
         """[B][N] torch view of the last local limb (poly must be torch-backed)."""
@@ -266,6 +293,17 @@ class LimbShardedPipeline:
         d0, d1, d2 = self.backend.tensor(self.basis, c0, c1, c0p, c1p)
         d2_full = self.comm.all_gather_limbs(d2, self.counts)  # the relin join
         return self.backend.keyswitch(self.basis, d2_full, key, d0, d1)
+
+    # -- rotation (engine.rs:412-463) ---------------------------------------
+    def rotate(self, c0, c1, k: int, key):
+        """rotate_ciphertext with slot offset k and this rank's slice of the
+        rotation key (upload_key): sigma is limb-local, sigma(c1) is
+        all-gathered, the gadget sum runs on the local target limbs."""
+        r0 = self.backend.rotate(self.basis, c0, k)
+        r1 = self.backend.rotate_planes(self.basis, c1, k)
+        full = self.comm.all_gather_limbs(r1, self.counts)  # the rotation join
+        a0, a1 = self.backend.keyswitch(self.basis, full, key, None, None)
+        return self.backend.add(self.basis, a0, r0), a1
 
     # -- rescale (engine.rs:263-282) -----------------------------------------
     def rescale(self, c0, c1):
