@@ -4,8 +4,9 @@ The host samplers are not the reference's RNG streams, so parity is
 relational: key relations hold with small errors, and decryptions of
 encrypt / multiply+relin / rescale / rotate match the exact plaintext
 arithmetic within noise bounds.  This mirrors the reference's tolerance
-tests (tests/integration_mul.rs), with coefficient packing standing in for
-the f64 encoder, which is out of scope.
+tests (tests/integration_mul.rs).  The last two tests run the reference's
+examples/encrypt_mul.rs and examples/rotation_demo.rs end to end through
+the device encoder, with the examples' own parameters and error bounds.
 """
 from __future__ import annotations
 
@@ -106,3 +107,53 @@ def test_rotation_key_switch(gpu):
         want = rn.RnsPoly.from_coeffs(m, eng.basis).rotate_slots(k).to_coeffs()
         got = CkksEngine.decrypt(out, sk).to_coeffs_exact()
         assert _maxdiff(got, want) < 1 << 45, k
+
+
+@pytest.mark.gpu
+def test_encrypt_mul_example_slots(gpu):
+    """examples/encrypt_mul.rs: N=16, 4 x 31-bit primes, scale 2^30; encode ->
+    encrypt -> gadget mul -> rescale -> decrypt -> decode within 1e-4."""
+    rn = gpu
+    from rns_ntt.engine import CkksEngine
+
+    n = 16
+    eng = CkksEngine(rn.generate_primes(31, 4, n), n, error_std=3.2, hamming_weight=n // 2)
+    rng = np.random.default_rng(42)
+    sk = eng.generate_secret_key(rng)
+    pk = eng.generate_public_key(sk, rng)
+    rlk = eng.generate_gadget_relin_key(sk, rng)
+    a, b = [1.0, 2.0, 3.0, 4.0], [0.5, 1.0, 1.5, 2.0]
+    enc = rn.CkksEncoder(n, 30)
+    logq = eng.basis.total_bits()
+    ct_a = eng.encrypt(enc.encode(a, eng.basis), pk, rng, logq=logq)
+    ct_b = eng.encrypt(enc.encode(b, eng.basis), pk, rng, logq=logq)
+    assert ct_a.logp == 30
+    prod = CkksEngine.rescale_ciphertext(CkksEngine.mul_ciphertexts_gadget(ct_a, ct_b, rlk))
+    assert prod.logp == 60 - eng.basis.moduli()[-1].bit_length()
+    pt = CkksEngine.decrypt_plaintext(prod, CkksEngine.secret_on(sk, prod.c0.basis))
+    got = enc.decode(pt)[:4]
+    assert np.max(np.abs(got - np.multiply(a, b))) <= 1e-4
+
+
+@pytest.mark.gpu
+def test_rotation_demo_example_slots(gpu):
+    """examples/rotation_demo.rs: N=32, 3 x 30-bit primes, scale 2^58;
+    rotate(+1), add the original, rotate(+2); every slot within 1e-4."""
+    rn = gpu
+    from rns_ntt.engine import CkksEngine
+
+    n, slots = 32, 16
+    eng = CkksEngine(rn.generate_primes(30, 3, n), n, error_std=3.2, hamming_weight=n // 2)
+    rng = np.random.default_rng(7)
+    sk = eng.generate_secret_key(rng)
+    pk = eng.generate_public_key(sk, rng)
+    rk1 = eng.generate_gadget_rotation_key(sk, 1, rng)
+    rk2 = eng.generate_gadget_rotation_key(sk, 2, rng)
+    enc = rn.CkksEncoder(n, 58)
+    v = np.arange(1, slots + 1, dtype=np.float64)
+    ct = eng.encrypt(enc.encode(v, eng.basis), pk, rng)
+    r1 = CkksEngine.rotate_ciphertext(ct, rk1)
+    out = CkksEngine.rotate_ciphertext(CkksEngine.add_ciphertexts(ct, r1), rk2)
+    got = enc.decode(CkksEngine.decrypt_plaintext(out, sk))
+    want = np.roll(v + np.roll(v, -1), -2)  # rotate_vec: slot i <- slot i + k
+    assert np.max(np.abs(got - want)) <= 1e-4

@@ -10,9 +10,9 @@ The samplers are numpy's (ternary secret with a fixed Hamming weight,
 rounded Gaussian errors, uniform residues), because the reference's
 ChaCha20 + rand_distr streams cannot be reproduced bit-exactly.  Parity for
 these paths is therefore relational: key relations and decryption error
-bounds (tests/test_gpu_engine.py), as SURVEY §8f prescribes.  The CKKS
-encoder (f64 special FFT) is out of scope.  Callers pack plaintexts as
-scaled integer coefficients.
+bounds (tests/test_gpu_engine.py), as SURVEY §8f prescribes.  Plaintexts
+are either scaled integer coefficients (an RnsPoly) or slot-encoded
+``Plaintext``s from ``CkksEncoder`` (the device special FFT, §8f row 4).
 """
 from __future__ import annotations
 
@@ -21,7 +21,7 @@ from typing import Optional
 
 import numpy as np
 
-from . import (Ciphertext, RnsBasis, RnsGadgetKey, RnsPoly, mul_ciphertexts_gadget,
+from . import (Ciphertext, Plaintext, RnsBasis, RnsGadgetKey, RnsPoly, mul_ciphertexts_gadget,
                rescale_ciphertext, rotate_ciphertext)
 
 
@@ -97,8 +97,12 @@ class CkksEngine:
         return self._gadget_key(sk, sk.rotate_slots(rotation), rng, rotation)
 
     # -- encryption (engine.rs:84-127) -----------------------------------------
-    def encrypt(self, plaintext: RnsPoly, pk: PublicKey, rng, logp: int = 0,
+    def encrypt(self, plaintext, pk: PublicKey, rng, logp: int = 0,
                 logq: Optional[int] = None) -> Ciphertext:
+        """``plaintext`` is an RnsPoly (with ``logp``) or a Plaintext, whose
+        scale_bits become the ciphertext's logp (engine.rs:84-112)."""
+        if isinstance(plaintext, Plaintext):
+            logp, plaintext = plaintext.scale_bits, plaintext.poly
         u = RnsPoly.from_coeffs(self._ternary(rng)[0], self.basis)
         e0 = RnsPoly.from_coeffs(self._gaussian(rng)[0], self.basis)
         e1 = RnsPoly.from_coeffs(self._gaussian(rng)[0], self.basis)
@@ -110,6 +114,12 @@ class CkksEngine:
     def decrypt(ct: Ciphertext, sk: RnsPoly) -> RnsPoly:
         """m = c0 + c1 * s (engine.rs:114-127); sk must share ct's basis."""
         return ct.c1 * sk + ct.c0
+
+    @staticmethod
+    def decrypt_plaintext(ct: Ciphertext, sk: RnsPoly) -> Plaintext:
+        """engine.rs:114-128: the decryption as a Plaintext with
+        scale_bits = logp and all N/2 slots, ready for CkksEncoder.decode."""
+        return Plaintext(CkksEngine.decrypt(ct, sk), ct.logp, ct.c0.basis.degree // 2)
 
     @staticmethod
     def add_ciphertexts(ct1: Ciphertext, ct2: Ciphertext) -> Ciphertext:
