@@ -23,11 +23,15 @@ $(LIBDIR)/rnt_encode.o: $(CSRC)/rnt_encode.hip $(CSRC)/rnt_internal.hpp
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(LIBDIR)/rnt_sample.o: $(CSRC)/rnt_sample.hip $(CSRC)/rnt_internal.hpp
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIBDIR)/rnt_api.o: $(CSRC)/rnt_api.cpp $(CSRC)/rnt_internal.hpp $(CSRC)/rnt_hostmath.hpp include/rnsntt.h
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBDIR)/librnsntt.so: $(LIBDIR)/rnt_kernels.o $(LIBDIR)/rnt_plane.o $(LIBDIR)/rnt_encode.o $(LIBDIR)/rnt_api.o
+$(LIBDIR)/librnsntt.so: $(LIBDIR)/rnt_kernels.o $(LIBDIR)/rnt_plane.o $(LIBDIR)/rnt_encode.o $(LIBDIR)/rnt_sample.o $(LIBDIR)/rnt_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 oracle/liboracle.so: oracle/oracle.c oracle/oracle.h

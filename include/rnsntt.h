@@ -175,6 +175,21 @@ int rnt_automorphism(rnt_buf* out, const rnt_buf* in, uint64_t g);
  * reference's automorphism(5^|k|) then automorphism(2N-1). */
 int rnt_rotate_slots(rnt_buf* out, const rnt_buf* in, int32_t k);
 
+/* ---- samplers (PolySampler, src/rings/traits.rs:74-127) */
+/* Fill every poly of `out` (coefficient domain) from the counter-based
+ * Philox4x32-10 stream (seed, stream): a draw depends only on (seed, stream,
+ * sampler, poly, limb, index), never on launch geometry or batch split.  The
+ * reference's ChaCha20 streams are not reproduced.
+ *   uniform  : residues uniform in [0, q_l), independent per limb
+ *              (sample_uniform, poly.rs:438-444);
+ *   gaussian : round(N(0, std_dev)) per coefficient, reduced into every limb
+ *              (sample_gaussian, poly.rs:447-459); std_dev must be finite > 0;
+ *   ternary  : exactly hamming_weight coefficients +-1, the rest 0
+ *              (sample_tribits, poly.rs:462-469); hamming_weight <= N. */
+int rnt_sample_uniform(rnt_buf* out, uint64_t seed, uint64_t stream);
+int rnt_sample_gaussian(rnt_buf* out, double std_dev, uint64_t seed, uint64_t stream);
+int rnt_sample_ternary(rnt_buf* out, size_t hamming_weight, uint64_t seed, uint64_t stream);
+
 /* ---- CKKS encoder / decoder (src/encoding) ---------- */
 /* CkksEncoder::encode_complex (ckks_encoder.rs:85-122) for every poly of
  * `out`: values = [n_polys][n_values] complex slots as interleaved (re, im)

@@ -12,5 +12,5 @@ mkdir -p $V
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$C "$@" -c ${KSRC:-$C/rnt_kernels.hip} -o $V/k_$NAME.o &
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$C "$@" -c ${PSRC:-$C/rnt_plane.hip} -o $V/p_$NAME.o &
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $V/k_$NAME.o $V/p_$NAME.o $L/rnt_encode.o $L/rnt_api.o -o $V/librnsntt_$NAME.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $V/k_$NAME.o $V/p_$NAME.o $L/rnt_encode.o $L/rnt_sample.o $L/rnt_api.o -o $V/librnsntt_$NAME.so
 echo $V/librnsntt_$NAME.so

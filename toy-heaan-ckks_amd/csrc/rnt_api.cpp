@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cinttypes>
 #include <cstdarg>
 #include <cstdio>
@@ -49,7 +50,7 @@ inline size_t word_bytes(const rnt::Tables* t) { return t->wide ? 8 : 4; }
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
-    "plane_fwd", "plane_mul", "sfft"};
+    "plane_fwd", "plane_mul", "sfft", "sample"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -1078,6 +1079,45 @@ extern "C" int rnt_to_coeffs(const rnt_buf* buf, int64_t* host, size_t n_polys) 
 
 extern "C" int rnt_crt_centered(const rnt_buf* buf, uint64_t* host, size_t n_polys, size_t words) {
   return crt_download(buf, host, n_polys, words, "rnt_crt_centered");
+}
+
+// ---------------------------------------------------------------------------
+// samplers (PolySampler, traits.rs:74-127; rnt_sample.hip)
+// ---------------------------------------------------------------------------
+static int sample_into(rnt_buf* out, int kind, double sigma, size_t h, uint64_t seed,
+                       uint64_t stream, const char* name) {
+  if (int rc = set_device(out->ctx)) return rc;
+  rnt::Launch k = launch_for(out);
+  rnt::SampleKey s;
+  s.k0 = (uint32_t)seed;
+  s.k1 = (uint32_t)(seed >> 32) ^ (uint32_t)(stream >> 32);
+  s.stream = (uint32_t)stream;
+  LAUNCH(k.t, rnt::K_SAMPLE, rnt::launch_sample(k, kind, out->data, s, sigma, (uint32_t)h), name);
+  out->in_ntt = 0;
+  return RNT_OK;
+}
+
+extern "C" int rnt_sample_uniform(rnt_buf* out, uint64_t seed, uint64_t stream) {
+  if (int rc = check_buf(out, "rnt_sample_uniform")) return rc;
+  return sample_into(out, 0, 0.0, 0, seed, stream, "sample_uniform");
+}
+
+extern "C" int rnt_sample_gaussian(rnt_buf* out, double std_dev, uint64_t seed, uint64_t stream) {
+  if (int rc = check_buf(out, "rnt_sample_gaussian")) return rc;
+  // poly.rs:452-453 / sampling.rs:31-45 panic on these
+  if (!(std_dev > 0.0) || !std::isfinite(std_dev))
+    return fail(RNT_ERR_BAD_ARGUMENT, "sample_gaussian: std_dev must be finite and positive");
+  return sample_into(out, 1, std_dev, 0, seed, stream, "sample_gaussian");
+}
+
+extern "C" int rnt_sample_ternary(rnt_buf* out, size_t hamming_weight, uint64_t seed,
+                                  uint64_t stream) {
+  if (int rc = check_buf(out, "rnt_sample_ternary")) return rc;
+  // sampling.rs:71-80 panics on an oversized Hamming weight
+  if (hamming_weight > out->ctx->t->n)
+    return fail(RNT_ERR_BAD_ARGUMENT, "sample_tribits: hamming weight %zu exceeds degree %zu",
+                hamming_weight, out->ctx->t->n);
+  return sample_into(out, 2, 0.0, hamming_weight, seed, stream, "sample_tribits");
 }
 
 // ---------------------------------------------------------------------------

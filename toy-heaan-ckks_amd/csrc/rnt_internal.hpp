@@ -120,7 +120,7 @@ struct Tables {
 enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
-  K_PLANE_FWD, K_PLANE_MUL, K_SFFT, K_COUNT
+  K_PLANE_FWD, K_PLANE_MUL, K_SFFT, K_SAMPLE, K_COUNT
 };
 
 struct Prof {
@@ -235,6 +235,15 @@ hipError_t launch_ks_rows(const Launch& k, void* u0, void* u1, uint64_t u_ls, co
 hipError_t launch_tensor_rows(const Launch& k, void* d0hat, void* d1hat, void* d2row,
                               const void* c0, const void* c1, const void* c0p,
                               const void* c1p, uint64_t ls);
+// Device samplers (rnt_sample.hip): kind 0 uniform residues, 1 rounded
+// Gaussian (sigma), 2 ternary with exactly `hamming_weight` nonzeros; every
+// poly of `out` ([k.L][k.B][N], limb stride k.B * N) in the coefficient domain.
+struct SampleKey {
+  uint32_t k0, k1;  // Philox key: seed low word, seed high word ^ stream high word
+  uint32_t stream;  // stream low word (a counter word)
+};
+hipError_t launch_sample(const Launch& k, int kind, void* out, SampleKey s, double sigma,
+                         uint32_t hamming_weight);
 // CKKS canonical embedding (rnt_encode.hip).  Twiddle table: N/2 complex
 // doubles (interleaved re, im).  encode: values [B][n_values] double2 ->
 // coeffs [B][N] i64 (work: [B][N/2] double2); decode: centred i64 coeffs

@@ -43,6 +43,7 @@ __all__ = [
     "rescale_ciphertext",
     "Plaintext",
     "CkksEncoder",
+    "DeviceRng",
 ]
 
 
@@ -85,6 +86,23 @@ def find_psi(modulus: int, degree: int) -> int:
     r = ctypes.c_uint64(0)
     check(load().rnt_find_psi(modulus, degree, ctypes.byref(r)))
     return int(r.value)
+
+
+class DeviceRng:
+    """The seeded generator passed where the reference passes ``&mut rng``
+    to a PolySampler (traits.rs:74-127).  Every sampler call takes the next
+    stream of the device's counter-based Philox4x32-10 generator
+    (rnt_sample_*), so a seed fixes every later sample, as a seeded
+    ChaCha20Rng does in the reference (whose streams are not reproduced)."""
+
+    def __init__(self, seed: int):
+        self.seed = int(seed) & ((1 << 64) - 1)
+        self.stream = 0
+
+    def next_stream(self) -> int:
+        s = self.stream
+        self.stream += 1
+        return s
 
 
 # ---------------------------------------------------------------------------
@@ -262,6 +280,30 @@ class RnsPoly:
         p.n_polys = n_polys
         p._owner = owner
         return p
+
+    # -- PolySampler (traits.rs:74-127; poly.rs:438-477), on the device -----
+    @classmethod
+    def sample_uniform(cls, basis: RnsBasis, rng: DeviceRng, n_polys: int = 1) -> "RnsPoly":
+        p = cls(basis, n_polys)
+        check(load().rnt_sample_uniform(p._h, rng.seed, rng.next_stream()))
+        return p
+
+    @classmethod
+    def sample_gaussian(cls, std_dev: float, basis: RnsBasis, rng: DeviceRng, n_polys: int = 1) -> "RnsPoly":
+        p = cls(basis, n_polys)
+        check(load().rnt_sample_gaussian(p._h, float(std_dev), rng.seed, rng.next_stream()))
+        return p
+
+    @classmethod
+    def sample_tribits(cls, hamming_weight: int, basis: RnsBasis, rng: DeviceRng, n_polys: int = 1) -> "RnsPoly":
+        p = cls(basis, n_polys)
+        check(load().rnt_sample_ternary(p._h, int(hamming_weight), rng.seed, rng.next_stream()))
+        return p
+
+    @classmethod
+    def sample_noise(cls, variance: float, basis: RnsBasis, rng: DeviceRng, n_polys: int = 1) -> "RnsPoly":
+        """poly.rs:471-477: Gaussian with std_dev = sqrt(variance)."""
+        return cls.sample_gaussian(float(np.sqrt(variance)), basis, rng, n_polys)
 
     def device_ptr(self) -> tuple[int, int]:
         """(device address of the [L][B][N] storage, word bytes)."""

@@ -109,6 +109,9 @@ SIGNATURES = {
     "rnt_ct_rescale": (c_int, [_P, _P, _P, _P]),
     "rnt_encode": (c_int, [_P, c_void_p, c_size_t, c_uint32]),
     "rnt_decode": (c_int, [_P, c_void_p, c_size_t, c_uint32]),
+    "rnt_sample_uniform": (c_int, [_P, c_uint64, c_uint64]),
+    "rnt_sample_gaussian": (c_int, [_P, ctypes.c_double, c_uint64, c_uint64]),
+    "rnt_sample_ternary": (c_int, [_P, c_size_t, c_uint64, c_uint64]),
 }
 
 _lib = None

@@ -6,9 +6,11 @@ multiply, rotate and rescale already in `rns_ntt`.  Every polynomial stays
 in device memory and every ring operation runs through librnsntt; only the
 random samples are drawn on the host.
 
-The samplers are numpy's (ternary secret with a fixed Hamming weight,
-rounded Gaussian errors, uniform residues), because the reference's
-ChaCha20 + rand_distr streams cannot be reproduced bit-exactly.  Parity for
+The samplers run on the device when ``rng`` is an ``rns_ntt.DeviceRng``
+(Philox4x32-10 streams, rnt_sample_*: ternary secret with a fixed Hamming
+weight, rounded Gaussian errors, uniform residues), or on the host with a
+numpy Generator; neither reproduces the reference's ChaCha20 + rand_distr
+streams bit-exactly.  Parity for
 these paths is therefore relational: key relations and decryption error
 bounds (tests/test_gpu_engine.py), as SURVEY §8f prescribes.  Plaintexts
 are either scaled integer coefficients (an RnsPoly) or slot-encoded
@@ -21,7 +23,7 @@ from typing import Optional
 
 import numpy as np
 
-from . import (Ciphertext, Plaintext, RnsBasis, RnsGadgetKey, RnsPoly, mul_ciphertexts_gadget,
+from . import (Ciphertext, DeviceRng, Plaintext, RnsBasis, RnsGadgetKey, RnsPoly, mul_ciphertexts_gadget,
                rescale_ciphertext, rotate_ciphertext)
 
 
@@ -49,7 +51,17 @@ class CkksEngine:
         self.error_std = error_std
         self.hamming_weight = hamming_weight if hamming_weight is not None else degree // 2
 
-    # -- host samplers (types/traits.rs PolySampler, not bit-compatible) -----
+    # -- samplers (traits.rs PolySampler): device for a DeviceRng, else host -
+    def _tern_poly(self, rng, count=1) -> RnsPoly:
+        if isinstance(rng, DeviceRng):
+            return RnsPoly.sample_tribits(self.hamming_weight, self.basis, rng, count)
+        return RnsPoly.from_coeffs(self._ternary(rng, count), self.basis)
+
+    def _gauss_poly(self, rng, count=1) -> RnsPoly:
+        if isinstance(rng, DeviceRng):
+            return RnsPoly.sample_gaussian(self.error_std, self.basis, rng, count)
+        return RnsPoly.from_coeffs(self._gaussian(rng, count), self.basis)
+
     def _ternary(self, rng, count=1):
         n = self.degree
         out = np.zeros((count, n), dtype=np.int64)
@@ -63,17 +75,19 @@ class CkksEngine:
 
     def _uniform(self, rng, count=1, basis: Optional[RnsBasis] = None):
         b = basis or self.basis
+        if isinstance(rng, DeviceRng):
+            return RnsPoly.sample_uniform(b, rng, count)
         q = np.array(b.moduli(), dtype=np.uint64)[None, :, None]
         ch = rng.integers(0, 1 << 62, size=(count, len(b.moduli()), self.degree), dtype=np.uint64) % q
         return RnsPoly.from_channels(ch, b)
 
     # -- keys (engine.rs:288-399, keys/*.rs) ---------------------------------
     def generate_secret_key(self, rng) -> RnsPoly:
-        return RnsPoly.from_coeffs(self._ternary(rng)[0], self.basis)
+        return self._tern_poly(rng)
 
     def generate_public_key(self, sk: RnsPoly, rng) -> PublicKey:
         a = self._uniform(rng)
-        b = -(a * sk) + RnsPoly.from_coeffs(self._gaussian(rng)[0], self.basis)
+        b = -(a * sk) + self._gauss_poly(rng)
         return PublicKey(b, a)
 
     def _gadget_key(self, sk: RnsPoly, target: RnsPoly, rng, rotation=None) -> RnsGadgetKey:
@@ -86,7 +100,7 @@ class CkksEngine:
             plain[i, i] = t[i]
         s_rep = RnsPoly.from_channels(np.broadcast_to(sk.channels(), (L, L, n)).copy(), self.basis)
         a = self._uniform(rng, count=L)
-        e = RnsPoly.from_coeffs(self._gaussian(rng, count=L), self.basis)
+        e = self._gauss_poly(rng, count=L)
         b = -(a * s_rep) + e + RnsPoly.from_channels(plain, self.basis)
         return RnsGadgetKey(a, b, rotation)
 
@@ -103,9 +117,9 @@ class CkksEngine:
         scale_bits become the ciphertext's logp (engine.rs:84-112)."""
         if isinstance(plaintext, Plaintext):
             logp, plaintext = plaintext.scale_bits, plaintext.poly
-        u = RnsPoly.from_coeffs(self._ternary(rng)[0], self.basis)
-        e0 = RnsPoly.from_coeffs(self._gaussian(rng)[0], self.basis)
-        e1 = RnsPoly.from_coeffs(self._gaussian(rng)[0], self.basis)
+        u = self._tern_poly(rng)
+        e0 = self._gauss_poly(rng)
+        e1 = self._gauss_poly(rng)
         c0 = pk.b * u + e0 + plaintext
         c1 = pk.a * u + e1
         return Ciphertext(c0, c1, logp, self.basis.total_bits() if logq is None else logq)
