@@ -6,6 +6,8 @@
 //
 // Build: __graft_entry__.build() -> tests/cpp/bin/test_rns_poly; run by
 // tests/test_cpp_host.py (-m gpu).  Exit status = number of failed tests.
+#include <cmath>
+#include <complex>
 #include <cstdio>
 #include <functional>
 #include <random>
@@ -278,6 +280,80 @@ int main() {
   run("basis_validation_matches_reference", [] {
     CHECK(throws_kind([] { RnsBasis<8>::create({}); }, RnsNttErrorKind::EmptyBasis));
     CHECK(throws_kind([] { RnsBasis<8>::create({19}); }, RnsNttErrorKind::NonNttFriendlyModulus));
+  });
+
+  // ---- CkksEncoder (ckks_encoder.rs:161-228 tests), on the device --------
+  // basis {97, 113}, scale_bits 5, epsilon 0.1, as in the reference module
+  const auto enc_basis = [] { return RnsBasis<8>::create({97, 113}); };
+  const auto near = [](double a, double b, double eps) { return std::fabs(a - b) <= eps; };
+  run("encoder_roundtrip_real_values", [&] {
+    CkksEncoder<8> enc(5);
+    const std::vector<double> values{1.0, -1.0, 0.5, -0.5};
+    const auto out = enc.decode(enc.encode(values, enc_basis()));
+    for (size_t i = 0; i < values.size(); ++i) CHECK(near(values[i], out[i], 0.1));
+  });
+  run("encoder_roundtrip_complex_values", [&] {
+    CkksEncoder<8> enc(5);
+    const std::vector<std::complex<double>> values{{1.0, 0.5}, {-0.5, 0.25}};
+    const auto out = enc.decode_complex(enc.encode_complex(values, enc_basis()));
+    for (size_t i = 0; i < values.size(); ++i) {
+      CHECK(near(values[i].real(), out[i].real(), 0.1));
+      CHECK(near(values[i].imag(), out[i].imag(), 0.1));
+    }
+  });
+  run("encoder_single_value_roundtrip", [&] {
+    CkksEncoder<8> enc(5);
+    CHECK(near(enc.decode(enc.encode({3.0}, enc_basis()))[0], 3.0, 0.1));
+  });
+  run("encoder_slot_count_preserved", [&] {
+    CkksEncoder<8> enc(5);
+    CHECK(enc.decode(enc.encode({1.0, 2.0, 3.0}, enc_basis())).size() == 3);
+  });
+  run("encoder_max_slots_is_half_degree", [] { CHECK(CkksEncoder<8>(10).max_slots() == 4); });
+  run("encoder_panics_on_too_many_values", [&] {
+    CkksEncoder<8> enc(5);
+    bool threw = false;
+    try {
+      enc.encode(std::vector<double>(5, 0.0), enc_basis());
+    } catch (const std::invalid_argument& e) {
+      threw = std::string(e.what()).find("exceed max slots") != std::string::npos;
+    }
+    CHECK(threw);
+  });
+
+  // ---- samplers (sampling.rs:98-242), on the device ----------------------
+  run("sample_gaussian_has_reasonable_mean_and_variance", [] {
+    std::mt19937_64 rng(17);
+    double sum = 0, sq = 0;
+    size_t cnt = 0;
+    for (int t = 0; t < 256; ++t) {
+      const auto c = Poly::sample_gaussian(3.2, basis_17_97(), rng).to_coeffs();
+      for (int64_t v : c) {
+        sum += (double)v;
+        sq += (double)v * v;
+        ++cnt;
+      }
+    }
+    const double mean = sum / cnt, var = sq / cnt - mean * mean;
+    CHECK(std::fabs(mean) < 0.5 && std::fabs(var - 3.2 * 3.2) < 2.5);
+  });
+  run("sample_tribits_handles_weight_extremes", [] {
+    std::mt19937_64 rng(5);
+    for (size_t hw : {size_t(0), size_t(8)}) {
+      const auto c = Poly::sample_tribits(hw, basis_17_97(), rng).to_coeffs();
+      size_t nz = 0;
+      for (int64_t v : c) {
+        CHECK(v >= -1 && v <= 1);
+        nz += v != 0;
+      }
+      CHECK(nz == hw);
+    }
+    CHECK(throws_kind([&] { Poly::sample_tribits(9, basis_17_97(), rng); }, RnsNttErrorKind::BadArgument));
+  });
+  run("sample_gaussian_rejects_non_positive_std_dev", [] {
+    std::mt19937_64 rng(1);
+    CHECK(throws_kind([&] { Poly::sample_gaussian(0.0, basis_17_97(), rng); }, RnsNttErrorKind::BadArgument));
+    CHECK(throws_kind([&] { Poly::sample_gaussian(-1.0, basis_17_97(), rng); }, RnsNttErrorKind::BadArgument));
   });
   std::printf("%d/%d passed\n", g_run - g_failed, g_run);
   return g_failed;

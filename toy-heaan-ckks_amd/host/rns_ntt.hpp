@@ -16,6 +16,8 @@
 #pragma once
 
 #include <array>
+#include <cmath>
+#include <complex>
 #include <cstdint>
 #include <memory>
 #include <optional>
@@ -246,45 +248,103 @@ class RnsPoly {
     return out;
   }
 
-  // PolySampler (traits.rs:74-127).  Host RNG: the reference's ChaCha20
-  // streams are not reproduced, only the distributions.
+  // PolySampler (traits.rs:74-127; poly.rs:438-477), sampled on the
+  // device (rnt_sample_*, Philox4x32-10).  The caller's Rng supplies only a
+  // 64-bit seed per call, so a seeded Rng fixes every sample, as in the
+  // reference; its ChaCha20 sample values are not reproduced.
   template <class Rng>
   static RnsPoly sample_uniform(const BasisRef<N>& basis, Rng& rng) {
-    const auto mods = basis->moduli();
-    std::vector<Channel> ch(mods.size());
-    for (size_t l = 0; l < mods.size(); ++l) {
-      std::uniform_int_distribution<uint64_t> d(0, mods[l] - 1);
-      for (auto& c : ch[l]) c = d(rng);
-    }
-    return from_channels(ch, basis, false);
+    RnsPoly p(basis);
+    check(rnt_sample_uniform(p.buf_, draw_seed(rng), 0));
+    return p;
   }
+  // sample_tribits: exactly hamming_weight coefficients +-1; a weight above
+  // N is a panic in the reference (sampling.rs:71-80), BadArgument here
   template <class Rng>
   static RnsPoly sample_tribits(size_t hamming_weight, const BasisRef<N>& basis, Rng& rng) {
-    std::vector<int64_t> c(N, 0);
-    std::vector<size_t> idx(N);
-    for (size_t i = 0; i < N; ++i) idx[i] = i;
-    for (size_t i = 0; i < hamming_weight && i < N; ++i) {  // partial Fisher-Yates
-      std::uniform_int_distribution<size_t> d(i, N - 1);
-      std::swap(idx[i], idx[d(rng)]);
-      c[idx[i]] = (rng() & 1) ? 1 : -1;
-    }
-    return from_coeffs(c, basis);
+    RnsPoly p(basis);
+    check(rnt_sample_ternary(p.buf_, hamming_weight, draw_seed(rng), 0));
+    return p;
   }
   template <class Rng>
   static RnsPoly sample_gaussian(double std_dev, const BasisRef<N>& basis, Rng& rng) {
-    std::normal_distribution<double> d(0.0, std_dev);
-    std::vector<int64_t> c(N);
-    for (auto& x : c) x = (int64_t)std::llround(d(rng));
-    return from_coeffs(c, basis);
+    RnsPoly p(basis);
+    check(rnt_sample_gaussian(p.buf_, std_dev, draw_seed(rng), 0));
+    return p;
+  }
+  // sample_noise (poly.rs:471-477): Gaussian with std_dev = sqrt(variance)
+  template <class Rng>
+  static RnsPoly sample_noise(double variance, const BasisRef<N>& basis, Rng& rng) {
+    return sample_gaussian(std::sqrt(variance), basis, rng);
   }
 
  private:
+  template <size_t M>
+  friend class CkksEncoder;
   explicit RnsPoly(BasisRef<N> basis) : basis_(std::move(basis)) {
     check(rnt_buf_alloc(basis_->ctx(), 1, &buf_));
   }
+  template <class Rng>
+  static uint64_t draw_seed(Rng& rng) {
+    return std::uniform_int_distribution<uint64_t>()(rng);
+  }
+  void touch() { host_.reset(); }
   BasisRef<N> basis_;
   rnt_buf* buf_ = nullptr;
   mutable std::optional<std::vector<Channel>> host_;
+};
+
+// Plaintext (crypto/types.rs): an encoded polynomial, its scale and slot count.
+template <size_t N>
+struct Plaintext {
+  RnsPoly<N> poly;
+  uint32_t scale_bits;
+  size_t slots;
+};
+
+// CkksEncoder<DEGREE> (ckks_encoder.rs:32-157).  The canonical embedding
+// runs on the device (rnt_encode / rnt_decode: the O(N log N) special FFT
+// in f64) instead of the reference's O(N^2) Vandermonde sums.
+template <size_t N>
+class CkksEncoder {
+ public:
+  explicit CkksEncoder(uint32_t scale_bits) : scale_bits_(scale_bits) {
+    if (((size_t)1 << log2_exact(N)) != N) throw std::invalid_argument("CkksEncoder: DEGREE must be a power of two");
+    if (scale_bits == 0) throw std::invalid_argument("CkksEncoder: scale_bits must be positive");
+  }
+  double scale_factor() const { return std::ldexp(1.0, (int)scale_bits_); }
+  size_t max_slots() const { return N / 2; }
+
+  // encode (ckks_encoder.rs:65-82) / encode_complex (:85-99); more than N/2
+  // values is a panic in the reference, std::invalid_argument here
+  Plaintext<N> encode(const std::vector<double>& values, BasisRef<N> basis) const {
+    std::vector<std::complex<double>> c(values.begin(), values.end());
+    return encode_complex(c, std::move(basis), "encode");
+  }
+  Plaintext<N> encode_complex(const std::vector<std::complex<double>>& values, BasisRef<N> basis,
+                              const char* name = "encode_complex") const {
+    if (values.size() > N / 2)
+      throw std::invalid_argument(std::string(name) + ": " + std::to_string(values.size()) +
+                                  " values exceed max slots " + std::to_string(N / 2));
+    RnsPoly<N> p(std::move(basis));
+    check(rnt_encode(p.buf_, reinterpret_cast<const double*>(values.data()), values.size(), scale_bits_));
+    return Plaintext<N>{std::move(p), scale_bits_, values.size()};
+  }
+
+  // decode (:129-131) / decode_complex (:134-156)
+  std::vector<double> decode(const Plaintext<N>& pt) const {
+    std::vector<double> out;
+    for (const auto& z : decode_complex(pt)) out.push_back(z.real());
+    return out;
+  }
+  std::vector<std::complex<double>> decode_complex(const Plaintext<N>& pt) const {
+    std::vector<std::complex<double>> out(pt.slots);
+    check(rnt_decode(pt.poly.handle(), reinterpret_cast<double*>(out.data()), pt.slots, pt.scale_bits));
+    return out;
+  }
+
+ private:
+  uint32_t scale_bits_;
 };
 
 }  // namespace rns_ntt
