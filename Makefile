@@ -23,7 +23,7 @@ $(LIBDIR)/rnt_encode.o: $(CSRC)/rnt_encode.hip $(CSRC)/rnt_internal.hpp
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBDIR)/rnt_sample.o: $(CSRC)/rnt_sample.hip $(CSRC)/rnt_internal.hpp
+$(LIBDIR)/rnt_sample.o: $(CSRC)/rnt_sample.hip $(CSRC)/rnt_internal.hpp $(CSRC)/rnt_modarith.hpp
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

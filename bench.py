@@ -36,6 +36,7 @@ sys.path.insert(0, PKG)
 METRIC = "RNS-NTT poly-muls/sec (N=2^16, 16 primes) at 1/2/4/8 GPUs; % HBM roofline"
 CT_METRIC = "ct x ct -> relin -> rescale ciphertexts/sec (N=2^16, 16 primes, limb-sharded)"
 ROT_METRIC = "rotation key-switches/sec (N=2^17, 32 primes, power-of-two Galois offsets)"
+ENC_METRIC = "CKKS encode+decode round trips/sec (N=2^16, 16 primes, N/2 complex slots)"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); ~6.3 TB/s achievable
 
 
@@ -48,11 +49,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=("polymul", "ctmul", "rotate"), default="polymul")
+    p.add_argument("--workload", choices=("polymul", "ctmul", "rotate", "encode"), default="polymul")
     p.add_argument("--shard", choices=("limb", "batch"), default="limb")
     p.add_argument("--batch", type=int, default=256, help="poly-mul pairs per GPU per step")
     p.add_argument("--ct-batch", type=int, default=128, help="ciphertext pairs per GPU per step (ctmul)")
     p.add_argument("--rot-batch", type=int, default=8, help="ciphertexts per rotation (rotate)")
+    p.add_argument("--enc-batch", type=int, default=64, help="plaintexts per step (encode)")
     p.add_argument("--log-n", type=int, default=16)
     p.add_argument("--limbs", type=int, default=16)
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
@@ -171,8 +173,8 @@ def run_polymul(args, comm, world, rank, local_rank):
     comm.barrier()
     elapsed = comm.max(t1 - t0)
     kernels = {}
-    # whole-plane path (N=2^16, u32: plane_fwd + plane_mul) or the
-    # three-launch column/row/column path (any other shape, RNT_PLANE=0)
+    # the three-launch column/row/column path (default) or the opt-in
+    # whole-plane path (RNT_PLANE=1 at N=2^16 with u32 words)
     for k in ("plane_fwd", "plane_mul", "col_fwd", "row_mul", "col_inv"):
         cnt, ms = B.profile_read(k)
         if cnt:
@@ -414,6 +416,80 @@ def run_rotate(args, comm, world, rank, local_rank):
     }
 
 
+def run_encode(args, comm, world, rank, local_rank):
+    """CkksEncoder.encode_complex + decode_complex
+    (ckks_encoder.rs:85-156) of a batch of full-slot plaintexts through the
+    device special FFT (rnt_encode / rnt_decode).  Slot values start and end
+    on the host, so the wall rate includes their PCIe copies; the special-FFT
+    kernels are timed with HIP events for the roofline."""
+    import numpy as np
+
+    import rns_ntt as rn
+
+    n = 1 << args.log_n
+    L = args.limbs
+    mod = rn.generate_primes(31, L, n)
+    Bs = rn.RnsBasis(mod, n, device=local_rank)
+    B = args.enc_batch
+    rng = np.random.default_rng(3 + rank)
+    v = rng.uniform(-1, 1, (B, n // 2)) + 1j * rng.uniform(-1, 1, (B, n // 2))
+    scale = 40
+    enc = rn.CkksEncoder(n, scale)
+
+    def step():
+        return enc.decode_complex(enc.encode_complex(v, Bs))
+
+    for _ in range(args.warmup):
+        step()
+    Bs.sync()
+    comm.barrier()
+    Bs.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    Bs.sync()
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = comm.max(t1 - t0)
+    kernels = {}
+    for k in ("sfft", "crt", "import"):
+        cnt, ms = Bs.profile_read(k)
+        if cnt:
+            kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
+    Bs.profile_enable(False)
+    err = float(np.max(np.abs(out - v)))
+    # algorithmic bytes of one special-FFT launch (encode or decode of the
+    # batch): the N/2 complex slots (16 B) and the N i64 coefficients (8 B)
+    alg = B * (n // 2 * 16 + n * 8)
+    sf = kernels.get("sfft", {"avg_ms": float("nan")})
+    achieved = alg / (sf["avg_ms"] * 1e-3) / 1e9
+    return {
+        "metric": ENC_METRIC,
+        "value": B * args.steps * world / elapsed,
+        "unit": "round-trips/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded uniform complex slots in [-1, 1]^2)",
+        "config": {
+            "workload": f"encode_complex + decode_complex, N=2^{args.log_n}, L={L} x 31-bit primes, "
+                        f"{n // 2} slots, scale 2^{scale}, {B} plaintexts per step",
+            "parallelism": f"replicas x{world}",
+            "roundtrip_max_err": err,
+            "parity_spot_check": err < n / 2.0 ** scale,
+        },
+        "roofline": {"bound": "hbm", "kernel": "sfft", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_launch": alg, "kernels": kernels},
+        "cpu_baseline": None,
+    }
+
+
 def run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod):
     """Config 5 limb-sharded: each rank owns L/world limbs of a
     global batch of rot_batch * world ciphertexts and a [L][L_r][N] slice of
@@ -490,7 +566,8 @@ def main():
     from rns_ntt.dist import Comm
 
     comm = Comm.from_env()
-    run = {"polymul": run_polymul, "ctmul": run_ctmul, "rotate": run_rotate}[args.workload]
+    run = {"polymul": run_polymul, "ctmul": run_ctmul, "rotate": run_rotate,
+           "encode": run_encode}[args.workload]
     line = run(args, comm, world, rank, local_rank)
     if rank == 0:
         print(json.dumps(line), flush=True)

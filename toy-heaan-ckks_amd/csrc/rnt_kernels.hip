@@ -1116,26 +1116,13 @@ k_import(W* __restrict__ dst, const uint64_t* __restrict__ stage, TabPtrs<W> tp,
 template <class W>
 __global__ void __launch_bounds__(256)
 k_import_coeffs(W* __restrict__ dst, const int64_t* __restrict__ coeffs, TabPtrs<W> tp,
-                uint32_t log_n, uint32_t L, uint32_t B, uint64_t ls, uint64_t total) {
+                uint32_t L, uint64_t ls, uint64_t total) {
+  // one thread per coefficient ([B][N] = the [L][B][N] offset within a
+  // limb): read it once, write its residue into every limb
   const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;  // total = L * B * N, order [L][B][N]
-  const uint64_t N = 1ull << log_n;
-  const uint64_t k = gid & (N - 1);
-  const uint64_t lp = gid >> log_n;
-  const uint32_t l = (uint32_t)(lp / B);
-  const uint64_t p = lp - (uint64_t)l * B;
-  const int64_t c = coeffs[p * N + k];
-  const uint64_t q = (uint64_t)tp.lc[l].q;
-  uint64_t v;
-  if (c >= 0) {
-    v = (uint64_t)c % q;
-  } else {
-    // rem_euclid: |c| <= 2^63
-    const uint64_t m = (uint64_t)(-(c + 1)) + 1u;  // |c| without overflow
-    const uint64_t r = m % q;
-    v = r == 0 ? 0 : q - r;
-  }
-  dst[(uint64_t)l * ls + p * N + k] = (W)v;
+  if (gid >= total) return;
+  const int64_t c = coeffs[gid];
+  for (uint32_t l = 0; l < L; ++l) dst[(uint64_t)l * ls + gid] = rem_euclid<W>(c, tp.lc[l]);
 }
 
 template <class W>
@@ -1417,12 +1404,10 @@ static hipError_t import_t(const Launch& k, void* dst, const uint64_t* stage, in
 
 template <class W>
 static hipError_t import_coeffs_t(const Launch& k, void* dst, const int64_t* stage) {
-  const uint64_t total = ((uint64_t)k.B * k.L) << k.t->log_n;
-  if (total == 0) return hipSuccess;
-  const uint64_t ls = (uint64_t)k.B << k.t->log_n;
+  const uint64_t total = (uint64_t)k.B << k.t->log_n;
+  if (total == 0 || k.L == 0) return hipSuccess;
   hipLaunchKernelGGL((k_import_coeffs<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,
-                     (W*)dst, stage, tab_ptrs<W>(k.t), k.t->log_n, (uint32_t)k.L, (uint32_t)k.B,
-                     ls, total);
+                     (W*)dst, stage, tab_ptrs<W>(k.t), (uint32_t)k.L, total, total);
   return hipGetLastError();
 }
 

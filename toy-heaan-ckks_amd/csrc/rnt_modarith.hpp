@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "rnt_internal.hpp"
+
 namespace rnt {
 
 __host__ __device__ __forceinline__ uint32_t mulhi(uint32_t a, uint32_t b) {
@@ -184,6 +186,29 @@ __device__ __forceinline__ void gs_bfly(W& x, W& y, W w, W wp, const Mod<W>& m) 
   const W u = x, v = y;
   x = add_mod<W>(u, v, m.q);
   y = shoup_mul<W>(u - v + m.q, w, wp, m);  // u - v + q in (0, 2q): any x < 2^w is fine
+}
+
+// m mod q for a 64-bit magnitude m, canonical.  The 32-bit path splits m
+// into halves, hi * (2^32 mod q) + lo, each reduced by a Shoup product, so
+// there is no 64-bit division (a long software sequence on the device); the
+// 64-bit path uses %.
+template <class W>
+__device__ __forceinline__ W mag_mod(uint64_t m, const LimbConst<W>& lc) {
+  if constexpr (sizeof(W) == 4) {
+    const uint32_t a = shoup_mul<uint32_t>((uint32_t)(m >> 32), lc.rmod, lc.rmod_p, lc.q);
+    const uint32_t b = shoup_mul<uint32_t>((uint32_t)m, 1u, lc.one_p, lc.q);
+    return add_mod<uint32_t>(a, b, lc.q);
+  } else {
+    return (W)(m % (uint64_t)lc.q);
+  }
+}
+
+// c.rem_euclid(q) (from_coeffs, poly.rs:55-61), |c| <= 2^63.
+template <class W>
+__device__ __forceinline__ W rem_euclid(int64_t c, const LimbConst<W>& lc) {
+  if (c >= 0) return mag_mod<W>((uint64_t)c, lc);
+  const W r = mag_mod<W>((uint64_t)(-(c + 1)) + 1u, lc);  // |c| without overflow
+  return r == 0 ? (W)0 : (W)(lc.q - r);
 }
 
 }  // namespace rnt

@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include "rnt_internal.hpp"
+#include "rnt_modarith.hpp"
 
 namespace rnt {
 
@@ -60,12 +61,6 @@ __device__ __forceinline__ uint4 draw(const SampleKey& s, uint32_t index, uint32
 __device__ __forceinline__ uint64_t lo64(uint4 v) { return (uint64_t)v.x | ((uint64_t)v.y << 32); }
 __device__ __forceinline__ uint64_t hi64(uint4 v) { return (uint64_t)v.z | ((uint64_t)v.w << 32); }
 
-__device__ __forceinline__ uint64_t reduce_i64(int64_t c, uint64_t q) {
-  if (c >= 0) return (uint64_t)c % q;
-  const uint64_t r = ((uint64_t)(-(c + 1)) + 1u) % q;  // |c| without overflow
-  return r == 0 ? 0 : q - r;
-}
-
 template <class W>
 __global__ void __launch_bounds__(256)
 k_sample_uniform(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, SampleKey s,
@@ -77,7 +72,7 @@ k_sample_uniform(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, Sampl
   const uint32_t l = (uint32_t)(lp / B);
   const uint32_t p = (uint32_t)(lp - (uint64_t)l * B);
   const uint64_t q = (uint64_t)lc[l].q;
-  const uint64_t rem = (0 - q) % q;  // 2^64 mod q
+  const uint64_t rem = (uint64_t)mag_mod<W>(0 - q, lc[l]);  // 2^64 mod q = (2^64 - q) mod q
   const uint64_t lim = 0 - rem;      // accept x < 2^64 - rem (all x when rem == 0)
   uint64_t x = 0;
   for (uint32_t att = 0; att < 16; ++att) {  // a miss has probability < q / 2^64 per draw
@@ -87,7 +82,7 @@ k_sample_uniform(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, Sampl
     x = hi64(v);
     if (x < lim) break;  // (rem != 0 here)
   }
-  out[gid] = (W)(x % q);
+  out[gid] = mag_mod<W>(x, lc[l]);
 }
 
 // f64::round (ties away from zero), then `as i64`.
@@ -111,7 +106,7 @@ k_sample_gaussian(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, Samp
   const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2) * sigma;
   const int64_t e = round_away(z);
   const uint64_t ls = (uint64_t)B << log_n;
-  for (uint32_t l = 0; l < L; ++l) out[l * ls + gid] = (W)reduce_i64(e, (uint64_t)lc[l].q);
+  for (uint32_t l = 0; l < L; ++l) out[l * ls + gid] = rem_euclid<W>(e, lc[l]);
 }
 
 constexpr uint32_t kTernThreads = 1024;
@@ -158,7 +153,7 @@ k_sample_ternary(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, Sampl
     if (h > 0 && tern_key(s, i, p) <= prefix)
       c = (draw(s, i, 0, p, 0, kDrawTernSign).x & 1u) ? 1 : -1;
     const uint64_t off = (uint64_t)p * N + i;
-    for (uint32_t l = 0; l < L; ++l) out[l * ls + off] = (W)reduce_i64(c, (uint64_t)lc[l].q);
+    for (uint32_t l = 0; l < L; ++l) out[l * ls + off] = rem_euclid<W>(c, lc[l]);
   }
 }
 
