@@ -205,6 +205,8 @@ rnt::Tables::~Tables() {
   }
 }
 
+static long env_long(const char* name, long dflt);
+
 // ---------------------------------------------------------------------------
 // diagnostics
 // ---------------------------------------------------------------------------
@@ -381,7 +383,7 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     return fail(RNT_ERR_INVALID_DEGREE, "ring degree 2^%u exceeds this backend's maximum 2^%d",
                 log_n, rnt::kMaxLogN);
   const uint64_t n = 1ull << log_n;
-  bool wide = false;
+  bool wide = false, lazy30 = true;
   for (size_t i = 0; i < count; ++i) {
     if (!rnt::host::is_ntt_friendly(moduli[i], n))
       return fail(RNT_ERR_NON_NTT_FRIENDLY,
@@ -390,6 +392,7 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
       return fail(RNT_ERR_BAD_ARGUMENT,
                   "modulus %" PRIu64 " >= 2^63 (the reference's add_mod overflows)", moduli[i]);
     if (moduli[i] >= (1ull << 31)) wide = true;
+    if (moduli[i] >= (1ull << 30)) lazy30 = false;
   }
   try {
     int ndev = 0;
@@ -400,6 +403,8 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     auto t = std::make_shared<rnt::Tables>();
     t->device = device;
     t->wide = wide ? 1 : 0;
+    // RNT_LAZY30=0 keeps the canonical product path for 30-bit bases (A/B)
+    t->lazy30 = !wide && lazy30 && env_long("RNT_LAZY30", 1) != 0;
     t->log_n = log_n;
     t->n = (size_t)n;
     t->L = count;
@@ -799,17 +804,18 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
       char* s0 = (char*)out->ws + (size_t)si * scratch_words * wb;
       char* s1 = s0 + scratch_words / 2 * wb;
       const uint64_t sls = (uint64_t)kc.B * n;
-      LAUNCH_ON(kc.t, kc.s, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, s0, pa, s1, pb, ls, sls),
+      LAUNCH_ON(kc.t, kc.s, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, s0, pa, s1, pb, ls, sls, true),
                 "column forward");
-      LAUNCH_ON(kc.t, kc.s, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, s0, s1, sls), "row mul");
-      LAUNCH_ON(kc.t, kc.s, rnt::K_COL_INV, rnt::launch_col_inv(kc, o, ls, s0, sls, 1, nullptr),
+      LAUNCH_ON(kc.t, kc.s, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, s0, s1, sls, true), "row mul");
+      LAUNCH_ON(kc.t, kc.s, rnt::K_COL_INV, rnt::launch_col_inv(kc, o, ls, s0, sls, 1, nullptr, true),
                 "column inverse");
       continue;
     }
-    LAUNCH_ON(kc.t, kc.s, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, o, pa, w, pb, ls, ls),
+    // lazy: the Harvey 30-bit variant when every q < 2^30 (Tables::lazy30)
+    LAUNCH_ON(kc.t, kc.s, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, o, pa, w, pb, ls, ls, true),
               "column forward");
-    LAUNCH_ON(kc.t, kc.s, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, o, w, ls), "row mul");
-    LAUNCH_ON(kc.t, kc.s, rnt::K_COL_INV, rnt::launch_col_inv(kc, o, ls, o, ls, 1, nullptr),
+    LAUNCH_ON(kc.t, kc.s, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, o, w, ls, true), "row mul");
+    LAUNCH_ON(kc.t, kc.s, rnt::K_COL_INV, rnt::launch_col_inv(kc, o, ls, o, ls, 1, nullptr, true),
               "column inverse");
   }
   if (plan.streams > 1) HIP_TRY(aux_join(tm, plan.streams), "stream join");

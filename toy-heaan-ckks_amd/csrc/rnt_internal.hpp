@@ -81,6 +81,7 @@ struct CrtDev {
 struct Tables {
   int device = 0;
   int wide = 0;            // 0: W = u32, 1: W = u64
+  bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path
   uint32_t log_n = 0;
   size_t n = 0;
   size_t L = 0;            // channel count of the root basis
@@ -184,15 +185,20 @@ struct Launch {
 // All arrays are [limb][poly][N] with an explicit limb stride `*_ls` (words);
 // k.B polys (a batch or a chunk of one) and k.L limbs are processed.
 // Forward column pass on up to two operands (in0->out0, in1->out1).
+// lazy (all three): the product path's Harvey-lazy 30-bit variant (q < 2^30,
+// see rnt_modarith.hpp Mod30) where lazy30_ok(); the intermediates between
+// the three launches are then unreduced, the product's output canonical.
+bool lazy30_ok(const Tables* t);
 hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* out1,
-                          const void* in1, uint64_t in_ls, uint64_t out_ls);
+                          const void* in1, uint64_t in_ls, uint64_t out_ls, bool lazy = false);
 // Row pass.  mode 0: forward rows (in place on x); 1: inverse rows (in place
 // on x); 2: poly-mul rows: x <- INVrow(FWDrow(x) (.) FWDrow(y) * 2^-w).
-hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls);
+hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls,
+                      bool lazy = false);
 // Inverse column pass with n^-1 folded into the last stage; rfold adds the
 // Montgomery factor 2^w.  addend (optional, coefficient domain, out layout).
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
-                          uint64_t in_ls, int rfold, const void* addend);
+                          uint64_t in_ls, int rfold, const void* addend, bool lazy = false);
 // Whole-plane product path (rnt_plane.hip; u32 bases at N = 2^16):
 // bhat <- forward transform of b in a private order; out <- a * b.
 bool plane_supported(const Tables* t);

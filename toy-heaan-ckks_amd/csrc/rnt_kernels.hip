@@ -63,6 +63,19 @@ __device__ __forceinline__ Mod<W> mod_of(const LimbConst<W>& lc) {
   return Mod<W>{lc.q, (W)(W(0) - lc.q)};
 }
 
+// The product path's modulus bundle: LZ = Harvey-lazy 30-bit arithmetic
+// (rnt_modarith.hpp Mod30; u32 words and q < 2^30 only).
+template <class W, bool LZ>
+__device__ __forceinline__ auto mod_for(const LimbConst<W>& lc) {
+  static_assert(!LZ || sizeof(W) == 4, "lazy 30-bit arithmetic needs 32-bit words");
+  if constexpr (LZ) {
+    const uint32_t q = (uint32_t)lc.q;
+    return Mod30{q, 0u - q, 2u * q};
+  } else {
+    return mod_of(lc);
+  }
+}
+
 // Buffer-resource view of a wave-uniform base (a (limb, poly) plane or a
 // limb's twiddle table): loads/stores take a 32-bit per-lane element offset
 // plus a wave-uniform one that lands in the instruction's SGPR soffset, so
@@ -420,9 +433,9 @@ struct Fold {
 // CT stages on bits [BB, BB+K) for NOPS operands sharing twiddles.  `node0`
 // = heap index base of register 0: (heap root of this transform) * 2^LOGX +
 // its transform-local index, so stage s's node is node0 >> (s+1) + (i >> ...).
-template <class W, int NOPS, int LOGE, int K, int BB, class TS>
+template <class W, int NOPS, int LOGE, int K, int BB, class TS, class MO>
 __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0, const TS& tw,
-                                        const Mod<W>& mo) {
+                                        const MO& mo) {
   constexpr int E = 1 << LOGE;
 #pragma unroll
   for (int sl = K - 1; sl >= 0; --sl) {
@@ -443,9 +456,9 @@ __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0,
 #pragma unroll
       for (int o = 0; o < NOPS; ++o) {
         if (lazy)
-          ct_bfly_lazy<W>(x[o][i], x[o][i | d], t[m].w, t[m].p, mo);
+          ct_bfly_lazy(x[o][i], x[o][i | d], t[m].w, t[m].p, mo);
         else
-          ct_bfly<W>(x[o][i], x[o][i | d], t[m].w, t[m].p, mo);
+          ct_bfly(x[o][i], x[o][i | d], t[m].w, t[m].p, mo);
       }
     }
   }
@@ -453,10 +466,10 @@ __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0,
 
 // GS stages; with FOLD the transform's top stage (bit LOGX-1, distance N/2
 // of the whole network) applies the folded n^-1 constants instead.
-template <class W, int NOPS, int LOGE, int K, int BB, int LOGX, bool FOLD, class TS>
+template <class W, int NOPS, int LOGE, int K, int BB, int LOGX, bool FOLD, class TS, class MO>
 __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0, const TS& itw,
-                                        const Mod<W>& mo, const Fold<W>& f) {
-  const W q = mo.q;
+                                        const MO& mo, const Fold<W>& f) {
+  const W bias = gs_bias(mo);
   constexpr int E = 1 << LOGE;
 #pragma unroll
   for (int sl = 0; sl < K; ++sl) {
@@ -469,8 +482,8 @@ __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0,
 #pragma unroll
         for (int o = 0; o < NOPS; ++o) {
           const W u = x[o][i], v = x[o][i | d];
-          x[o][i] = shoup_mul<W>(u + v, f.c1, f.c1p, mo);
-          x[o][i | d] = shoup_mul<W>(u - v + q, f.c2, f.c2p, mo);
+          x[o][i] = shoup_mul(u + v, f.c1, f.c1p, mo);
+          x[o][i | d] = shoup_mul(u - v + bias, f.c2, f.c2p, mo);
         }
       }
       continue;
@@ -486,7 +499,7 @@ __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0,
       if (i & d) continue;
       const int m = i >> (sl + 1);
 #pragma unroll
-      for (int o = 0; o < NOPS; ++o) gs_bfly<W>(x[o][i], x[o][i | d], t[m].w, t[m].p, mo);
+      for (int o = 0; o < NOPS; ++o) gs_bfly(x[o][i], x[o][i | d], t[m].w, t[m].p, mo);
     }
   }
 }
@@ -546,17 +559,17 @@ struct XPos {
   uint32_t heap;
 };
 
-template <class G, class W, int NOPS, int PP, class TS>
+template <class G, class W, int NOPS, int PP, class TS, class MO>
 __device__ __forceinline__ void fwd_pass(W (&x)[NOPS][G::E], const XPos& xp, W* lds, const TS& tw,
-                                         const Mod<W>& q) {
+                                         const MO& q) {
   constexpr int BB = G::bb(PP);
   if constexpr (PP > 0) xchg<G, W, NOPS, G::bb(PP - 1), BB>(x, lds, xp.slot, xp.tau);
   pass_ct<W, NOPS, G::LOGE, G::k(PP), BB>(x, xp.heap + G::base(xp.tau, BB), tw, q);
 }
 
-template <class G, class W, int NOPS, int PP, bool FOLD, class TS>
+template <class G, class W, int NOPS, int PP, bool FOLD, class TS, class MO>
 __device__ __forceinline__ void inv_pass(W (&x)[NOPS][G::E], const XPos& xp, W* lds, const TS& itw,
-                                         const Mod<W>& q, const Fold<W>& f) {
+                                         const MO& q, const Fold<W>& f) {
   constexpr int BB = G::bb(PP);
   if constexpr (PP < G::P - 1) xchg<G, W, NOPS, G::bb(PP + 1), BB>(x, lds, xp.slot, xp.tau);
   pass_gs<W, NOPS, G::LOGE, G::k(PP), BB, G::LOGX_, FOLD>(x, xp.heap + G::base(xp.tau, BB), itw, q,
@@ -564,9 +577,9 @@ __device__ __forceinline__ void inv_pass(W (&x)[NOPS][G::E], const XPos& xp, W* 
 }
 
 // All forward passes (first-pass distribution in, last-pass out).
-template <class G, class W, int NOPS, class TS>
+template <class G, class W, int NOPS, class TS, class MO>
 __device__ __forceinline__ void xf_fwd(W (&x)[NOPS][G::E], const XPos& xp, W* lds, const TS& tw,
-                                       const Mod<W>& q) {
+                                       const MO& q) {
   if constexpr (G::P > 0) fwd_pass<G, W, NOPS, 0>(x, xp, lds, tw, q);
   if constexpr (G::P > 1) fwd_pass<G, W, NOPS, 1>(x, xp, lds, tw, q);
   if constexpr (G::P > 2) fwd_pass<G, W, NOPS, 2>(x, xp, lds, tw, q);
@@ -574,9 +587,9 @@ __device__ __forceinline__ void xf_fwd(W (&x)[NOPS][G::E], const XPos& xp, W* ld
 }
 
 // All inverse passes (last-pass distribution in, first-pass out).
-template <class G, class W, int NOPS, bool FOLD = false, class TS>
+template <class G, class W, int NOPS, bool FOLD = false, class TS, class MO>
 __device__ __forceinline__ void xf_inv(W (&x)[NOPS][G::E], const XPos& xp, W* lds, const TS& itw,
-                                       const Mod<W>& q, const Fold<W>& f = Fold<W>{}) {
+                                       const MO& q, const Fold<W>& f = Fold<W>{}) {
   if constexpr (G::P > 3) inv_pass<G, W, NOPS, 3, FOLD>(x, xp, lds, itw, q, f);
   if constexpr (G::P > 2) inv_pass<G, W, NOPS, 2, FOLD>(x, xp, lds, itw, q, f);
   if constexpr (G::P > 1) inv_pass<G, W, NOPS, 1, FOLD>(x, xp, lds, itw, q, f);
@@ -671,7 +684,7 @@ struct ColAddr {
   __device__ __forceinline__ void refresh() { asm volatile("" : "+s"(s)); }
 };
 
-template <class W, int LOG_R, int LOG_TC>
+template <class W, int LOG_R, int LOG_TC, bool LZ = false>
 __global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t log_n,
            uint32_t log_c, uint32_t B, uint64_t in_ls, uint64_t out_ls) {
@@ -686,7 +699,7 @@ k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t
   ColAddr<G, G::BB0> a0(cp, log_c);
   ColAddr<G, G::BBL> al(cp, log_c);
   const auto tw = col_twiddles<W, G::UNIFORM>(tp.tw + (uint64_t)cp.l * N, N);
-  const Mod<W> m = mod_of(tp.lc[cp.l]);
+  const auto m = mod_for<W, LZ>(tp.lc[cp.l]);  // LZ: outputs in [0, 4q)
   W x[1][E];
   const BufView<W> src(in0 + ip, N), dst(out0 + op, N);
   // operand 1 first: out0 may alias in1 (out = a * b with out == b).  With
@@ -719,7 +732,7 @@ k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t
   for (int i = 0; i < E; ++i) dst.st(x[0][i], al.v, i * al.s);
 }
 
-template <class W, int LOG_R, int LOG_TC>
+template <class W, int LOG_R, int LOG_TC, bool LZ = false>
 __global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, uint32_t log_c,
            uint32_t B, uint64_t in_ls, uint64_t out_ls, int rfold) {
@@ -741,7 +754,7 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
   W x[1][E];
 #pragma unroll
   for (int i = 0; i < E; ++i) x[0][i] = src.ld(al.v, i * al.s);
-  xf_inv<G, W, 1, true>(x, cp.xp, lds, itw, mod_of(lc), f);
+  xf_inv<G, W, 1, true>(x, cp.xp, lds, itw, mod_for<W, LZ>(lc), f);  // canonical out
   a0.refresh();
   if (addend != nullptr) {
     const BufView<W> ad(addend + op, N);
@@ -793,7 +806,7 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
 
 // mode 0: forward rows in place; 1: inverse rows in place;
 // 2: poly-mul rows: x <- INV(FWD(x) (.) FWD(y)) with Montgomery pointwise.
-template <class W, int MODE, int LOG_C>
+template <class W, int MODE, int LOG_C, bool LZ = false>
 __global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kRowMinWaves : 1)
 k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_n, uint32_t B,
       uint64_t ls, uint64_t rows_total) {
@@ -816,11 +829,24 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
       v[0][i] = xg[base + b0 + ((uint32_t)i << G::BB0)];
       v[1][i] = yg[base + b0 + ((uint32_t)i << G::BB0)];
     }
-    xf_fwd<G, W, 2>(v, rp.xp, lds, tw, mod_of(lc));
+    const auto mo = mod_for<W, LZ>(lc);
+    xf_fwd<G, W, 2>(v, rp.xp, lds, tw, mo);
     W z[1][E];
+    if constexpr (LZ) {
+      // [0, 4q) inputs -> [0, 2q); a b < 4q^2 < q 2^32, so the Montgomery
+      // quotient leaves (ab + mq) / 2^32 < 2q: the GS passes' input range
 #pragma unroll
-    for (int i = 0; i < E; ++i) z[0][i] = mont_mul<W>(v[0][i], v[1][i], lc.q, lc.qinv);
-    xf_inv<G, W, 1>(z, rp.xp, lds, itw, mod_of(lc));
+      for (int i = 0; i < E; ++i) {
+        const uint32_t a = csub<uint32_t>(v[0][i], mo.q2), b = csub<uint32_t>(v[1][i], mo.q2);
+        const uint64_t t = mul64(a, b);
+        const uint32_t mm = (uint32_t)t * (0u - (uint32_t)lc.qinv);
+        z[0][i] = (uint32_t)(mad64(mm, (uint32_t)lc.q, t) >> 32);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < E; ++i) z[0][i] = mont_mul<W>(v[0][i], v[1][i], lc.q, lc.qinv);
+    }
+    xf_inv<G, W, 1>(z, rp.xp, lds, itw, mo);
     if (rp.active) {
 #pragma unroll
       for (int i = 0; i < E; ++i) xg[base + b0 + ((uint32_t)i << G::BB0)] = z[0][i];
@@ -1210,7 +1236,7 @@ static dim3 col_grid(const Launch& k, const Geom& g, uint32_t y, uint32_t z) {
   return dim3((unsigned)x, y, z);
 }
 
-template <class W>
+template <class W, bool LZ>
 static hipError_t col_fwd_t(const Launch& k, void* out0, const void* in0, void* out1,
                             const void* in1, uint64_t in_ls, uint64_t out_ls) {
   const Geom g = geom_for(k.t->log_n);
@@ -1221,9 +1247,9 @@ static hipError_t col_fwd_t(const Launch& k, void* out0, const void* in0, void* 
     if (grid.x == 0) return hipErrorInvalidConfiguration;
     hipError_t e = hipSuccess;
 #define RNT_L2(R, TC)                                                                           \
-  e = allow_lds(k_colt_fwd<W, R, TC>, col_lds<W, R, TC>());                                     \
+  e = allow_lds(k_colt_fwd<W, R, TC, LZ>, col_lds<W, R, TC>());                                 \
   if (e != hipSuccess) return e;                                                                \
-  hipLaunchKernelGGL((k_colt_fwd<W, R, TC>), grid, dim3(ColGeo<R, TC>::THREADS),                \
+  hipLaunchKernelGGL((k_colt_fwd<W, R, TC, LZ>), grid, dim3(ColGeo<R, TC>::THREADS),                \
                      (col_lds<W, R, TC>()), k.s, (W*)out0, (const W*)in0, (W*)out1, (const W*)in1, \
                      tp, g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls)
 #define RNT_L(R)                          \
@@ -1247,7 +1273,7 @@ static hipError_t col_fwd_t(const Launch& k, void* out0, const void* in0, void* 
   return hipGetLastError();
 }
 
-template <class W>
+template <class W, bool LZ>
 static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const void* in,
                             uint64_t in_ls, int rfold, const void* addend) {
   const Geom g = geom_for(k.t->log_n);
@@ -1258,9 +1284,9 @@ static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const v
     if (grid.x == 0) return hipErrorInvalidConfiguration;
     hipError_t e = hipSuccess;
 #define RNT_L2(R, TC)                                                                        \
-  e = allow_lds(k_colt_inv<W, R, TC>, col_lds<W, R, TC>());                                  \
+  e = allow_lds(k_colt_inv<W, R, TC, LZ>, col_lds<W, R, TC>());                              \
   if (e != hipSuccess) return e;                                                             \
-  hipLaunchKernelGGL((k_colt_inv<W, R, TC>), grid, dim3(ColGeo<R, TC>::THREADS),             \
+  hipLaunchKernelGGL((k_colt_inv<W, R, TC, LZ>), grid, dim3(ColGeo<R, TC>::THREADS),             \
                      (col_lds<W, R, TC>()), k.s, (W*)out, (const W*)in, (const W*)addend, tp, \
                      g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls, rfold)
 #define RNT_L(R)                          \
@@ -1284,7 +1310,7 @@ static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const v
   return hipGetLastError();
 }
 
-template <class W, int MODE, int LOG_C>
+template <class W, int MODE, int LOG_C, bool LZ = false>
 static hipError_t row_launch(const Launch& k, void* x, const void* y, uint64_t ls) {
   using G = RowGeo<LOG_C>;
   const Geom g = geom_for(k.t->log_n);
@@ -1292,19 +1318,25 @@ static hipError_t row_launch(const Launch& k, void* x, const void* y, uint64_t l
   if (rows == 0) return hipSuccess;
   const unsigned blocks = (unsigned)((rows + G::RPW - 1) / G::RPW);
   const size_t lds = row_lds<W, LOG_C>(MODE == 2 ? 2 : 1);
-  hipError_t e = allow_lds(k_row<W, MODE, LOG_C>, lds);
+  hipError_t e = allow_lds(k_row<W, MODE, LOG_C, LZ>, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_row<W, MODE, LOG_C>), dim3(blocks), dim3(G::THREADS), lds, k.s, (W*)x,
+  hipLaunchKernelGGL((k_row<W, MODE, LOG_C, LZ>), dim3(blocks), dim3(G::THREADS), lds, k.s, (W*)x,
                      (const W*)y, tab_ptrs<W>(k.t), g.log_n, (uint32_t)k.B, ls, rows);
   return hipGetLastError();
 }
 
 template <class W>
-static hipError_t row_t(const Launch& k, int mode, void* x, const void* y, uint64_t ls) {
+static hipError_t row_t(const Launch& k, int mode, void* x, const void* y, uint64_t ls, bool lz) {
   const Geom g = geom_for(k.t->log_n);
 #define RNT_L0(C) return row_launch<W, 0, C>(k, x, y, ls)
 #define RNT_L1(C) return row_launch<W, 1, C>(k, x, y, ls)
 #define RNT_L2(C) return row_launch<W, 2, C>(k, x, y, ls)
+#define RNT_L2Z(C) return row_launch<W, 2, C, true>(k, x, y, ls)
+  if constexpr (sizeof(W) == 4) {
+    if (mode == 2 && lz) {
+      RNT_DISPATCH_LOGC(g.log_c, RNT_L2Z)
+    }
+  }
   if (mode == 0) {
     RNT_DISPATCH_LOGC(g.log_c, RNT_L0)
   } else if (mode == 1) {
@@ -1315,6 +1347,7 @@ static hipError_t row_t(const Launch& k, int mode, void* x, const void* y, uint6
 #undef RNT_L0
 #undef RNT_L1
 #undef RNT_L2
+#undef RNT_L2Z
   return hipErrorInvalidValue;
 }
 
@@ -1522,18 +1555,26 @@ static hipError_t tensor_rows_t(const Launch& k, void* d0hat, void* d1hat, void*
 // W dispatch -----------------------------------------------------------------
 #define RNT_WIDE(CALL32, CALL64) return k.t->wide ? (CALL64) : (CALL32)
 
-hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* out1,
-                          const void* in1, uint64_t in_ls, uint64_t out_ls) {
-  RNT_WIDE(col_fwd_t<uint32_t>(k, out0, in0, out1, in1, in_ls, out_ls),
-           col_fwd_t<uint64_t>(k, out0, in0, out1, in1, in_ls, out_ls));
+bool lazy30_ok(const Tables* t) {
+  return !t->wide && t->lazy30 && geom_for(t->log_n).log_r >= 5;
 }
-hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls) {
-  RNT_WIDE(row_t<uint32_t>(k, mode, x, y, ls), row_t<uint64_t>(k, mode, x, y, ls));
+hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* out1,
+                          const void* in1, uint64_t in_ls, uint64_t out_ls, bool lazy) {
+  if (lazy && lazy30_ok(k.t))
+    return col_fwd_t<uint32_t, true>(k, out0, in0, out1, in1, in_ls, out_ls);
+  RNT_WIDE((col_fwd_t<uint32_t, false>(k, out0, in0, out1, in1, in_ls, out_ls)),
+           (col_fwd_t<uint64_t, false>(k, out0, in0, out1, in1, in_ls, out_ls)));
+}
+hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls, bool lazy) {
+  const bool lz = lazy && lazy30_ok(k.t);
+  RNT_WIDE(row_t<uint32_t>(k, mode, x, y, ls, lz), row_t<uint64_t>(k, mode, x, y, ls, false));
 }
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
-                          uint64_t in_ls, int rfold, const void* addend) {
-  RNT_WIDE(col_inv_t<uint32_t>(k, out, out_ls, in, in_ls, rfold, addend),
-           col_inv_t<uint64_t>(k, out, out_ls, in, in_ls, rfold, addend));
+                          uint64_t in_ls, int rfold, const void* addend, bool lazy) {
+  if (lazy && lazy30_ok(k.t))
+    return col_inv_t<uint32_t, true>(k, out, out_ls, in, in_ls, rfold, addend);
+  RNT_WIDE((col_inv_t<uint32_t, false>(k, out, out_ls, in, in_ls, rfold, addend)),
+           (col_inv_t<uint64_t, false>(k, out, out_ls, in, in_ls, rfold, addend)));
 }
 hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a, const void* b) {
   RNT_WIDE(elementwise_t<uint32_t>(k, op, out, a, b), elementwise_t<uint64_t>(k, op, out, a, b));

@@ -188,6 +188,47 @@ __device__ __forceinline__ void gs_bfly(W& x, W& y, W w, W wp, const Mod<W>& m) 
   y = shoup_mul<W>(u - v + m.q, w, wp, m);  // u - v + q in (0, 2q): any x < 2^w is fine
 }
 
+// ---- 30-bit moduli: Harvey's lazy butterflies -----------------------------
+// With q < 2^30, 4q < 2^32 leaves two bits of headroom (31-bit primes leave
+// one), so the product path keeps values unreduced (Harvey 2014, Alg. 4/5):
+// forward CT values live in [0, 4q), inverse GS values in [0, 2q), and only
+// the one reduction that keeps a sum below 4q remains per butterfly.  The
+// reference's own examples use 30-bit bases (rotation_demo.rs,
+// rotation_stress.rs).  Outputs at the product's end are canonical again.
+struct Mod30 {
+  uint32_t q;   // modulus, < 2^30
+  uint32_t nq;  // 2^32 - q
+  uint32_t q2;  // 2q
+};
+
+// CT: x in [0, 4q), any y < 2^32 -> both outputs in [0, 4q).
+__device__ __forceinline__ void ct_bfly(uint32_t& x, uint32_t& y, uint32_t w, uint32_t wp,
+                                        const Mod30& m) {
+  const uint32_t t = shoup_lazy(y, w, wp, Mod<uint32_t>{m.q, m.nq});  // [0, 2q)
+  const uint32_t u = csub<uint32_t>(x, m.q2);                          // [0, 2q)
+  x = u + t;
+  y = u + (m.q2 - t);
+}
+__device__ __forceinline__ void ct_bfly_lazy(uint32_t& x, uint32_t& y, uint32_t w, uint32_t wp,
+                                             const Mod30& m) {
+  ct_bfly(x, y, w, wp, m);
+}
+// GS: u, v in [0, 2q) -> (u + v) in [0, 2q), (u - v) w in [0, 2q).
+__device__ __forceinline__ void gs_bfly(uint32_t& x, uint32_t& y, uint32_t w, uint32_t wp,
+                                        const Mod30& m) {
+  const uint32_t u = x, v = y;
+  x = csub<uint32_t>(u + v, m.q2);
+  y = shoup_lazy(u - v + m.q2, w, wp, Mod<uint32_t>{m.q, m.nq});
+}
+// Canonical Shoup product of any x < 2^32 (the inverse's folded last stage).
+__device__ __forceinline__ uint32_t shoup_mul(uint32_t x, uint32_t w, uint32_t wp, const Mod30& m) {
+  return csub<uint32_t>(shoup_lazy(x, w, wp, Mod<uint32_t>{m.q, m.nq}), m.q);
+}
+// What the GS difference u - v is biased by to stay non-negative.
+template <class W>
+__device__ __forceinline__ W gs_bias(const Mod<W>& m) { return m.q; }   // u, v in [0, q)
+__device__ __forceinline__ uint32_t gs_bias(const Mod30& m) { return m.q2; }  // u, v in [0, 2q)
+
 // m mod q for a 64-bit magnitude m, canonical.  The 32-bit path splits m
 // into halves, hi * (2^32 mod q) + lo, each reduced by a Shoup product, so
 // there is no 64-bit division (a long software sequence on the device); the
