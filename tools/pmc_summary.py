@@ -14,8 +14,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-NAMES = {"k_colt_fwd<unsigned int, 8, 6>": "col_fwd", "k_row<unsigned int, 2, 8>": "row_mul",
-         "k_colt_inv<unsigned int, 8, 6>": "col_inv"}
+NAMES = {"k_colt_fwd<unsigned int, 8, 6, false>": "col_fwd", "k_row<unsigned int, 2, 8, false>": "row_mul",
+         "k_colt_inv<unsigned int, 8, 6, false>": "col_inv"}
 
 
 def short(kname):
