@@ -29,7 +29,11 @@ namespace rnt {
 
 constexpr int kMaxLogN = 17;
 constexpr int kRowElems = 16;  // elements per thread per operand in the row pass
-constexpr int kRowThreads = 256;
+// threads per row-pass workgroup (at least one row's C/16 threads)
+#ifndef RNT_ROW_THREADS
+#define RNT_ROW_THREADS 256
+#endif
+constexpr int kRowThreads = RNT_ROW_THREADS;
 
 template <class W>
 struct LimbConst {
