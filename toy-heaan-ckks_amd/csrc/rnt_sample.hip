@@ -85,10 +85,12 @@ k_sample_uniform(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, Sampl
   out[gid] = mag_mod<W>(x, lc[l]);
 }
 
-// f64::round (ties away from zero), then `as i64`.
+// f64::round (ties away from zero), then `as i64` (saturating).
 __device__ __forceinline__ int64_t round_away(double z) {
   double r = trunc(z);
   if (fabs(z - r) >= 0.5) r += copysign(1.0, z);
+  if (r >= 9223372036854775807.0) return INT64_MAX;
+  if (r <= -9223372036854775808.0) return INT64_MIN;
   return (int64_t)r;
 }
 
