@@ -328,19 +328,24 @@ k_ks_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32
 // threads x E registers.  Passes run from the top bits down: full radix-16
 // passes on bits [bb, bb+4), then (if LOGX % 4) a partial pass on bits
 // [0, REM) with register bits [0, 4).  LOGX < 4: one thread holds it all.
+// LOGX = 9 (the N = 2^17 rows) may instead run three radix-8 passes (3+3+3
+// rather than 4+4+1, whose last exchange buys a single stage).
+#ifndef RNT_ROW_RADIX8
+#define RNT_ROW_RADIX8 0
+#endif
 template <int LOGX>
 struct PassSched {
   static constexpr int LOGX_ = LOGX;
-  static constexpr int LOGE = LOGX >= 4 ? 4 : LOGX;
+  static constexpr int LOGE = LOGX < 4 ? LOGX : (RNT_ROW_RADIX8 && LOGX == 9) ? 3 : 4;
   static constexpr int E = 1 << LOGE;
   static constexpr int LOG_T = LOGX - LOGE;
   static constexpr int T = 1 << LOG_T;
   static constexpr int X = 1 << LOGX;
-  static constexpr int FULL = LOGE == 4 ? LOGX / 4 : 0;
-  static constexpr int REM = LOGE == 4 ? LOGX % 4 : LOGX;
+  static constexpr int FULL = LOGX >= 4 ? LOGX / LOGE : 0;
+  static constexpr int REM = LOGX >= 4 ? LOGX % LOGE : LOGX;
   static constexpr int P = FULL + (REM ? 1 : 0);
-  static constexpr int bb(int p) { return (p >= 0 && p < FULL) ? LOGX - 4 * (p + 1) : 0; }
-  static constexpr int k(int p) { return p < FULL ? 4 : REM; }
+  static constexpr int bb(int p) { return (p >= 0 && p < FULL) ? LOGX - LOGE * (p + 1) : 0; }
+  static constexpr int k(int p) { return p < FULL ? LOGE : REM; }
   static constexpr int BB0 = bb(0);
   static constexpr int BBL = bb(P - 1);
   // transform-local index of register i in the distribution with register
@@ -359,17 +364,19 @@ struct RowGeo : PassSched<LOG_C> {
   using S = PassSched<LOG_C>;
   static constexpr int LOGC = LOG_C;
   static constexpr int C = 1 << LOG_C;
-  static constexpr int PADC = C + (C >> 4);
+  // one pad word per 2^PADSH: 16 (radix-16 passes) or 8 (radix-8)
+  static constexpr int PADSH = S::LOGE == 3 ? 3 : 4;
+  static constexpr int PADC = C + (C >> PADSH);
   static constexpr int THREADS = S::T > kRowThreads ? S::T : kRowThreads;
   static constexpr int RPW = THREADS / S::T;  // rows per workgroup
   static constexpr int REGION = RPW * PADC;   // LDS words per operand
   __device__ static __forceinline__ uint32_t slot_of(uint32_t tid) { return tid >> S::LOG_T; }
   __device__ static __forceinline__ uint32_t tau_of(uint32_t tid) { return tid & (S::T - 1); }
   __device__ static __forceinline__ uint32_t lds_off(uint32_t slot, uint32_t j) {
-    return slot * PADC + j + (j >> 4);
+    return slot * PADC + j + (j >> PADSH);
   }
   static constexpr uint32_t lds_ioff(int i, int b) {
-    return ((uint32_t)i << b) + (((uint32_t)i << b) >> 4);
+    return ((uint32_t)i << b) + (((uint32_t)i << b) >> PADSH);
   }
 };
 
