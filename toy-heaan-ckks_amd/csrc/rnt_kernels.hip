@@ -80,6 +80,14 @@ __device__ __forceinline__ auto mod_for(const LimbConst<W>& lc) {
 // limb's twiddle table): loads/stores take a 32-bit per-lane element offset
 // plus a wave-uniform one that lands in the instruction's SGPR soffset, so
 // strided column access costs no VALU address arithmetic.
+// Cache-policy bits (`aux`) of the plane loads and stores; the planes are
+// streamed once per launch (2 = nt).
+#ifndef RNT_BUF_LD_AUX
+#define RNT_BUF_LD_AUX 0
+#endif
+#ifndef RNT_BUF_ST_AUX
+#define RNT_BUF_ST_AUX 0
+#endif
 template <class W>
 struct BufView {
   __amdgpu_buffer_rsrc_t r;
@@ -87,23 +95,23 @@ struct BufView {
       : r(__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(elems * sizeof(W)), 0x00020000)) {}
   __device__ __forceinline__ W ld(uint32_t v, uint32_t s) const {
     if constexpr (sizeof(W) == 4) {
-      return __builtin_amdgcn_raw_buffer_load_b32(r, v * 4u, s * 4u, 0);
+      return __builtin_amdgcn_raw_buffer_load_b32(r, v * 4u, s * 4u, RNT_BUF_LD_AUX);
     } else {
-      return __builtin_bit_cast(W, __builtin_amdgcn_raw_buffer_load_b64(r, v * 8u, s * 8u, 0));
+      return __builtin_bit_cast(W, __builtin_amdgcn_raw_buffer_load_b64(r, v * 8u, s * 8u, RNT_BUF_LD_AUX));
     }
   }
   // four consecutive words (the compiler does not merge the raw buffer
   // builtins into wide loads by itself)
   __device__ __forceinline__ void ld4(W (&o)[4], uint32_t v, uint32_t s) const {
     if constexpr (sizeof(W) == 4) {
-      const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, v * 4u, s * 4u, 0);
+      const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, v * 4u, s * 4u, RNT_BUF_LD_AUX);
       o[0] = q[0];
       o[1] = q[1];
       o[2] = q[2];
       o[3] = q[3];
     } else {
-      const auto a = __builtin_amdgcn_raw_buffer_load_b128(r, v * 8u, s * 8u, 0);
-      const auto b = __builtin_amdgcn_raw_buffer_load_b128(r, v * 8u + 16u, s * 8u, 0);
+      const auto a = __builtin_amdgcn_raw_buffer_load_b128(r, v * 8u, s * 8u, RNT_BUF_LD_AUX);
+      const auto b = __builtin_amdgcn_raw_buffer_load_b128(r, v * 8u + 16u, s * 8u, RNT_BUF_LD_AUX);
       o[0] = (uint64_t)a[0] | ((uint64_t)a[1] << 32);
       o[1] = (uint64_t)a[2] | ((uint64_t)a[3] << 32);
       o[2] = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
@@ -112,10 +120,10 @@ struct BufView {
   }
   __device__ __forceinline__ void st(W x, uint32_t v, uint32_t s) const {
     if constexpr (sizeof(W) == 4) {
-      __builtin_amdgcn_raw_buffer_store_b32(x, r, v * 4u, s * 4u, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(x, r, v * 4u, s * 4u, RNT_BUF_ST_AUX);
     } else {
       using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, x), r, v * 8u, s * 8u, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, x), r, v * 8u, s * 8u, RNT_BUF_ST_AUX);
     }
   }
 };
