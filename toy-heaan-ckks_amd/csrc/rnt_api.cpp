@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -103,17 +104,116 @@ int set_device(const rnt_ctx* ctx) {
   return RNT_OK;
 }
 
+// Workspace blocks of freed buffers, kept per device for reuse.  A caller
+// that makes fresh output buffers every step (the limb-sharded pipeline)
+// then reuses the same gigabytes of key-switch scratch instead of a
+// hipMalloc / hipFree of them per call; that churn made a long ct-mul run
+// fall to ~1/15 of its rate after ~30 steps at 128 ciphertexts.  Each live
+// buffer still owns its block exclusively, and a block is only pooled once
+// its buffer's stream has drained.  RNT_WS_POOL_MB caps the idle bytes.
+struct WsBlock {
+  int device;
+  void* p;
+  size_t bytes;
+};
+std::mutex g_ws_mu;
+std::vector<WsBlock> g_ws_pool;  // oldest first
+size_t g_ws_pool_bytes = 0;
+
+static size_t ws_pool_cap() {
+  static const size_t cap = [] {
+    const char* e = getenv("RNT_WS_POOL_MB");
+    const long mb = e ? atol(e) : 65536L;
+    return (size_t)(mb > 0 ? mb : 0) << 20;
+  }();
+  return cap;
+}
+
+// Smallest idle block on `device` of at least `bytes`, or nullptr.
+static void* ws_take(int device, size_t bytes, size_t* got) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  size_t best = g_ws_pool.size();
+  for (size_t i = 0; i < g_ws_pool.size(); ++i) {
+    const WsBlock& w = g_ws_pool[i];
+    if (w.device == device && w.bytes >= bytes &&
+        (best == g_ws_pool.size() || w.bytes < g_ws_pool[best].bytes))
+      best = i;
+  }
+  if (best == g_ws_pool.size()) return nullptr;
+  void* p = g_ws_pool[best].p;
+  *got = g_ws_pool[best].bytes;
+  g_ws_pool_bytes -= *got;
+  g_ws_pool.erase(g_ws_pool.begin() + (long)best);
+  return p;
+}
+
+// Hand an idle block (its stream drained) to the pool; the oldest blocks
+// are freed while the pool would exceed its cap.
+static void ws_give(int device, void* p, size_t bytes) {
+  if (!p) return;
+  std::vector<WsBlock> drop;
+  {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    g_ws_pool.push_back({device, p, bytes});
+    g_ws_pool_bytes += bytes;
+    while (g_ws_pool_bytes > ws_pool_cap() && !g_ws_pool.empty()) {
+      drop.push_back(g_ws_pool.front());
+      g_ws_pool_bytes -= g_ws_pool.front().bytes;
+      g_ws_pool.erase(g_ws_pool.begin());
+    }
+  }
+  for (const WsBlock& w : drop) {
+    (void)hipSetDevice(w.device);
+    (void)hipFree(w.p);
+  }
+  if (!drop.empty()) (void)hipSetDevice(device);
+}
+
+// Free every idle block of `device` (before retrying a failed allocation).
+static void ws_drain(int device) {
+  std::vector<WsBlock> drop;
+  {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (size_t i = 0; i < g_ws_pool.size();) {
+      if (g_ws_pool[i].device == device) {
+        drop.push_back(g_ws_pool[i]);
+        g_ws_pool_bytes -= g_ws_pool[i].bytes;
+        g_ws_pool.erase(g_ws_pool.begin() + (long)i);
+      } else {
+        ++i;
+      }
+    }
+  }
+  for (const WsBlock& w : drop) (void)hipFree(w.p);
+}
+
 // Grow the buffer's private workspace to at least `bytes`.
 int ensure_ws(rnt_buf* b, size_t bytes) {
   if (b->ws_bytes >= bytes) return RNT_OK;
+  const int dev = b->ctx->t->device;
   if (b->ws) {
     // the stream may still be using the old workspace
     HIP_TRY(hipStreamSynchronize(b->ctx->t->stream), "hipStreamSynchronize");
-    HIP_TRY(hipFree(b->ws), "hipFree");
+    ws_give(dev, b->ws, b->ws_bytes);
     b->ws = nullptr;
     b->ws_bytes = 0;
   }
-  HIP_TRY(hipMalloc(&b->ws, bytes), "hipMalloc(workspace)");
+  size_t got = 0;
+  if (void* p = ws_take(dev, bytes, &got)) {
+    b->ws = p;
+    b->ws_bytes = got;
+    return RNT_OK;
+  }
+  hipError_t e = hipMalloc(&b->ws, bytes);
+  if (e == hipErrorOutOfMemory) {
+    (void)hipGetLastError();
+    ws_drain(dev);
+    e = hipMalloc(&b->ws, bytes);
+  }
+  if (e != hipSuccess) {
+    b->ws = nullptr;
+    return hip_fail(e, "hipMalloc(workspace)");
+  }
   b->ws_bytes = bytes;
   return RNT_OK;
 }
@@ -405,6 +505,10 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     t->wide = wide ? 1 : 0;
     // RNT_LAZY30=0 keeps the canonical product path for 30-bit bases (A/B)
     t->lazy30 = !wide && lazy30 && env_long("RNT_LAZY30", 1) != 0;
+    {
+      const long jg = env_long("RNT_DEC_JG", 1);  // A/B knob, 1..L
+      t->dec_jg = (uint32_t)(jg < 1 ? 1 : jg > 1024 ? 1024 : jg);
+    }
     t->log_n = log_n;
     t->n = (size_t)n;
     t->L = count;
@@ -534,7 +638,8 @@ extern "C" int rnt_buf_free(rnt_buf* b) {
     (void)hipStreamSynchronize(b->ctx->t->stream);
   }
   if (b->owns) (void)hipFree(b->data);
-  (void)hipFree(b->ws);
+  if (b->ctx) ws_give(b->ctx->t->device, b->ws, b->ws_bytes);  // stream drained above
+  else (void)hipFree(b->ws);
   (void)hipFree(b->stage);
   ctx_release(b->ctx);
   delete b;

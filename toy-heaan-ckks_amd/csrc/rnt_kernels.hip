@@ -781,14 +781,15 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
   for (int i = 0; i < E; ++i) dst.st(x[0][i], a0.v, i * a0.s);
 }
 
-// Tiled key-switch decomposition: grid x = target limb j (fastest, so the
-// L workgroups that reduce one source tile of d mod every q_j run back to
-// back and read it from L2), y = p * (C / TC) + column tile, z = source
-// limb i.
+// Tiled key-switch decomposition: grid x = group of jg target limbs j
+// (fastest, so the workgroups that reduce one source tile of d mod every q_j
+// run back to back and read it from L2; each loads the tile once and loops
+// over its group), y = p * (C / TC) + column tile, z = source limb i.
 template <class W, int LOG_R, int LOG_TC>
 __global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32_t log_n,
-                 uint32_t log_c, uint32_t L, uint32_t B, uint64_t d_ls) {
+                 uint32_t log_c, uint32_t L, uint32_t B, uint64_t d_ls, uint32_t Lt,
+                 uint32_t jg) {
   using G = ColGeo<LOG_R, LOG_TC>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -798,7 +799,9 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
   const uint32_t p = blockIdx.y >> tpp_log;
   const uint32_t ct = blockIdx.y & ((1u << tpp_log) - 1);
   const uint32_t i = blockIdx.z;
-  const uint32_t j = blockIdx.x;
+  // this workgroup's target limbs: [j0, j1), the source tile loaded once
+  const uint32_t j0 = blockIdx.x * jg;
+  const uint32_t j1 = j0 + jg < Lt ? j0 + jg : Lt;
   ColPos cp;
   cp.xp.slot = G::slot_of(threadIdx.x);
   cp.xp.tau = G::tau_of(threadIdx.x);
@@ -807,16 +810,23 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
   const ColAddr<G, G::BB0> a0(cp, log_c);
   ColAddr<G, G::BBL> al(cp, log_c);
   const BufView<W> src(d + (uint64_t)i * d_ls + (uint64_t)p * N, N);
-  const BufView<W> dst(S + (((uint64_t)j * L + i) * B + p) * N, N);
-  const LimbConst<W> lc = tp.lc[j];
-  W x[1][E];
+  W raw[E];
 #pragma unroll
-  for (int e = 0; e < E; ++e) x[0][e] = shoup_mul<W>(src.ld(a0.v, e * a0.s), (W)1, lc.one_p, lc.q);
-  xf_fwd<G, W, 1>(x, cp.xp, lds, col_twiddles<W, G::UNIFORM>(tp.tw + (uint64_t)j * N, N),
-                  mod_of(lc));
-  al.refresh();
+  for (int e = 0; e < E; ++e) raw[e] = src.ld(a0.v, e * a0.s);
+#pragma unroll 1
+  for (uint32_t j = j0; j < j1; ++j) {
+    const BufView<W> dst(S + (((uint64_t)j * L + i) * B + p) * N, N);
+    const LimbConst<W> lc = tp.lc[j];
+    W x[1][E];
 #pragma unroll
-  for (int e = 0; e < E; ++e) dst.st(x[0][e], al.v, e * al.s);
+    for (int e = 0; e < E; ++e) x[0][e] = shoup_mul<W>(raw[e], (W)1, lc.one_p, lc.q);
+    // (the transform's LDS exchange ends in a barrier: the next j may reuse it)
+    xf_fwd<G, W, 1>(x, cp.xp, lds, col_twiddles<W, G::UNIFORM>(tp.tw + (uint64_t)j * N, N),
+                    mod_of(lc));
+    al.refresh();
+#pragma unroll
+    for (int e = 0; e < E; ++e) dst.st(x[0][e], al.v, e * al.s);
+  }
 }
 
 // mode 0: forward rows in place; 1: inverse rows in place;
@@ -1478,14 +1488,17 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
   if (g.log_r >= 5) {
     const dim3 g0 = col_grid(k, g, Ls, (uint32_t)k.L);
     if (g0.x == 0 || g0.x > 65535u) return hipErrorInvalidConfiguration;
-    const dim3 grid((uint32_t)k.L, g0.x, Ls);
+    // target limbs per workgroup (Tables::dec_jg): the source tile is read
+    // once per group instead of once per target limb
+    const uint32_t jg = k.t->dec_jg ? k.t->dec_jg : 1u;
+    const dim3 grid(((uint32_t)k.L + jg - 1) / jg, g0.x, Ls);
     hipError_t e = hipSuccess;
 #define RNT_L2(R, TC)                                                                         \
   e = allow_lds(k_colt_decompose<W, R, TC>, col_lds<W, R, TC>());                             \
   if (e != hipSuccess) return e;                                                              \
   hipLaunchKernelGGL((k_colt_decompose<W, R, TC>), grid, dim3(ColGeo<R, TC>::THREADS),        \
                      (col_lds<W, R, TC>()), k.s, (W*)S, (const W*)d, tp, g.log_n, g.log_c,      \
-                     Ls, (uint32_t)k.B, d_ls)
+                     Ls, (uint32_t)k.B, d_ls, (uint32_t)k.L, jg)
 #define RNT_L(R)                          \
   if (col_log_tc(g) == 6) {               \
     RNT_L2(R, 6);                         \

@@ -203,9 +203,9 @@ class RnsBasis:
             acc = (acc + (int(r) * pow(qi % m, -1, m) % m) * qi) % Q
         return acc - Q if acc > Q // 2 else acc
 
-    def __del__(self):
+    def __del__(self, _lib=_lib):  # module globals may be gone at interpreter exit
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
+        if h is not None and h.value and _lib is not None and _lib._lib is not None:
             _lib._lib.rnt_ctx_destroy(h)
             self._h = None
 
@@ -431,9 +431,9 @@ class RnsPoly:
             out.append(row)
         return out[0] if self.n_polys == 1 else out
 
-    def __del__(self):
+    def __del__(self, _lib=_lib):  # module globals may be gone at interpreter exit
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
+        if h is not None and h.value and _lib is not None and _lib._lib is not None:
             _lib._lib.rnt_buf_free(h)
             self._h = None
 
