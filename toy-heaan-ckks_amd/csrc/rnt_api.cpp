@@ -506,8 +506,8 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     // RNT_LAZY30=0 keeps the canonical product path for 30-bit bases (A/B)
     t->lazy30 = !wide && lazy30 && env_long("RNT_LAZY30", 1) != 0;
     {
-      const long jg = env_long("RNT_DEC_JG", 1);  // A/B knob, 1..L
-      t->dec_jg = (uint32_t)(jg < 1 ? 1 : jg > 1024 ? 1024 : jg);
+      const long jg = env_long("RNT_DEC_JG", 0);  // A/B knob: 0 = auto, else 1..1024
+      t->dec_jg = (uint32_t)(jg < 0 ? 0 : jg > 1024 ? 1024 : jg);
     }
     t->log_n = log_n;
     t->n = (size_t)n;

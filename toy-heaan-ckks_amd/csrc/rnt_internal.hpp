@@ -86,7 +86,7 @@ struct Tables {
   int device = 0;
   int wide = 0;            // 0: W = u32, 1: W = u64
   bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path
-  uint32_t dec_jg = 1;     // key-switch decomposition: target limbs per workgroup
+  uint32_t dec_jg = 0;     // key-switch decomposition: target limbs per workgroup (0 = auto)
   uint32_t log_n = 0;
   size_t n = 0;
   size_t L = 0;            // channel count of the root basis
