@@ -1490,12 +1490,12 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
     if (g0.x == 0 || g0.x > 65535u) return hipErrorInvalidConfiguration;
     // target limbs per workgroup (Tables::dec_jg; 0 = auto): the source tile
     // is read once per group instead of once per target limb.  Auto takes
-    // groups of 16 (+3.7% ct-mul at B=128, profiles/r01_ab_dec_jg.txt) and
-    // halves them while the grid would fall under 16 workgroups per CU.
+    // groups of 16 (vs one limb per group: ks_decompose -8%, profiles/r01_ab_dec_jg.txt) and
+    // halves them while the grid would fall under 4 workgroups per CU.
     uint32_t jg = k.t->dec_jg;
     if (jg == 0) {
       jg = 16;
-      while (jg > 1 && ((uint32_t)k.L + jg - 1) / jg * (uint64_t)g0.x * Ls < 4096u) jg >>= 1;
+      while (jg > 1 && ((uint32_t)k.L + jg - 1) / jg * (uint64_t)g0.x * Ls < 1024u) jg >>= 1;
     }
     const dim3 grid(((uint32_t)k.L + jg - 1) / jg, g0.x, Ls);
     hipError_t e = hipSuccess;
