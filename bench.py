@@ -279,13 +279,17 @@ def run_ctmul(args, comm, world, rank, local_rank):
     c = [pipe.upload(x) for x in cts]
     key = pipe.upload_key(key_a, key_b)
     state0 = (pipe.basis, pipe.moduli, list(pipe.counts), pipe.limbs, pipe.owner_last)
+    lib_stream = pipe.backend.shared_stream(pipe.basis)
+    if os.environ.get("RNT_SHARED_STREAM", "1") == "0":  # A/B: torch's own stream + host syncs
+        lib_stream = torch.cuda.current_stream()
 
     def step():
         # every step starts from the same level (rescale drops a limb)
         pipe.basis, pipe.moduli, counts, pipe.limbs, pipe.owner_last = state0
         pipe.counts = list(counts)
-        m0, m1 = pipe.mul_relin(c[0], c[1], c[2], c[3], key)
-        return pipe.rescale(m0, m1)
+        with torch.cuda.stream(lib_stream):  # torch ops share the library's stream
+            m0, m1 = pipe.mul_relin(c[0], c[1], c[2], c[3], key)
+            return pipe.rescale(m0, m1)
 
     for _ in range(args.warmup):
         step()

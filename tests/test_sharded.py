@@ -216,9 +216,13 @@ def test_sharded_layout_bookkeeping():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shared", [False, True], ids=["torch-stream", "shared-stream"])
 @pytest.mark.parametrize("world", [2, 4])
-def test_limb_sharded_gpu_threads_match_unsharded(gpu, world):
+def test_limb_sharded_gpu_threads_match_unsharded(gpu, world, shared):
+    import contextlib
     import threading
+
+    import torch
 
     import rns_ntt as rn
     from rns_ntt.sharded import GpuBackend, LimbShardedPipeline, ThreadComm
@@ -231,8 +235,12 @@ def test_limb_sharded_gpu_threads_match_unsharded(gpu, world):
 
     def rank_main(r):
         try:
-            pipe = LimbShardedPipeline(mods, n, comm.rank_view(r), GpuBackend(0))
-            relin, resc = _run_rank(pipe, cts, key_a, key_b)
+            be = GpuBackend(0)
+            pipe = LimbShardedPipeline(mods, n, comm.rank_view(r), be)
+            # shared: torch runs on the library's stream and the host syncs drop out
+            ctx = torch.cuda.stream(be.shared_stream(pipe.basis)) if shared else contextlib.nullcontext()
+            with ctx:
+                relin, resc = _run_rank(pipe, cts, key_a, key_b)
             results[r] = (r, (pipe.limbs.start, pipe.limbs.stop), relin, resc)
         except BaseException as e:  # surface thread failures in the test
             errors.append(e)

@@ -109,8 +109,10 @@ class _ThreadRank:
 
         c = self._c
         c._slots[self.rank] = local
+        _stream_done(local)  # ranks read each other's tensors from their own streams
         c._bar.wait()
         out = torch.cat([s for s in c._slots], 0)
+        _stream_done(out)
         c._bar.wait()
         return out
 
@@ -118,11 +120,21 @@ class _ThreadRank:
         c = self._c
         if self.rank == src:
             c._slots[src] = t
+            _stream_done(t)
         c._bar.wait()
         if self.rank != src:
             t.copy_(c._slots[src])
+            _stream_done(t)
         c._bar.wait()
         return t
+
+
+def _stream_done(t):
+    """Wait for this thread's current stream when `t` lives on a GPU."""
+    if getattr(t, "is_cuda", False):
+        import torch
+
+        torch.cuda.current_stream(t.device).synchronize()
 
 
 # ---------------------------------------------------------------------------
@@ -153,8 +165,27 @@ class GpuBackend:
     def _dtype(self, basis):
         return self.torch.int32 if max(basis.moduli()) < (1 << 31) else self.torch.int64
 
-    def _sync_torch(self):
+    def shared_stream(self, basis):
+        """The library context's HIP stream as a torch stream.  Run the
+        pipeline under ``with torch.cuda.stream(backend.shared_stream(basis))``
+        and torch's allocations, copies and collective joins are ordered with
+        the library's kernels on one stream, so the host syncs below drop out."""
+        return self.torch.cuda.ExternalStream(basis.stream(), device=self.tdev)
+
+    def _same_stream(self, basis) -> bool:
+        return self.torch.cuda.current_stream(self.tdev).cuda_stream == basis.stream()
+
+    def _sync_torch(self, basis=None):
+        """Before a library op on torch memory: torch's stream must be done
+        with it, unless torch is running on the library's own stream."""
+        if basis is not None and self._same_stream(basis):
+            return
         self.torch.cuda.synchronize(self.tdev)
+
+    def _lib_done(self, basis):
+        """After a library op whose output torch reads next."""
+        if not self._same_stream(basis):
+            basis.sync()
 
     def _empty(self, basis, shape):
         return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
@@ -185,10 +216,10 @@ class GpuBackend:
         from . import ct_tensor
 
         B, N = c0.n_polys, basis.degree
-        self._sync_torch()  # torch may hand back memory its stream last used
+        self._sync_torch(basis)  # torch may hand back memory its stream last used
         d2_t = self._empty(basis, (basis.channel_count(), B, N))
         d0, d1, _ = ct_tensor(c0, c1, c0p, c1p, d2_out=self._wrap(basis, d2_t, B))
-        basis.sync()
+        self._lib_done(basis)
         return d0, d1, d2_t
 
     def keyswitch(self, basis, src_full, key, d0, d1):
@@ -197,11 +228,11 @@ class GpuBackend:
         from . import keyswitch_ext
 
         B, N, L = int(src_full.shape[1]), basis.degree, basis.channel_count()
-        self._sync_torch()
+        self._sync_torch(basis)
         out_t = self._empty(basis, (2, L, B, N))
         o0, o1 = self._wrap(basis, out_t[0], B), self._wrap(basis, out_t[1], B)
         keyswitch_ext(src_full.data_ptr(), src_full.shape[0], key, basis, B, d0, d1, o0, o1)
-        basis.sync()
+        self._lib_done(basis)
         return o0, o1
 
     def rotate(self, basis, poly, k: int):
@@ -214,11 +245,11 @@ class GpuBackend:
         from . import check, load
 
         B = poly.n_polys
-        self._sync_torch()
+        self._sync_torch(basis)
         t = self._empty(basis, (basis.channel_count(), B, basis.degree))
         out = self._wrap(basis, t, B)
         check(load().rnt_rotate_slots(out.handle, poly.handle, int(k)))
-        basis.sync()
+        self._lib_done(basis)
         return t
 
     def add(self, basis, a, b):
@@ -235,10 +266,10 @@ class GpuBackend:
         from . import rescale_ext
 
         B = poly.n_polys
-        self._sync_torch()
+        self._sync_torch(basis)
         out_t = self._empty(basis, (out_basis.channel_count(), B, basis.degree))
         out = rescale_ext(poly, last_plane.data_ptr(), q_last, out_basis, out=self._wrap(out_basis, out_t, B))
-        basis.sync()
+        self._lib_done(basis)
         return out
 
 
