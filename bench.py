@@ -279,9 +279,11 @@ def run_ctmul(args, comm, world, rank, local_rank):
     c = [pipe.upload(x) for x in cts]
     key = pipe.upload_key(key_a, key_b)
     state0 = (pipe.basis, pipe.moduli, list(pipe.counts), pipe.limbs, pipe.owner_last)
-    lib_stream = pipe.backend.shared_stream(pipe.basis)
-    if os.environ.get("RNT_SHARED_STREAM", "1") == "0":  # A/B: torch's own stream + host syncs
-        lib_stream = torch.cuda.current_stream()
+    # shared stream: measured at N=1 only (RCCL joins on an external stream
+    # are not yet run on a multi-GPU box), so it is the N=1 default;
+    # RNT_SHARED_STREAM=0/1 forces it off/on (A/B)
+    shared = os.environ.get("RNT_SHARED_STREAM", "1" if world == 1 else "0") != "0"
+    lib_stream = pipe.backend.shared_stream(pipe.basis) if shared else torch.cuda.current_stream()
 
     def step():
         # every step starts from the same level (rescale drops a limb)
