@@ -673,3 +673,135 @@ double or_polymul_batch_mt(const or_basis* b, uint64_t* a, const uint64_t* rhs,
   pthread_mutex_destroy(&job.mu);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ------------------------------------------------------------------ */
+/* Channel-parallel key-switch (test infrastructure: the same per-channel  */
+/* arithmetic as or_gadget_keyswitch / or_mul_ciphertexts_gadget /          */
+/* or_rotate_ciphertext, spread over threads so the oracle can check the    */
+/* BASELINE config-4/5 rings in seconds).  Every target channel j of the   */
+/* gadget sum depends only on d[*] and channel j of the keys               */
+/* (engine.rs:505-528: alpha_i[j] = d[i] mod q_j, then channel-wise ring   */
+/* products), so channels are independent work items.                      */
+/* ------------------------------------------------------------------ */
+
+typedef void (*chan_fn)(void* ctx, size_t ch, uint64_t* scratch);
+typedef struct {
+  chan_fn fn;
+  void* ctx;
+  size_t items, next, scratch_words;
+  pthread_mutex_t mu;
+} par_job;
+
+static void* par_worker(void* arg) {
+  par_job* job = (par_job*)arg;
+  uint64_t* scratch = (uint64_t*)malloc(job->scratch_words * sizeof(uint64_t));
+  for (;;) {
+    pthread_mutex_lock(&job->mu);
+    size_t it = job->next++;
+    pthread_mutex_unlock(&job->mu);
+    if (it >= job->items) break;
+    job->fn(job->ctx, it, scratch);
+  }
+  free(scratch);
+  return NULL;
+}
+
+static void par_for(size_t items, int threads, size_t scratch_words, chan_fn fn, void* ctx) {
+  if (threads < 1) threads = 1;
+  if ((size_t)threads > items) threads = (int)(items ? items : 1);
+  par_job job;
+  job.fn = fn; job.ctx = ctx; job.items = items; job.next = 0; job.scratch_words = scratch_words;
+  pthread_mutex_init(&job.mu, NULL);
+  pthread_t* th = (pthread_t*)malloc((size_t)threads * sizeof(pthread_t));
+  for (int i = 0; i < threads; i++) pthread_create(&th[i], NULL, par_worker, &job);
+  for (int i = 0; i < threads; i++) pthread_join(th[i], NULL);
+  free(th);
+  pthread_mutex_destroy(&job.mu);
+}
+
+typedef struct {
+  const or_basis* b;
+  const uint64_t *d, *key_a, *key_b;
+  uint64_t *acc0, *acc1;
+} ks_ctx;
+
+/* target channel j of engine.rs:505-528 */
+static void ks_channel(void* vc, size_t j, uint64_t* scratch) {
+  ks_ctx* c = (ks_ctx*)vc;
+  const or_basis* b = c->b;
+  size_t L = b->channels, n = b->n, sz = L * n;
+  uint64_t qj = b->moduli[j];
+  uint64_t* alpha = scratch;
+  uint64_t* tb = scratch + n;
+  uint64_t* mul_scratch = scratch + 2 * n;
+  uint64_t* a0 = c->acc0 + j * n;
+  uint64_t* a1 = c->acc1 + j * n;
+  memset(a0, 0, n * sizeof(uint64_t));
+  memset(a1, 0, n * sizeof(uint64_t));
+  for (size_t i = 0; i < L; i++) {
+    for (size_t k = 0; k < n; k++) alpha[k] = c->d[i * n + k] % qj; /* :507-516 */
+    memcpy(tb, alpha, n * sizeof(uint64_t));
+    channel_mul_coeff(&b->tables[j], n, tb, c->key_b + i * sz + j * n, mul_scratch); /* :521-523 */
+    for (size_t k = 0; k < n; k++) a0[k] = or_add_mod(a0[k], tb[k], qj);
+    channel_mul_coeff(&b->tables[j], n, alpha, c->key_a + i * sz + j * n, mul_scratch); /* :525-527 */
+    for (size_t k = 0; k < n; k++) a1[k] = or_add_mod(a1[k], alpha[k], qj);
+  }
+}
+
+void or_gadget_keyswitch_mt(const or_basis* b, const uint64_t* d, const uint64_t* key_a,
+                            const uint64_t* key_b, uint64_t* acc0, uint64_t* acc1, int threads) {
+  ks_ctx c = {b, d, key_a, key_b, acc0, acc1};
+  par_for(b->channels, threads, 3 * b->n, ks_channel, &c);
+}
+
+typedef struct {
+  const or_basis* b;
+  const uint64_t *c0, *c1, *c0p, *c1p;
+  uint64_t *out0, *out1, *d2;
+} tensor_ctx;
+
+/* channel ch of the tensor product engine.rs:480-493 */
+static void tensor_channel(void* vc, size_t ch, uint64_t* scratch) {
+  tensor_ctx* c = (tensor_ctx*)vc;
+  const or_basis* b = c->b;
+  size_t n = b->n, o = ch * n;
+  uint64_t q = b->moduli[ch];
+  const or_table* t = &b->tables[ch];
+  uint64_t* d1b = scratch;
+  uint64_t* ms = scratch + n;
+  memcpy(c->out0 + o, c->c0 + o, n * 8); channel_mul_coeff(t, n, c->out0 + o, c->c0p + o, ms);
+  memcpy(c->out1 + o, c->c0 + o, n * 8); channel_mul_coeff(t, n, c->out1 + o, c->c1p + o, ms);
+  memcpy(d1b, c->c1 + o, n * 8); channel_mul_coeff(t, n, d1b, c->c0p + o, ms);
+  for (size_t k = 0; k < n; k++) c->out1[o + k] = or_add_mod(c->out1[o + k], d1b[k], q);
+  memcpy(c->d2 + o, c->c1 + o, n * 8); channel_mul_coeff(t, n, c->d2 + o, c->c1p + o, ms);
+}
+
+void or_mul_ciphertexts_gadget_mt(const or_basis* b, const uint64_t* c0, const uint64_t* c1,
+                                  const uint64_t* c0p, const uint64_t* c1p,
+                                  const uint64_t* key_a, const uint64_t* key_b,
+                                  uint64_t* out0, uint64_t* out1, int threads) {
+  size_t sz = b->channels * b->n;
+  uint64_t* d2 = (uint64_t*)malloc(sz * sizeof(uint64_t));
+  uint64_t* r0 = (uint64_t*)malloc(sz * sizeof(uint64_t));
+  uint64_t* r1 = (uint64_t*)malloc(sz * sizeof(uint64_t));
+  tensor_ctx tc = {b, c0, c1, c0p, c1p, out0, out1, d2};
+  par_for(b->channels, threads, 2 * b->n, tensor_channel, &tc);
+  or_gadget_keyswitch_mt(b, d2, key_a, key_b, r0, r1, threads);
+  or_add_assign(b, out0, 0, r0, 0); /* :530 */
+  or_add_assign(b, out1, 0, r1, 0); /* :531 */
+  free(d2); free(r0); free(r1);
+}
+
+void or_rotate_ciphertext_mt(const or_basis* b, const uint64_t* c0, const uint64_t* c1, int32_t k,
+                             const uint64_t* key_a, const uint64_t* key_b,
+                             uint64_t* out0, uint64_t* out1, int threads) {
+  size_t sz = b->channels * b->n;
+  uint64_t* c1r = (uint64_t*)malloc(sz * sizeof(uint64_t));
+  uint64_t* ks0 = (uint64_t*)malloc(sz * sizeof(uint64_t));
+  int f0, f1;
+  or_rotate_slots(b, c0, 0, k, out0, &f0); /* :417 */
+  or_rotate_slots(b, c1, 0, k, c1r, &f1);  /* :418 */
+  or_gadget_keyswitch_mt(b, c1r, key_a, key_b, ks0, out1, threads); /* :426-452 */
+  or_add_assign(b, out0, 0, ks0, 0);       /* :454-455 */
+  free(c1r); free(ks0);
+}

@@ -138,6 +138,22 @@ void or_rotate_ciphertext(const or_basis* b, const uint64_t* c0,
                           const uint64_t* key_a, const uint64_t* key_b,
                           uint64_t* out0, uint64_t* out1);
 
+/* Channel-parallel forms of the three above (identical results; `threads`
+ * workers over target channels).  Test infrastructure for the config-4/5
+ * rings only. */
+void or_gadget_keyswitch_mt(const or_basis* b, const uint64_t* d,
+                            const uint64_t* key_a, const uint64_t* key_b,
+                            uint64_t* acc0, uint64_t* acc1, int threads);
+void or_mul_ciphertexts_gadget_mt(const or_basis* b, const uint64_t* c0,
+                                  const uint64_t* c1, const uint64_t* c0p,
+                                  const uint64_t* c1p, const uint64_t* key_a,
+                                  const uint64_t* key_b, uint64_t* out0,
+                                  uint64_t* out1, int threads);
+void or_rotate_ciphertext_mt(const or_basis* b, const uint64_t* c0,
+                             const uint64_t* c1, int32_t k,
+                             const uint64_t* key_a, const uint64_t* key_b,
+                             uint64_t* out0, uint64_t* out1, int threads);
+
 /* ---- CPU baseline driver (bench.py cpu_baseline leg) ---------------------- */
 /* Runs `count` coefficient-domain poly-muls a[i] *= b[i] ([count][L][N] each)
  * with `threads` std::thread-style workers over (poly, limb) work items.

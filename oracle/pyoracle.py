@@ -76,6 +76,10 @@ _SIGS = {
     "or_gadget_keyswitch": (None, [_B, _U64P, _U64P, _U64P, _U64P, _U64P]),
     "or_mul_ciphertexts_gadget": (None, [_B, _U64P, _U64P, _U64P, _U64P, _U64P, _U64P, _U64P, _U64P]),
     "or_rotate_ciphertext": (None, [_B, _U64P, _U64P, c_int32, _U64P, _U64P, _U64P, _U64P]),
+    "or_gadget_keyswitch_mt": (None, [_B, _U64P, _U64P, _U64P, _U64P, _U64P, c_int]),
+    "or_mul_ciphertexts_gadget_mt": (None, [_B, _U64P, _U64P, _U64P, _U64P, _U64P, _U64P, _U64P, _U64P,
+                                            c_int]),
+    "or_rotate_ciphertext_mt": (None, [_B, _U64P, _U64P, c_int32, _U64P, _U64P, _U64P, _U64P, c_int]),
     "or_polymul_batch_mt": (c_double, [_B, _U64P, _U64P, c_size_t, c_int]),
 }
 
@@ -235,28 +239,48 @@ def rotate_slots(b: Basis, a, k, in_ntt=False):
     return out, bool(f.value)
 
 
-def keyswitch(b: Basis, d, key_a, key_b):
-    """key_a/key_b: [L][L][N] coefficient domain."""
+def keyswitch(b: Basis, d, key_a, key_b, threads: int = 1):
+    """key_a/key_b: [L][L][N] coefficient domain.  threads > 1 runs the
+    channel-parallel form (same arithmetic per target channel)."""
     acc0 = np.zeros((b.L, b.n), dtype=np.uint64)
     acc1 = np.zeros((b.L, b.n), dtype=np.uint64)
-    lib().or_gadget_keyswitch(b.ref, _p(_poly(d)), _p(_poly(key_a)), _p(_poly(key_b)), _p(acc0), _p(acc1))
+    args = (b.ref, _p(_poly(d)), _p(_poly(key_a)), _p(_poly(key_b)), _p(acc0), _p(acc1))
+    if threads > 1:
+        lib().or_gadget_keyswitch_mt(*args, threads)
+    else:
+        lib().or_gadget_keyswitch(*args)
     return acc0, acc1
 
 
-def mul_ciphertexts_gadget(b: Basis, c0, c1, c0p, c1p, key_a, key_b):
+def mul_ciphertexts_gadget(b: Basis, c0, c1, c0p, c1p, key_a, key_b, threads: int = 1):
     o0 = np.zeros((b.L, b.n), dtype=np.uint64)
     o1 = np.zeros((b.L, b.n), dtype=np.uint64)
-    lib().or_mul_ciphertexts_gadget(b.ref, _p(_poly(c0)), _p(_poly(c1)), _p(_poly(c0p)), _p(_poly(c1p)),
-                                    _p(_poly(key_a)), _p(_poly(key_b)), _p(o0), _p(o1))
+    args = (b.ref, _p(_poly(c0)), _p(_poly(c1)), _p(_poly(c0p)), _p(_poly(c1p)),
+            _p(_poly(key_a)), _p(_poly(key_b)), _p(o0), _p(o1))
+    if threads > 1:
+        lib().or_mul_ciphertexts_gadget_mt(*args, threads)
+    else:
+        lib().or_mul_ciphertexts_gadget(*args)
     return o0, o1
 
 
-def rotate_ciphertext(b: Basis, c0, c1, k, key_a, key_b):
+def rotate_ciphertext(b: Basis, c0, c1, k, key_a, key_b, threads: int = 1):
     o0 = np.zeros((b.L, b.n), dtype=np.uint64)
     o1 = np.zeros((b.L, b.n), dtype=np.uint64)
-    lib().or_rotate_ciphertext(b.ref, _p(_poly(c0)), _p(_poly(c1)), k, _p(_poly(key_a)), _p(_poly(key_b)),
-                               _p(o0), _p(o1))
+    args = (b.ref, _p(_poly(c0)), _p(_poly(c1)), k, _p(_poly(key_a)), _p(_poly(key_b)), _p(o0), _p(o1))
+    if threads > 1:
+        lib().or_rotate_ciphertext_mt(*args, threads)
+    else:
+        lib().or_rotate_ciphertext(*args)
     return o0, o1
+
+
+def host_threads(cap: int = 16) -> int:
+    """Worker threads for the oracle on this host (the GPU box's CPU share is
+    16; os.cpu_count() reports the whole machine)."""
+    import os
+
+    return max(1, min(cap, os.cpu_count() or 1))
 
 
 def polymul_batch_mt(b: Basis, a, rhs, threads):

@@ -88,12 +88,41 @@ __device__ __forceinline__ auto mod_for(const LimbConst<W>& lc) {
 #ifndef RNT_BUF_ST_AUX
 #define RNT_BUF_ST_AUX 0
 #endif
+// Measurement builds only (tools/build_variant.sh -DRNT_MEAS=...; never the
+// shipped library): 1 = the product kernels (k_colt_fwd, k_row<2>,
+// k_colt_inv) move no plane data through memory (synthetic loads, stores
+// kept behind a never-true compare), 2 = their butterflies are skipped.
+// They time the VALU-only and memory/LDS-only parts of the poly-mul
+// ("ceiling").
+#ifndef RNT_MEAS
+#define RNT_MEAS 0
+#endif
+constexpr int kMeas = RNT_MEAS;
+template <class W>
+__device__ __forceinline__ W meas_val(uint32_t v, uint32_t s) {
+  return (W)((v * 2654435761u + s) & 0x3fffffffu);
+}
+template <class W>
+__device__ __forceinline__ W gload(const W* p, uint64_t i) {
+  if constexpr (kMeas == 1) return meas_val<W>((uint32_t)i, 0u);
+  return p[i];
+}
+template <class W>
+__device__ __forceinline__ void gstore(W* p, uint64_t i, W x) {
+  if constexpr (kMeas == 1) {
+    if (x == (W)0xffffffffu) p[i] = x;
+    return;
+  }
+  p[i] = x;
+}
+
 template <class W>
 struct BufView {
   __amdgpu_buffer_rsrc_t r;
   __device__ BufView(const W* base, uint32_t elems)
       : r(__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(elems * sizeof(W)), 0x00020000)) {}
   __device__ __forceinline__ W ld(uint32_t v, uint32_t s) const {
+    if constexpr (kMeas == 1) return meas_val<W>(v, s);
     if constexpr (sizeof(W) == 4) {
       return __builtin_amdgcn_raw_buffer_load_b32(r, v * 4u, s * 4u, RNT_BUF_LD_AUX);
     } else {
@@ -119,6 +148,9 @@ struct BufView {
     }
   }
   __device__ __forceinline__ void st(W x, uint32_t v, uint32_t s) const {
+    if constexpr (kMeas == 1) {
+      if (x != (W)0xffffffffu) return;
+    }
     if constexpr (sizeof(W) == 4) {
       __builtin_amdgcn_raw_buffer_store_b32(x, r, v * 4u, s * 4u, RNT_BUF_ST_AUX);
     } else {
@@ -451,6 +483,7 @@ struct Fold {
 template <class W, int NOPS, int LOGE, int K, int BB, class TS, class MO>
 __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0, const TS& tw,
                                         const MO& mo) {
+  if constexpr (kMeas == 2) return;
   constexpr int E = 1 << LOGE;
 #pragma unroll
   for (int sl = K - 1; sl >= 0; --sl) {
@@ -484,6 +517,7 @@ __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0,
 template <class W, int NOPS, int LOGE, int K, int BB, int LOGX, bool FOLD, class TS, class MO>
 __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0, const TS& itw,
                                         const MO& mo, const Fold<W>& f) {
+  if constexpr (kMeas == 2) return;
   const W bias = gs_bias(mo);
   constexpr int E = 1 << LOGE;
 #pragma unroll
@@ -851,8 +885,8 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
     W v[2][E];
 #pragma unroll
     for (int i = 0; i < E; ++i) {
-      v[0][i] = xg[base + b0 + ((uint32_t)i << G::BB0)];
-      v[1][i] = yg[base + b0 + ((uint32_t)i << G::BB0)];
+      v[0][i] = gload(xg, base + b0 + ((uint32_t)i << G::BB0));
+      v[1][i] = gload(yg, base + b0 + ((uint32_t)i << G::BB0));
     }
     const auto mo = mod_for<W, LZ>(lc);
     xf_fwd<G, W, 2>(v, rp.xp, lds, tw, mo);
@@ -874,7 +908,7 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
     xf_inv<G, W, 1>(z, rp.xp, lds, itw, mo);
     if (rp.active) {
 #pragma unroll
-      for (int i = 0; i < E; ++i) xg[base + b0 + ((uint32_t)i << G::BB0)] = z[0][i];
+      for (int i = 0; i < E; ++i) gstore(xg, base + b0 + ((uint32_t)i << G::BB0), z[0][i]);
     }
   } else if constexpr (MODE == 0) {
     W v[1][E];
