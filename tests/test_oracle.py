@@ -191,3 +191,22 @@ def test_config_prime_chains(vectors, manifest):
         assert mod == [int(x) for x in vectors[f"{name}/moduli"]]
         for q, psi in zip(mod, vectors[f"{name}/psi"]):
             assert orc.lib().or_find_primitive_root(q, 2 * m["n"]) == int(psi)
+
+
+def test_channel_parallel_keyswitch_matches_serial():
+    """or_*_mt (test infrastructure for the config-4/5 checks) give the
+    serial restatement's results exactly."""
+    n = 64
+    mod = orc.generate_primes(31, 4, n)
+    b = orc.Basis(mod, n)
+    rng = np.random.default_rng(8)
+    c = [orc.uniform_poly(mod, n, rng) for _ in range(4)]
+    ka, kb = orc.uniform_poly(mod, n, rng, batch=4), orc.uniform_poly(mod, n, rng, batch=4)
+    for x, y in zip(orc.mul_ciphertexts_gadget(b, *c, ka, kb), orc.mul_ciphertexts_gadget(b, *c, ka, kb, threads=3)):
+        assert np.array_equal(x, y)
+    for k in (1, -3, 0):
+        for x, y in zip(orc.rotate_ciphertext(b, c[0], c[1], k, ka, kb),
+                        orc.rotate_ciphertext(b, c[0], c[1], k, ka, kb, threads=3)):
+            assert np.array_equal(x, y)
+    for x, y in zip(orc.keyswitch(b, c[2], ka, kb), orc.keyswitch(b, c[2], ka, kb, threads=2)):
+        assert np.array_equal(x, y)

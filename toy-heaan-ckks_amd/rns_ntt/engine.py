@@ -46,7 +46,15 @@ class CkksEngine:
 
     def __init__(self, moduli, degree: int, error_std: float = 3.2,
                  hamming_weight: Optional[int] = None, device: int = 0):
-        self.basis = RnsBasis(list(moduli), degree, device=device)
+        # an existing RnsBasis is shared, as CkksEngine::new(basis.clone(), ..)
+        # shares the Arc (engine.rs:36-41): a level-l engine built on a
+        # rescaled ciphertext's basis encrypts onto that same basis
+        if isinstance(moduli, RnsBasis):
+            if moduli.degree != degree:
+                raise ValueError(f"basis degree {moduli.degree} != engine degree {degree}")
+            self.basis = moduli
+        else:
+            self.basis = RnsBasis(list(moduli), degree, device=device)
         self.degree = degree
         self.error_std = error_std
         self.hamming_weight = hamming_weight if hamming_weight is not None else degree // 2
