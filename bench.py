@@ -38,6 +38,13 @@ CT_METRIC = "ct x ct -> relin -> rescale ciphertexts/sec (N=2^16, 16 primes, lim
 ROT_METRIC = "rotation key-switches/sec (N=2^17, 32 primes, power-of-two Galois offsets)"
 ENC_METRIC = "CKKS encode+decode round trips/sec (N=2^16, 16 primes, N/2 complex slots)"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); ~6.3 TB/s achievable
+# VALU peak in radix-2 butterflies/s: all 1024 SIMDs (256 CUs
+# x 4) issue the canonical 31-bit CT butterfly -- 3 half-rate + 8 full-rate
+# wave64 instructions -- for 64 lanes at a time, at the per-instruction costs
+# measured on this chip (tools/oprate.hip: 4.1 and 2.2 SIMD cycles) and the
+# 2.4 GHz maximum clock: 1024 * 64 * 2.4e9 / 29.9 = 5.26e12 butterflies/s.
+VALU_BFLY_CYCLES = 3 * 4.1 + 8 * 2.2
+VALU_PEAK_BFLY = 1024 * 64 * 2.4e9 / VALU_BFLY_CYCLES
 
 
 def log(*a):
@@ -59,7 +66,12 @@ def parse():
     p.add_argument("--limbs", type=int, default=16)
     p.add_argument("--prime-bits", type=int, default=31,
                    help="poly-mul primes from generate_primes(bits, L, N); 30 takes the lazy path")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    p.add_argument("--cpu-seconds", type=float, default=16.0, help="CPU baseline sample budget")
+    p.add_argument("--rot-keys", choices=("per-offset", "shared"), default="per-offset",
+                   help="rotate: a distinct gadget key per offset (SURVEY 8d sweep 1) or one resident key")
+    p.add_argument("--rot-offsets", choices=("pow2", "all"), default="pow2",
+                   help="rotate: the log2(N/2) power-of-two offsets, or every offset 1..N/2-1 with "
+                        "one resident key (SURVEY 8d sweep 2)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
 
@@ -80,29 +92,72 @@ def oracle():
     return orc
 
 
+def host_info():
+    """What the CPU baseline ran on: lscpu model and sockets, the machine's
+    CPU count and the CPUs this process may use (the GPU box gives each job a
+    share of 16 of the machine's many CPUs; os.cpu_count() reports them all)."""
+    info = {"cpu_count": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity"] = os.cpu_count()
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "Model name":
+                info["model"] = v
+            elif k == "Socket(s)":
+                info["sockets"] = int(v) if v.isdigit() else v
+            elif k == "Core(s) per socket":
+                info["cores_per_socket"] = int(v) if v.isdigit() else v
+            elif k == "Thread(s) per core":
+                info["threads_per_core"] = int(v) if v.isdigit() else v
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
+
+
+def usable_threads() -> int:
+    """All the CPUs this job may use, capped at the GPU box's share of 16."""
+    return max(1, min(16, host_info()["affinity"] or 1))
+
+
 def cpu_baseline(mod, n, budget_s):
-    """The oracle (reference-faithful C restatement, u128 `%`) on this host's
-    cores: a bounded sample of the same workload, timed in this run."""
+    """The oracle (reference-faithful C restatement of poly.rs:307-329, u128
+    `%`) on this host: single-threaded, as the reference runs, and over every
+    usable core (std::thread-style workers over (poly, limb) items), each on a
+    bounded sample of the same workload timed in this run."""
     import numpy as np
 
     orc = oracle()
-    threads = max(1, min(16, os.cpu_count() or 1))
     Bo = orc.Basis(mod, n)
     rng = np.random.default_rng(11)
-    count = threads  # one pair per worker per pass; each pair = L (poly, limb) items
-    a = orc.uniform_poly(mod, n, rng, batch=count)
-    b = orc.uniform_poly(mod, n, rng, batch=count)
-    done, elapsed = 0, 0.0
-    while elapsed < budget_s:
-        elapsed += orc.polymul_batch_mt(Bo, a, b, threads)
-        done += count
+
+    def timed(threads, budget):
+        count = threads  # one pair per worker per pass; each pair = L (poly, limb) items
+        a = orc.uniform_poly(mod, n, rng, batch=count)
+        b = orc.uniform_poly(mod, n, rng, batch=count)
+        done, elapsed = 0, 0.0
+        while elapsed < budget:
+            elapsed += orc.polymul_batch_mt(Bo, a, b, threads)
+            done += count
+        return done, elapsed
+
+    threads = usable_threads()
+    d1, e1 = timed(1, budget_s / 2)
+    dn, en = timed(threads, budget_s / 2)
     return {
-        "value": done / elapsed,
+        "value": dn / en,
         "unit": "poly-muls/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{done} coefficient-domain poly-muls (N={n}, L={len(mod)}), {count} per pass over "
-                  f"{threads} threads, {elapsed:.1f} s wall; oracle/oracle.c restating poly.rs:307-329",
+        "sample": f"{dn} coefficient-domain poly-muls (N={n}, L={len(mod)}), {threads} per pass over "
+                  f"{threads} threads, {en:.1f} s wall; oracle/oracle.c restating poly.rs:307-329",
+        "single_thread": {"value": d1 / e1, "cores": 1,
+                          "sample": f"{d1} poly-muls on one thread, {e1:.1f} s wall"},
+        "host": host_info(),
     }
 
 
@@ -113,19 +168,22 @@ def uniform(rng, mods, count, n):
     return rng.integers(0, 1 << 62, size=(count, len(mods), n), dtype=np.uint64) % q
 
 
-def traffic_for(kernel, batch, log_n, L):
-    """HBM bytes per launch of `kernel` from the committed PMC passes
-    (profiles/pmc_traffic.json, tools/pmc_summary.py) when they were taken
-    on this exact shape; else None."""
+def traffic_for(kernel, workload, batch, log_n, L):
+    """HBM bytes per launch of `kernel` (2 x FETCH_SIZE + WRITE_SIZE, the
+    gfx950 correction of MI355X_MICROARCH.md § HBM) from the committed
+    rocprofv3 --pmc passes of this exact workload shape
+    (profiles/pmc_traffic.json, tools/profile_run.sh + tools/pmc_summary.py);
+    None when no pass of this shape is committed."""
     tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(tpath) as f:
             t = json.load(f)
-        kt = t.get("kernels", {}).get(kernel)
-        if kt and t.get("batch") == batch and t.get("log_n") == log_n and t.get("L") == L:
-            return kt.get("bytes_per_launch")
     except (OSError, ValueError):
-        pass
+        return None
+    for e in t.get("entries", []):
+        if (e.get("workload"), e.get("batch"), e.get("log_n"), e.get("L")) == (workload, batch, log_n, L):
+            kt = e.get("kernels", {}).get(kernel)
+            return kt.get("bytes_per_launch") if kt else None
     return None
 
 
@@ -175,9 +233,7 @@ def run_polymul(args, comm, world, rank, local_rank):
     comm.barrier()
     elapsed = comm.max(t1 - t0)
     kernels = {}
-    # the three-launch column/row/column path (default) or the opt-in
-    # whole-plane path (RNT_PLANE=1 at N=2^16 with u32 words)
-    for k in ("plane_fwd", "plane_mul", "col_fwd", "row_mul", "col_inv"):
+    for k in ("col_fwd", "row_mul", "col_inv"):
         cnt, ms = B.profile_read(k)
         if cnt:
             kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
@@ -196,8 +252,7 @@ def run_polymul(args, comm, world, rank, local_rank):
     # the device word width) / its average launch time, measured with HIP
     # events on the library stream
     elem = Lr * batch * n
-    step_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb,
-                  "plane_fwd": 2 * elem * wb, "plane_mul": 3 * elem * wb}
+    step_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb}
     dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
     alg_bytes = {k: step_bytes[k] * args.steps / max(kernels[k]["launches"], 1) for k in kernels}
     achieved = alg_bytes[dom] / (kernels[dom]["avg_ms"] * 1e-3) / 1e9
@@ -210,7 +265,7 @@ def run_polymul(args, comm, world, rank, local_rank):
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
         # the committed PMC passes were taken on the default 31-bit workload
-        "traffic": traffic_for(dom, batch, args.log_n, Lr) if args.prime_bits == 31 else None,
+        "traffic": traffic_for(dom, "polymul", batch, args.log_n, Lr) if args.prime_bits == 31 else None,
         "alg_bytes_per_launch": alg_bytes[dom],
         # the metric's "% HBM roofline" (3*L*N*8 B per poly-mul)
         "whole_op_GBs": per_gpu * 3 * L * n * wb / 1e9,
@@ -218,6 +273,14 @@ def run_polymul(args, comm, world, rank, local_rank):
         "whole_op_frac_u64_equiv": per_gpu * 3 * L * n * 8 / 1e9 / HBM_PEAK_GBS,
         "kernels": kernels,
     }
+    if "row_mul" in kernels:
+        # the row kernel is VALU-bound: its butterflies (both
+        # forward row transforms and the inverse one) per second of its time
+        log_c = args.log_n - max(args.log_n // 2, 4) if args.log_n >= 8 else args.log_n
+        rb = 3 * elem * log_c // 2 * args.steps / kernels["row_mul"]["launches"]
+        ra = rb / (kernels["row_mul"]["avg_ms"] * 1e-3)
+        roofline["valu"] = {"kernel": "row_mul", "unit": "butterflies/s", "bfly_per_launch": rb,
+                            "achieved": ra, "peak": VALU_PEAK_BFLY, "frac": ra / VALU_PEAK_BFLY}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(mod, n, args.cpu_seconds)
@@ -297,6 +360,8 @@ def run_ctmul(args, comm, world, rank, local_rank):
         step()
     torch.cuda.synchronize()
     comm.barrier()
+    prof_basis = state0[0]  # drop_last views share its tables and profiler
+    prof_basis.profile_enable(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         r = step()
@@ -305,23 +370,59 @@ def run_ctmul(args, comm, world, rank, local_rank):
     comm.barrier()
     elapsed = comm.max(t1 - t0)
     value = B * args.steps / elapsed
+    kernels = {}
+    for k in ("col_fwd", "tensor_rows", "col_inv", "ks_decompose", "ks_rows", "rescale", "elementwise"):
+        cnt, ms = prof_basis.profile_read(k)
+        if cnt:
+            kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
+    prof_basis.profile_enable(False)
 
     parity_ok = None
     cpu = None
+    Lr = state0[2][rank]  # this rank's target limbs
     if rank == 0 and world == 1:
         orc = oracle()
         ob = orc.Basis(mod, n)
-        t = time.perf_counter()
-        o0, _ = orc.mul_ciphertexts_gadget(ob, cts[0][0], cts[1][0], cts[2][0], cts[3][0], key_a, key_b)
-        want0 = orc.rescale(ob, o0)
-        cpu_s = time.perf_counter() - t
-        parity_ok = bool(np.array_equal(pipe.download(r[0])[0], want0))
+        threads = usable_threads()
+        got = pipe.download(r[0])
+        # pair 0 and the batch's last pair (the last key-switch chunk)
+        parity_ok = True
+        for pi in sorted({0, B - 1}):
+            u = pi % uniq
+            o0, _ = orc.mul_ciphertexts_gadget(ob, cts[0][u], cts[1][u], cts[2][u], cts[3][u], key_a, key_b,
+                                               threads=threads)
+            parity_ok &= bool(np.array_equal(got[pi], orc.rescale(ob, o0)))
         if not args.no_cpu_baseline:
-            cpu = {"value": 1.0 / cpu_s, "unit": "ct-muls/s", "cores": 1, "kind": "port",
-                   "sample": f"1 ciphertext pair (N={n}, L={L}) through oracle mul_ciphertexts_gadget "
-                             f"+ rescale of c0, single thread, {cpu_s:.1f} s"}
+            def t_pair(th):
+                t = time.perf_counter()
+                o0, o1 = orc.mul_ciphertexts_gadget(ob, cts[0][0], cts[1][0], cts[2][0], cts[3][0], key_a, key_b,
+                                                    threads=th)
+                orc.rescale(ob, o0), orc.rescale(ob, o1)
+                return time.perf_counter() - t
+            s1 = t_pair(1)
+            sn = t_pair(threads)
+            cpu = {"value": 1.0 / sn, "unit": "ct-muls/s", "cores": threads, "kind": "port",
+                   "sample": f"1 ciphertext pair (N={n}, L={L}) through oracle mul_ciphertexts_gadget + rescale "
+                             f"of c0 and c1, channel-parallel over {threads} threads, {sn:.1f} s",
+                   "single_thread": {"value": 1.0 / s1, "cores": 1, "sample": f"the same pair on one thread, {s1:.1f} s"},
+                   "host": host_info()}
     # bytes per ciphertext: (4L + 2(L-1)) * N * 8
     ct_bytes = (4 * L + 2 * (L - 1)) * n * 8
+    log_c = args.log_n - max(args.log_n // 2, 4)
+    roof = {"bound": "valu", "kernel": "ks_rows", "unit": "butterflies/s", "peak": VALU_PEAK_BFLY,
+            "achieved": None, "frac": None, "traffic": None, "kernels": kernels,
+            "whole_pipeline_hbm": {"unit": "GB/s", "achieved": value / world * ct_bytes / 1e9,
+                                   "peak": HBM_PEAK_GBS,
+                                   "frac": value / world * ct_bytes / 1e9 / HBM_PEAK_GBS}}
+    if "ks_rows" in kernels:
+        # k_ks_rows per ciphertext on this rank: the forward row stages of
+        # alpha_i mod q_j for every (source i, own target j) and the inverse
+        # row stages of both accumulators (L_r target limbs)
+        bfly = B * args.steps * (L * Lr + 2 * Lr) * (n // 2) * log_c
+        ach = bfly / (kernels["ks_rows"]["total_ms"] * 1e-3)
+        roof.update(achieved=ach, frac=ach / VALU_PEAK_BFLY,
+                    bfly_per_launch=bfly / kernels["ks_rows"]["launches"],
+                    traffic=traffic_for("ks_rows", "ctmul", args.ct_batch, args.log_n, L))
     return {
         "metric": CT_METRIC,
         "value": value,
@@ -341,20 +442,28 @@ def run_ctmul(args, comm, world, rank, local_rank):
             "global_batch": B,
             "parallelism": f"limb-sharded x{world}: RCCL all-gather of d2, broadcast of q_L limb",
             "parity_spot_check": parity_ok,
+            "parity_pairs": sorted({0, B - 1}),
         },
-        "roofline": {"bound": "hbm", "kernel": "whole pipeline", "unit": "GB/s",
-                     "achieved": value / world * ct_bytes / 1e9, "peak": HBM_PEAK_GBS,
-                     "frac": value / world * ct_bytes / 1e9 / HBM_PEAK_GBS, "traffic": None},
+        "roofline": roof,
         "cpu_baseline": cpu,
     }
 
 
+def rotation_offsets(args, log_n):
+    n = 1 << log_n
+    if args.rot_offsets == "all":
+        return list(range(1, n // 2))  # every slot offset (one resident key, SURVEY §8d sweep 2)
+    return [1 << e for e in range(log_n - 1)]  # 1 .. N/4: all power-of-two slot offsets
+
+
 def run_rotate(args, comm, world, rank, local_rank):
     """BASELINE config 5: rotate_ciphertext (engine.rs:412-463)
-    over all log2(N/2) power-of-two offsets, reusing one resident rotation
-    key (the arithmetic per offset is identical; one key per offset would be
-    2 GiB each).  Defaults to N = 2^17, L = 32 when --log-n/--limbs are the
-    poly-mul defaults."""
+    over the log2(N/2) power-of-two slot offsets, each with its own gadget
+    rotation key (generate_gadget_rotation_key, engine.rs:348-399: 2 GiB of
+    u64 key per offset in the reference, 1 GiB resident here at u32), or with
+    --rot-offsets all every offset 1..N/2-1 reusing one resident key (the
+    arithmetic per offset is identical).  Defaults to N = 2^17, L = 32 when
+    --log-n/--limbs are the poly-mul defaults."""
     import numpy as np
 
     import rns_ntt as rn
@@ -368,15 +477,27 @@ def run_rotate(args, comm, world, rank, local_rank):
     Bs = rn.RnsBasis(mod, n, device=local_rank)
     B = args.rot_batch
     rng = np.random.default_rng(5 + rank)
-    c0 = rn.RnsPoly.from_channels(uniform(rng, mod, B, n), Bs)
-    c1 = rn.RnsPoly.from_channels(uniform(rng, mod, B, n), Bs)
-    key = rn.RnsGadgetKey.from_channels(uniform(rng, mod, L, n), uniform(rng, mod, L, n), Bs)
-    offsets = [1 << e for e in range(log_n - 1)]  # 1 .. N/4: all power-of-two slot offsets
+    c0_h, c1_h = uniform(rng, mod, B, n), uniform(rng, mod, B, n)
+    c0 = rn.RnsPoly.from_channels(c0_h, Bs)
+    c1 = rn.RnsPoly.from_channels(c1_h, Bs)
+    offsets = rotation_offsets(args, log_n)
+    per_offset = args.rot_keys == "per-offset" and args.rot_offsets == "pow2"
+    # keys: uniform a_i, b_i drawn on the device (the key relation does not
+    # change the arithmetic); key 0 also comes back to the host for the check
+    drng = rn.DeviceRng(99 + rank)
+    nkeys = len(offsets) if per_offset else 1
+    keys, check_key = [], None
+    for i in range(nkeys):
+        ka, kb = rn.RnsPoly.sample_uniform(Bs, drng, L), rn.RnsPoly.sample_uniform(Bs, drng, L)
+        if i == nkeys - 1:  # the key of the checked offset, coefficient domain (before prepare)
+            check_key = (ka.channels(), kb.channels())
+        keys.append(rn.RnsGadgetKey(ka, kb))
     out0, out1 = rn.RnsPoly(Bs, B), rn.RnsPoly(Bs, B)  # reused: the workspace stays allocated
     lib = rn.load()
 
     def step():
-        for k in offsets:
+        for i, k in enumerate(offsets):
+            key = keys[i if per_offset else 0]
             rn.check(lib.rnt_ct_rotate(out0.handle, out1.handle, c0.handle, c1.handle, k,
                                        key.a.handle, key.b.handle))
 
@@ -395,12 +516,50 @@ def run_rotate(args, comm, world, rank, local_rank):
     kernels = {}
     for k in ("ks_decompose", "ks_rows", "col_inv", "automorphism", "col_fwd", "row_fwd"):
         cnt, ms = Bs.profile_read(k)
-        kernels[k] = {"launches": cnt, "avg_ms": ms / cnt if cnt else None, "total_ms": ms}
+        if cnt:
+            kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
     Bs.profile_enable(False)
     rots = B * len(offsets) * args.steps * world
     value = rots / elapsed
-    # forward limb-NTT butterflies per key-switch: L^2 (alpha_i mod q_j) + 2L inverse
-    bfly = (L * L + 2 * L) * (n // 2) * log_n
+    log_c = log_n - max(log_n // 2, 4)
+    # k_ks_rows per rotation: forward row stages of alpha_i mod q_j for all
+    # (i, j) and the inverse row stages of both accumulators
+    bfly_rows = B * len(offsets) * args.steps * (L * L + 2 * L) * (n // 2) * log_c
+    roof = {"bound": "valu", "kernel": "ks_rows", "unit": "butterflies/s", "peak": VALU_PEAK_BFLY,
+            "achieved": None, "frac": None, "traffic": None, "kernels": kernels,
+            "whole_op_bfly_per_s": value / world * (L * L + 2 * L) * (n // 2) * log_n}
+    if "ks_rows" in kernels:
+        ach = bfly_rows / (kernels["ks_rows"]["total_ms"] * 1e-3)
+        roof.update(achieved=ach, frac=ach / VALU_PEAK_BFLY,
+                    bfly_per_launch=bfly_rows / kernels["ks_rows"]["launches"],
+                    traffic=traffic_for("ks_rows", "rotate", B, log_n, L))
+
+    parity_ok = None
+    cpu = None
+    if rank == 0:
+        # the last offset of the sweep, ciphertext 0 and the batch's last one,
+        # against the oracle's rotate_ciphertext (channel-parallel)
+        orc = oracle()
+        ob = orc.Basis(mod, n)
+        threads = usable_threads()
+        ki = len(offsets) - 1
+        key = keys[-1]
+        ka, kb = check_key
+        rn.check(lib.rnt_ct_rotate(out0.handle, out1.handle, c0.handle, c1.handle, offsets[ki],
+                                   key.a.handle, key.b.handle))
+        g0, g1 = out0.channels(), out1.channels()
+        parity_ok = True
+        t = time.perf_counter()
+        for pi in sorted({0, B - 1}):
+            w0, w1 = orc.rotate_ciphertext(ob, c0_h[pi], c1_h[pi], offsets[ki], ka, kb, threads=threads)
+            parity_ok &= bool(np.array_equal(g0[pi], w0) and np.array_equal(g1[pi], w1))
+        sn = (time.perf_counter() - t) / len({0, B - 1})
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = {"value": 1.0 / sn, "unit": "rotations/s", "cores": threads, "kind": "port",
+                   "sample": f"1 rotation (N={n}, L={L}) through oracle rotate_ciphertext (automorphism + "
+                             f"gadget key-switch, engine.rs:412-463), channel-parallel over {threads} threads, "
+                             f"{sn:.1f} s; single thread not run: one rotation is 6L^2 limb NTTs (~{16 * sn:.0f} s)",
+                   "host": host_info()}
     return {
         "metric": ROT_METRIC,
         "value": value,
@@ -413,16 +572,18 @@ def run_rotate(args, comm, world, rank, local_rank):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic (seeded uniform residues and key; one key reused for every offset)",
+        "data": ("synthetic (seeded uniform residues; a distinct device-sampled gadget key per offset)"
+                 if per_offset else "synthetic (seeded uniform residues; one device-sampled key reused for every offset)"),
         "config": {
-            "workload": f"rotate_ciphertext sweep over {len(offsets)} power-of-two offsets, "
+            "workload": f"rotate_ciphertext sweep over {len(offsets)} "
+                        f"{'power-of-two' if args.rot_offsets == 'pow2' else 'slot'} offsets, "
                         f"N=2^{log_n}, L={L} x 31-bit primes, {B} ciphertexts",
+            "keys": len(keys),
             "parallelism": f"replicas x{world} (each GPU its own ciphertexts)",
+            "parity_spot_check": parity_ok,
         },
-        "roofline": {"bound": "valu", "kernel": "ks_rows", "unit": "butterflies/s",
-                     "achieved": value / world * bfly, "peak": None, "frac": None, "traffic": None,
-                     "kernels": kernels},
-        "cpu_baseline": None,
+        "roofline": roof,
+        "cpu_baseline": cpu,
     }
 
 
@@ -558,8 +719,10 @@ def run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod):
                         f"N=2^{log_n}, L={L} x 31-bit primes, {B} ciphertexts (global)",
             "parallelism": f"limb-sharded x{world}: RCCL all-gather of sigma(c1) per offset",
         },
-        "roofline": {"bound": "valu", "kernel": "ks_rows", "unit": "butterflies/s",
-                     "achieved": value / world * bfly, "peak": None, "frac": None, "traffic": None},
+        # whole key-switch butterflies per GPU (no per-kernel events on this path)
+        "roofline": {"bound": "valu", "kernel": "whole key-switch", "unit": "butterflies/s",
+                     "achieved": value / world * bfly, "peak": VALU_PEAK_BFLY,
+                     "frac": value / world * bfly / VALU_PEAK_BFLY, "traffic": None},
         "cpu_baseline": None,
     }
 

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define RNT_ABI_VERSION 2
+#define RNT_ABI_VERSION 3
 
 /* Status codes.  1..6 mirror RnsNttError in order
  * (src/rings/backends/rns_ntt/errors.rs:4-20). */
@@ -61,6 +61,18 @@ typedef struct rnt_buf rnt_buf; /* == device storage of B RnsPoly (poly.rs:25-30
 int rnt_abi_version(void);
 const char* rnt_last_error(void);
 const char* rnt_status_string(int status);
+/* The RnsNttError fields (src/rings/backends/rns_ntt/errors.rs:4-20) of the
+ * calling thread's last failing call, so a binding can rebuild the
+ * reference's variant exactly.  Returns that call's status and writes
+ *   1 InvalidDegree          fields = {degree, 0}
+ *   2 EmptyBasis             fields = {0, 0}
+ *   3 NonNttFriendlyModulus  fields = {modulus, degree}
+ *   4 InvalidModDrop         fields = {drop_count, channel_count}
+ *   5 ChannelCountMismatch   fields = {expected, actual}
+ *   6 NonReducedCoefficient  fields = {coefficient, modulus}
+ * and {0, 0} for the statuses 7..11, which have no reference variant.
+ * 0 (and {0, 0}) if no call on this thread has failed. */
+int rnt_last_error_detail(uint64_t fields[2]);
 
 /* Number of visible HIP devices (0 without a GPU; never fails on CPU-only
  * hosts). */
@@ -111,7 +123,15 @@ int rnt_sync(const rnt_ctx* ctx);
 /* Allocates device storage for n_polys polynomials over ctx's basis, all
  * zero, coefficient domain (RnsPoly::zero, poly.rs:36-43). */
 int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out);
+/* Frees without waiting for the device: the buffer's device blocks go to a
+ * per-device cache behind an event on the context stream, and a later
+ * allocation's stream waits on that event before reusing them. */
 int rnt_buf_free(rnt_buf* buf);
+/* Returns every idle cached block of `device` (-1: all devices) to the HIP
+ * allocator, e.g. before a caller's own allocation that failed is retried;
+ * writes the bytes released when freed_bytes is non-NULL.  The cache holds
+ * at most RNT_WS_POOL_MB MiB (default 1/8 of the device's memory) idle. */
+int rnt_pool_trim(int device, size_t* freed_bytes);
 int rnt_buf_n_polys(const rnt_buf* buf, size_t* n);
 int rnt_buf_is_ntt(const rnt_buf* buf, int* in_ntt); /* is_ntt_domain, poly.rs:127-129 */
 /* RnsPoly::from_channels (poly.rs:73-99) for a batch: host

@@ -49,6 +49,17 @@ static bool throws_kind(F&& f, RnsNttErrorKind kind) {
   return false;
 }
 
+// the error a call throws (kind None-equivalent: BadArgument if none)
+template <class F>
+static RnsNttError caught(F&& f) {
+  try {
+    f();
+  } catch (const RnsNttError& e) {
+    return e;
+  }
+  return RnsNttError(RNT_ERR_BAD_ARGUMENT, "no error thrown");
+}
+
 // the reference's mul_assign_naive (poly.rs:339-367): schoolbook negacyclic
 // product per channel -- a test-side helper, as in the reference
 static std::vector<Poly::Channel> mul_naive(const Poly& a, const Poly& b) {
@@ -280,6 +291,28 @@ int main() {
   run("basis_validation_matches_reference", [] {
     CHECK(throws_kind([] { RnsBasis<8>::create({}); }, RnsNttErrorKind::EmptyBasis));
     CHECK(throws_kind([] { RnsBasis<8>::create({19}); }, RnsNttErrorKind::NonNttFriendlyModulus));
+  });
+
+  run("error_variants_carry_reference_fields", [] {
+    // errors.rs:4-20: the struct variants' payloads cross the C-ABI
+    // (rnt_last_error_detail) and come back with the reference's meaning
+    std::vector<Poly::Channel> bad(2);
+    bad[0].fill(3);
+    bad[0][5] = 17;
+    bad[1].fill(0);
+    auto e = caught([&] { Poly::from_channels(bad, basis_17_97(), false); });
+    CHECK(e.kind == RnsNttErrorKind::NonReducedCoefficient && e.coefficient == 17 && e.modulus == 17);
+    std::vector<Poly::Channel> one(1);
+    one[0].fill(0);
+    e = caught([&] { Poly::from_channels(one, basis_17_97(), false); });
+    CHECK(e.kind == RnsNttErrorKind::ChannelCountMismatch && e.expected == 2 && e.actual == 1);
+    e = caught([] { RnsBasis<8>::create({19}); });
+    CHECK(e.kind == RnsNttErrorKind::NonNttFriendlyModulus && e.modulus == 19 && e.degree == 8);
+    e = caught([] { basis_17_97()->drop_last(2); });
+    CHECK(e.kind == RnsNttErrorKind::InvalidModDrop && e.drop_count == 2 && e.channel_count == 2);
+    Poly single = Poly::from_coeffs(std::array<int64_t, 8>{1, 2, 3, 4, 5, 6, 7, 8}, RnsBasis<8>::create({17}));
+    e = caught([&] { single.rescale(); });
+    CHECK(e.kind == RnsNttErrorKind::InvalidModDrop && e.drop_count == 1 && e.channel_count == 1);
   });
 
   // ---- CkksEncoder (ckks_encoder.rs:161-228 tests), on the device --------

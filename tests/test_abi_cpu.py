@@ -26,7 +26,7 @@ def declared_functions():
 
 def test_library_loads_and_exports_every_declared_symbol():
     lib = rns_ntt.load()
-    assert lib.rnt_abi_version() == 2
+    assert lib.rnt_abi_version() == 3
     names = declared_functions()
     assert len(names) >= 35
     for n in names:
@@ -94,13 +94,38 @@ def test_ctx_validation_errors_without_gpu(kats):
     assert lib.rnt_ctx_create(3, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), 0, 0, ctypes.byref(h)) == 2
     with pytest.raises(rns_ntt.RnsNttError) as e:
         rns_ntt.RnsBasis([], 8)
-    assert e.value.kind == "EmptyBasis"
+    assert e.value.kind == "EmptyBasis" and e.value.fields == {}
+    bad = kats["basis_n8"]["rejects_non_friendly_modulus"]["modulus"]
     with pytest.raises(rns_ntt.RnsNttError) as e:
-        rns_ntt.RnsBasis([kats["basis_n8"]["rejects_non_friendly_modulus"]["modulus"]], 8)
+        rns_ntt.RnsBasis([bad], 8)
+    # NonNttFriendlyModulus { modulus, degree } (errors.rs:9-10, basis.rs:26-29)
     assert e.value.kind == "NonNttFriendlyModulus"
+    assert e.value.fields == {"modulus": bad, "degree": 8} and e.value.modulus == bad
     with pytest.raises(rns_ntt.RnsNttError) as e:
         rns_ntt.RnsBasis([17], 12)
-    assert e.value.kind == "InvalidDegree"
+    assert e.value.kind == "InvalidDegree" and e.value.fields == {"degree": 12}
+    q18 = rns_ntt.generate_primes(31, 1, 1 << 18)[0]
     with pytest.raises(rns_ntt.RnsNttError) as e:
-        rns_ntt.RnsBasis([rns_ntt.generate_primes(31, 1, 1 << 18)[0]], 1 << 18)
+        rns_ntt.RnsBasis([q18], 1 << 18)
     assert e.value.kind == "InvalidDegree"  # beyond this backend's 2^17 limit
+    assert e.value.fields == {"degree": 1 << 18}
+
+
+def test_error_detail_through_the_abi():
+    """rnt_last_error_detail returns the failing call's status and the
+    reference variant's fields (errors.rs:4-20), per thread."""
+    lib = rns_ntt.load()
+    f = (ctypes.c_uint64 * 2)()
+    psi = ctypes.c_uint64()
+    assert lib.rnt_find_psi(19, 8, ctypes.byref(psi)) == 3
+    assert lib.rnt_last_error_detail(f) == 3 and (f[0], f[1]) == (19, 8)
+    assert lib.rnt_find_psi(17, 12, ctypes.byref(psi)) == 1
+    assert lib.rnt_last_error_detail(f) == 1 and (f[0], f[1]) == (12, 0)
+    assert lib.rnt_last_error_detail(None) == 1
+    # a failure without a reference variant clears the fields
+    assert lib.rnt_find_psi(17, 8, None) == 11
+    assert lib.rnt_last_error_detail(f) == 11 and (f[0], f[1]) == (0, 0)
+    # equality compares variant and payload, like the reference's PartialEq
+    a = rns_ntt.RnsNttError(6, "x", {"coefficient": 17, "modulus": 17})
+    assert a == rns_ntt.RnsNttError(6, "y", {"coefficient": 17, "modulus": 17})
+    assert a != rns_ntt.RnsNttError(6, "x", {"coefficient": 18, "modulus": 17})

@@ -1,0 +1,156 @@
+"""The C-ABI boundary on the device: the reference's error payloads, the
+device block cache (buffers freed without a host wait, their blocks reused
+by later allocations on the same or another stream), and every runtime knob
+the library still reads, each on its non-default setting, bit-exact against
+the oracle.
+
+Knobs (read when a context is created, or per call for the cache cap):
+* RNT_LAZY30=0   -- 30-bit bases take the canonical product path instead of
+                    the Harvey-lazy one;
+* RNT_KS_WS_MB   -- key-switch scratch cap: 1 MiB cuts a config-3-shaped
+                    batch into one ciphertext per chunk;
+* RNT_WS_POOL_MB -- idle bytes the device cache keeps: 0 releases every
+                    freed block at once;
+* RNT_DEC_JG     -- covered by test_gpu_configs.py::test_decomposition_groups.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import pyoracle as orc
+
+pytestmark = pytest.mark.gpu
+
+T = orc.host_threads()
+
+
+def _rand(rng, mod, n, batch=None):
+    return orc.uniform_poly(mod, n, rng, batch=batch)
+
+
+def test_error_payloads_match_reference_variants(gpu):
+    """errors.rs:4-20 struct variants, rebuilt from rnt_last_error_detail."""
+    rn = gpu
+    Bd = rn.RnsBasis([17, 97], 8)
+    bad = np.zeros((2, 8), dtype=np.uint64)
+    bad[1, 3] = 100  # not reduced modulo 97 (poly.rs:83-93)
+    with pytest.raises(rn.RnsNttError) as e:
+        rn.RnsPoly.from_channels(bad, Bd)
+    assert e.value.kind == "NonReducedCoefficient"
+    assert e.value.fields == {"coefficient": 100, "modulus": 97}
+    with pytest.raises(rn.RnsNttError) as e:
+        rn.RnsPoly.from_channels(np.zeros((1, 8), dtype=np.uint64), Bd)
+    assert e.value.fields == {"expected": 2, "actual": 1} and e.value.kind == "ChannelCountMismatch"
+    with pytest.raises(rn.RnsNttError) as e:
+        Bd.drop_last(2)  # basis.rs:121-134
+    assert e.value.kind == "InvalidModDrop" and e.value.fields == {"drop_count": 2, "channel_count": 2}
+    one = rn.RnsPoly.from_channels(np.ones((1, 8), dtype=np.uint64), rn.RnsBasis([17], 8))
+    with pytest.raises(rn.RnsNttError) as e:
+        one.rescale()  # poly.rs:191-197
+    assert e.value.kind == "InvalidModDrop" and e.value.fields == {"drop_count": 1, "channel_count": 1}
+    # the gadget key must hold one poly per channel
+    d = rn.RnsPoly.from_channels(_rand(np.random.default_rng(1), [17, 97], 8, 1), Bd)
+    key = rn.RnsGadgetKey.from_channels(np.zeros((1, 2, 8), np.uint64), np.zeros((1, 2, 8), np.uint64), Bd)
+    with pytest.raises(rn.RnsNttError) as e:
+        rn.keyswitch(d, key)
+    assert e.value.kind == "ChannelCountMismatch" and e.value.fields == {"expected": 2, "actual": 1}
+
+
+def test_freed_blocks_are_reused_without_host_wait(gpu):
+    """Buffers freed while their kernels may still be queued hand their
+    blocks to later allocations; results and zero-initialisation stay exact.
+    A second context (its own stream) takes blocks freed on the first."""
+    rn = gpu
+    lib = rn.load()
+    n, L = 1 << 12, 4
+    mod = rn.generate_primes(31, L, n)
+    Bd, Bo = rn.RnsBasis(mod, n), orc.Basis(mod, n)
+    other = rn.RnsBasis(mod, n)  # same moduli, another stream
+    rng = np.random.default_rng(7)
+    a_h, b_h = _rand(rng, mod, n, 8), _rand(rng, mod, n, 8)
+    want = np.stack([orc.mul(Bo, a_h[i], b_h[i]) for i in range(8)])
+    a, b = rn.RnsPoly.from_channels(a_h, Bd), rn.RnsPoly.from_channels(b_h, Bd)
+    for it in range(6):
+        out = rn.RnsPoly(Bd, 8)  # fresh output (and workspace) each time
+        rn.check(lib.rnt_mul(out.handle, a.handle, b.handle))
+        if it % 2:
+            got = out.channels()
+            assert np.array_equal(got, want), it
+        del out  # freed right after queueing its product: no host wait
+        z = rn.RnsPoly(other if it % 3 == 0 else Bd, 8)  # takes the freed block
+        assert not z.channels().any(), it  # RnsPoly::zero
+        del z
+    freed = rn.pool_trim()
+    assert freed > 0
+    assert rn.pool_trim() == 0
+
+
+def test_pool_cap_zero_releases_every_block(gpu, monkeypatch):
+    """RNT_WS_POOL_MB=0: no idle block is kept; a ct-mul loop that makes
+    fresh outputs every step stays exact."""
+    rn = gpu
+    monkeypatch.setenv("RNT_WS_POOL_MB", "0")
+    n, L, B = 1 << 12, 4, 2
+    mod = rn.generate_primes(31, L, n)
+    Bd, Bo = rn.RnsBasis(mod, n), orc.Basis(mod, n)
+    rng = np.random.default_rng(8)
+    c = [_rand(rng, mod, n, B) for _ in range(4)]
+    ka, kb = _rand(rng, mod, n, L), _rand(rng, mod, n, L)
+    rlk = rn.RnsGadgetKey.from_channels(ka, kb, Bd)
+    up = lambda x: rn.RnsPoly.from_channels(x, Bd)  # noqa: E731
+    w0, w1 = orc.mul_ciphertexts_gadget(Bo, c[0][1], c[1][1], c[2][1], c[3][1], ka, kb)
+    for _ in range(3):
+        out = rn.mul_ciphertexts_gadget(rn.Ciphertext(up(c[0]), up(c[1])), rn.Ciphertext(up(c[2]), up(c[3])), rlk)
+        assert np.array_equal(out.c0.channels()[1], w0) and np.array_equal(out.c1.channels()[1], w1)
+        del out
+    assert rn.pool_trim() == 0  # nothing was kept
+
+
+def test_lazy30_off_takes_canonical_path(gpu, monkeypatch):
+    """RNT_LAZY30=0 on a 30-bit basis: the canonical 31-bit product kernels
+    run instead of the Harvey-lazy ones; products stay bit-exact."""
+    rn = gpu
+    monkeypatch.setenv("RNT_LAZY30", "0")
+    n, L = 1 << 14, 6
+    mod = rn.generate_primes(30, L, n)
+    Bd, Bo = rn.RnsBasis(mod, n), orc.Basis(mod, n)
+    q = np.array(mod, dtype=np.uint64)[:, None]
+    rng = np.random.default_rng(30)
+    full = np.broadcast_to(q - 1, (L, n)).copy()
+    x = np.stack([_rand(rng, mod, n), full, _rand(rng, mod, n)])
+    y = np.stack([_rand(rng, mod, n), full, full])
+    got = (rn.RnsPoly.from_channels(x, Bd) * rn.RnsPoly.from_channels(y, Bd)).channels()
+    for i in range(3):
+        assert np.array_equal(got[i], orc.mul(Bo, x[i], y[i])), i
+
+
+def test_small_keyswitch_scratch_chunks_every_ciphertext(gpu, monkeypatch):
+    """RNT_KS_WS_MB=1 at N=2^12, L=8 (S per ciphertext = 1 MiB): each
+    ciphertext is its own key-switch chunk, for the relinearisation and for
+    a limb shard's keyswitch_ext."""
+    rn = gpu
+    monkeypatch.setenv("RNT_KS_WS_MB", "1")
+    n, L, B = 1 << 12, 8, 3
+    mod = rn.generate_primes(31, L, n)
+    Bd, Bo = rn.RnsBasis(mod, n), orc.Basis(mod, n)
+    rng = np.random.default_rng(12)
+    c = [_rand(rng, mod, n, B) for _ in range(4)]
+    ka, kb = _rand(rng, mod, n, L), _rand(rng, mod, n, L)
+    rlk = rn.RnsGadgetKey.from_channels(ka, kb, Bd)
+    up = lambda x: rn.RnsPoly.from_channels(x, Bd)  # noqa: E731
+    out = rn.mul_ciphertexts_gadget(rn.Ciphertext(up(c[0]), up(c[1])), rn.Ciphertext(up(c[2]), up(c[3])), rlk)
+    o0, o1 = out.c0.channels(), out.c1.channels()
+    for p in range(B):
+        w0, w1 = orc.mul_ciphertexts_gadget(Bo, c[0][p], c[1][p], c[2][p], c[3][p], ka, kb)
+        assert np.array_equal(o0[p], w0) and np.array_equal(o1[p], w1), p
+    Lt = 3
+    Bt = rn.RnsBasis(mod[:Lt], n)
+    key_t = rn.RnsGadgetKey.from_channels(np.ascontiguousarray(ka[:, :Lt]), np.ascontiguousarray(kb[:, :Lt]), Bt)
+    d = up(c[1])
+    ptr, _ = d.device_ptr()
+    a0, a1 = rn.keyswitch_ext(ptr, L, key_t, Bt, B)
+    g0, g1 = a0.channels(), a1.channels()
+    for p in range(B):
+        w0, w1 = orc.keyswitch(Bo, c[1][p], ka, kb)
+        assert np.array_equal(g0[p], w0[:Lt]) and np.array_equal(g1[p], w1[:Lt]), p

@@ -1,7 +1,8 @@
 #!/bin/bash
-# One gpurun call: GPU parity tests, smoke, short bench, rocprofv3 kernel
-# trace.  Every GPU step has its own time limit; any failing step stops the
-# script (a failed parity test may be a device fault: start nothing more).
+# One gpurun call: GPU parity tests, smoke, the bench workloads, and
+# (PROFILE=1) a rocprofv3 kernel trace.  Every GPU step has its own time
+# limit; any failing step stops the script (a failed parity test may be a
+# device fault: start nothing more).
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -19,11 +20,13 @@ step() {  # step <name> <seconds> <cmd...>
   fi
   return 0
 }
-step pytest_gpu 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+if [ "${TESTS:-1}" = "1" ]; then
+  step pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
 step bench 600 python bench.py --steps 20 --warmup 3
-step bench_ctmul 900 python bench.py --workload ctmul --ct-batch ${CT_BATCH:-32} --steps 3 --warmup 1
-step bench_rotate 900 python bench.py --workload rotate --rot-batch ${ROT_BATCH:-4} --steps 2 --warmup 1
-if [ "${PROFILE:-1}" = "1" ]; then
+step bench_ctmul 900 python bench.py --workload ctmul --ct-batch ${CT_BATCH:-128} --steps 3 --warmup 1
+step bench_rotate 900 python bench.py --workload rotate --rot-batch ${ROT_BATCH:-8} --steps 2 --warmup 1
+if [ "${PROFILE:-0}" = "1" ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof" -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
 fi

@@ -10,19 +10,27 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-NAMES = {"k_colt_fwd<unsigned int, 8, 6, false>": "col_fwd", "k_row<unsigned int, 2, 8, false>": "row_mul",
-         "k_colt_inv<unsigned int, 8, 6, false>": "col_inv"}
+# u32 kernels -> bench.py's kernel ids (k_row's second template argument is
+# its mode: 0 forward rows, 1 inverse rows, 2 poly-mul rows)
+FN = {"k_colt_fwd": "col_fwd", "k_colt_inv": "col_inv", "k_ks_rows": "ks_rows",
+      "k_colt_decompose": "ks_decompose", "k_tensor_rows": "tensor_rows",
+      "k_automorph_odd": "automorphism", "k_rescale": "rescale"}
+ROW_MODES = {"0": "row_fwd", "1": "row_inv", "2": "row_mul"}
 
 
 def short(kname):
-    for k, v in NAMES.items():
-        if k in kname:
-            return v
-    return None
+    m = re.search(r"(k_\w+)<([^>]*)>", kname)
+    if not m or not m.group(2).startswith("unsigned int"):
+        return None
+    fn, targs = m.group(1), [t.strip() for t in m.group(2).split(",")]
+    if fn == "k_row":
+        return ROW_MODES.get(targs[1])
+    return FN.get(fn)
 
 
 def counters(d):
@@ -42,7 +50,9 @@ def counters(d):
 
 
 def main():
+    # pmc_summary.py <prof_dir> <tag> [workload batch log_n L]
     prof, tag = sys.argv[1], sys.argv[2]
+    workload, batch, log_n, L = (sys.argv[3:7] + ["polymul", "256", "16", "16"][len(sys.argv[3:7]):])
     res = collections.defaultdict(dict)
     for sub in ("fetch", "write", "sq", "grbm"):
         for k, d in counters(os.path.join(prof, sub)).items():
@@ -71,11 +81,22 @@ def main():
             e["frac_issue_stall"] = d.get("SQ_WAIT_INST_ANY", 0) / w
             e["frac_waitcnt_barrier"] = d.get("SQ_WAIT_ANY", 0) / w
         kernels[k] = e
-    meta = {"batch": 256, "log_n": 16, "L": 16, "source": f"tools/profile_run.sh {tag}", "kernels": kernels}
+    meta = {"workload": workload, "batch": int(batch), "log_n": int(log_n), "L": int(L),
+            "source": f"tools/profile_run.sh {tag}", "kernels": kernels}
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc.json"), "w") as f:
         json.dump(meta, f, indent=1)
-    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
-        json.dump(meta, f, indent=1)
+    # profiles/pmc_traffic.json: one entry per workload shape (bench.py
+    # roofline.traffic); a new pass of the same shape replaces the old one
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    entries = []
+    if os.path.exists(tpath):
+        old = json.load(open(tpath))
+        entries = old.get("entries", [dict(old, workload="polymul")] if "kernels" in old else [])
+    key = (workload, int(batch), int(log_n), int(L))
+    entries = [e for e in entries if (e.get("workload"), e.get("batch"), e.get("log_n"), e.get("L")) != key]
+    entries.append(meta)
+    with open(tpath, "w") as f:
+        json.dump({"entries": entries}, f, indent=1)
     for k, e in kernels.items():
         print(k, {x: (round(y, 3) if isinstance(y, float) else y) for x, y in e.items()})
 

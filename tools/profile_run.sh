@@ -1,9 +1,13 @@
 #!/bin/bash
-# profile_run.sh <tag>: rocprofv3 kernel-trace stats of the default bench,
-# then separate PMC passes (no tracing domains combined with --pmc) at the
-# same batch.  Every GPU step has its own time limit; any failure stops.
+# profile_run.sh <tag> [bench args...]: rocprofv3 kernel-trace stats of the
+# bench (default workload unless args say otherwise), then separate PMC
+# passes (no tracing domains combined with --pmc) of the same command.
+# Every GPU step has its own time limit; any failure stops.  Summarise on
+# the CPU afterwards: tools/pmc_summary.py gpurun_out/prof_<tag> <tag>
+# <workload> <batch> <log_n> <L>.
 set -o pipefail
-TAG=${1:-r01}
+TAG=${1:-r02}
+shift
 mkdir -p gpurun_out/prof_$TAG
 export TMPDIR=/tmp
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -16,7 +20,7 @@ step() {  # step <name> <seconds> <cmd...>
   echo "== $name rc=$rc" >&2
   if [ $rc -ne 0 ]; then tail -20 "$OUT/$name.err" >&2; exit $rc; fi
 }
-BENCH="bench.py --steps 5 --warmup 2 --no-cpu-baseline"
+BENCH="bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline $*"
 step trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $BENCH
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $BENCH

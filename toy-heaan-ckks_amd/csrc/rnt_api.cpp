@@ -23,14 +23,35 @@
 namespace {
 
 thread_local std::string g_last_error;
+// the RnsNttError fields of the last failure (rnt_last_error_detail)
+struct ErrDetail {
+  int status;
+  uint64_t a, b;
+};
+thread_local ErrDetail g_last_detail{0, 0, 0};
+
+int vfail(int code, uint64_t a, uint64_t b, const char* fmt, va_list ap) {
+  char buf[512];
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  g_last_error = buf;
+  g_last_detail = {code, a, b};
+  return code;
+}
 
 int fail(int code, const char* fmt, ...) {
-  char buf[512];
   va_list ap;
   va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
+  vfail(code, 0, 0, fmt, ap);
   va_end(ap);
-  g_last_error = buf;
+  return code;
+}
+
+// A failure that carries the reference variant's fields (errors.rs:4-20).
+int fail_fields(int code, uint64_t a, uint64_t b, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfail(code, a, b, fmt, ap);
+  va_end(ap);
   return code;
 }
 
@@ -51,7 +72,7 @@ inline size_t word_bytes(const rnt::Tables* t) { return t->wide ? 8 : 4; }
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
-    "plane_fwd", "plane_mul", "sfft", "sample"};
+    "sfft", "sample"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -104,138 +125,211 @@ int set_device(const rnt_ctx* ctx) {
   return RNT_OK;
 }
 
-// Workspace blocks of freed buffers, kept per device for reuse.  A caller
-// that makes fresh output buffers every step (the limb-sharded pipeline)
-// then reuses the same gigabytes of key-switch scratch instead of a
-// hipMalloc / hipFree of them per call; that churn made a long ct-mul run
-// fall to ~1/15 of its rate after ~30 steps at 128 ciphertexts.  Each live
-// buffer still owns its block exclusively, and a block is only pooled once
-// its buffer's stream has drained.  RNT_WS_POOL_MB caps the idle bytes.
-struct WsBlock {
+// Device block cache: the data, workspace and staging blocks of freed
+// buffers, kept per device for reuse.  A caller that makes fresh buffers
+// every step (the limb-sharded pipeline) then reuses the same gigabytes
+// instead of a hipMalloc / hipFree per call; that churn made a long ct-mul
+// run fall to ~1/15 of its rate after ~30 steps at 128 ciphertexts.
+// A freed block carries an event recorded on the stream of its last use.
+// The next taker's stream waits on that event (hipStreamWaitEvent), so no
+// free makes the host wait for the device; only a block leaving the cache
+// (hipFree) waits for its event first.  Idle bytes per device are capped at
+// RNT_WS_POOL_MB, by default 1/8 of the device's memory.
+struct PoolBlock {
   int device;
   void* p;
   size_t bytes;
+  hipEvent_t ev;     // recorded on `s` when the block was freed
+  hipStream_t s;
 };
-std::mutex g_ws_mu;
-std::vector<WsBlock> g_ws_pool;  // oldest first
-size_t g_ws_pool_bytes = 0;
+std::mutex g_pool_mu;
+std::vector<PoolBlock> g_pool;               // oldest first
+std::vector<std::pair<int, size_t>> g_pool_bytes;  // idle bytes per device
+std::vector<hipEvent_t> g_free_events;       // recycled events
 
-static size_t ws_pool_cap() {
-  static const size_t cap = [] {
-    const char* e = getenv("RNT_WS_POOL_MB");
-    const long mb = e ? atol(e) : 65536L;
+static size_t& pool_bytes_of(int device) {  // g_pool_mu held
+  for (auto& e : g_pool_bytes)
+    if (e.first == device) return e.second;
+  g_pool_bytes.push_back({device, 0});
+  return g_pool_bytes.back().second;
+}
+
+static size_t pool_cap(int device) {  // g_pool_mu held
+  if (const char* e = getenv("RNT_WS_POOL_MB")) {  // read per call: tests set it
+    const long mb = atol(e);
     return (size_t)(mb > 0 ? mb : 0) << 20;
-  }();
+  }
+  static std::vector<std::pair<int, size_t>> caps;  // default: 1/8 of the device
+  for (auto& c : caps)
+    if (c.first == device) return c.second;
+  size_t free_b = 0, total_b = 0;
+  const size_t cap = hipMemGetInfo(&free_b, &total_b) == hipSuccess ? total_b / 8 : ((size_t)8 << 30);
+  caps.push_back({device, cap});
   return cap;
 }
 
-// Smallest idle block on `device` of at least `bytes`, or nullptr.
-static void* ws_take(int device, size_t bytes, size_t* got) {
-  std::lock_guard<std::mutex> lk(g_ws_mu);
-  size_t best = g_ws_pool.size();
-  for (size_t i = 0; i < g_ws_pool.size(); ++i) {
-    const WsBlock& w = g_ws_pool[i];
-    if (w.device == device && w.bytes >= bytes &&
-        (best == g_ws_pool.size() || w.bytes < g_ws_pool[best].bytes))
-      best = i;
+static void pool_release(const PoolBlock& w) {  // g_pool_mu NOT held
+  (void)hipSetDevice(w.device);
+  if (w.ev) {
+    (void)hipEventSynchronize(w.ev);
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_free_events.push_back(w.ev);
   }
-  if (best == g_ws_pool.size()) return nullptr;
-  void* p = g_ws_pool[best].p;
-  *got = g_ws_pool[best].bytes;
-  g_ws_pool_bytes -= *got;
-  g_ws_pool.erase(g_ws_pool.begin() + (long)best);
-  return p;
+  (void)hipFree(w.p);
 }
 
-// Hand an idle block (its stream drained) to the pool; the oldest blocks
-// are freed while the pool would exceed its cap.
-static void ws_give(int device, void* p, size_t bytes) {
-  if (!p) return;
-  std::vector<WsBlock> drop;
+// Smallest idle block on `device` of at least `bytes` (and at most twice
+// that, so a small request does not pin a multi-GiB block), made safe to use
+// on stream `s`; nullptr if none.
+static void* pool_take(int device, size_t bytes, hipStream_t s, size_t* got) {
+  PoolBlock w{};
   {
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    g_ws_pool.push_back({device, p, bytes});
-    g_ws_pool_bytes += bytes;
-    while (g_ws_pool_bytes > ws_pool_cap() && !g_ws_pool.empty()) {
-      drop.push_back(g_ws_pool.front());
-      g_ws_pool_bytes -= g_ws_pool.front().bytes;
-      g_ws_pool.erase(g_ws_pool.begin());
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    size_t best = g_pool.size();
+    for (size_t i = 0; i < g_pool.size(); ++i) {
+      const PoolBlock& c = g_pool[i];
+      if (c.device == device && c.bytes >= bytes && c.bytes / 2 <= bytes &&
+          (best == g_pool.size() || c.bytes < g_pool[best].bytes))
+        best = i;
+    }
+    if (best == g_pool.size()) return nullptr;
+    w = g_pool[best];
+    pool_bytes_of(device) -= w.bytes;
+    g_pool.erase(g_pool.begin() + (long)best);
+  }
+  if (w.ev) {
+    // same stream: stream order already covers the last use
+    if (w.s != s && hipStreamWaitEvent(s, w.ev, 0) != hipSuccess) (void)hipEventSynchronize(w.ev);
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_free_events.push_back(w.ev);
+  }
+  *got = w.bytes;
+  return w.p;
+}
+
+// Hand a block whose last use was queued on stream `s` to the cache; the
+// oldest idle blocks of the device leave it while it is over its cap.
+static void pool_give(int device, void* p, size_t bytes, hipStream_t s) {
+  if (!p) return;
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (!g_free_events.empty()) {
+      ev = g_free_events.back();
+      g_free_events.pop_back();
     }
   }
-  for (const WsBlock& w : drop) {
-    (void)hipSetDevice(w.device);
-    (void)hipFree(w.p);
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+  if (ev && hipEventRecord(ev, s) != hipSuccess) {
+    (void)hipStreamSynchronize(s);  // no event: drain instead
+    (void)hipEventDestroy(ev);
+    ev = nullptr;
+  } else if (!ev) {
+    (void)hipStreamSynchronize(s);
   }
-  if (!drop.empty()) (void)hipSetDevice(device);
-}
-
-// Free every idle block of `device` (before retrying a failed allocation).
-static void ws_drain(int device) {
-  std::vector<WsBlock> drop;
+  std::vector<PoolBlock> drop;
   {
-    std::lock_guard<std::mutex> lk(g_ws_mu);
-    for (size_t i = 0; i < g_ws_pool.size();) {
-      if (g_ws_pool[i].device == device) {
-        drop.push_back(g_ws_pool[i]);
-        g_ws_pool_bytes -= g_ws_pool[i].bytes;
-        g_ws_pool.erase(g_ws_pool.begin() + (long)i);
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool.push_back({device, p, bytes, ev, s});
+    size_t& idle = pool_bytes_of(device);
+    idle += bytes;
+    const size_t cap = pool_cap(device);
+    for (size_t i = 0; idle > cap && i < g_pool.size();) {
+      if (g_pool[i].device == device) {
+        drop.push_back(g_pool[i]);
+        idle -= g_pool[i].bytes;
+        g_pool.erase(g_pool.begin() + (long)i);
       } else {
         ++i;
       }
     }
   }
-  for (const WsBlock& w : drop) (void)hipFree(w.p);
+  for (const PoolBlock& w : drop) pool_release(w);
+  if (!drop.empty()) (void)hipSetDevice(device);
+}
+
+// Free every idle block of `device` (-1: of every device).
+static size_t pool_drain(int device) {
+  std::vector<PoolBlock> drop;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_pool.size();) {
+      if (device < 0 || g_pool[i].device == device) {
+        drop.push_back(g_pool[i]);
+        pool_bytes_of(g_pool[i].device) -= g_pool[i].bytes;
+        g_pool.erase(g_pool.begin() + (long)i);
+      } else {
+        ++i;
+      }
+    }
+  }
+  size_t freed = 0;
+  for (const PoolBlock& w : drop) {
+    freed += w.bytes;
+    pool_release(w);
+  }
+  return freed;
+}
+
+// A device block of at least `bytes` for work on stream `s`: from the cache,
+// else hipMalloc (after emptying the device's cache if that fails).
+static hipError_t pool_malloc(int device, size_t bytes, hipStream_t s, void** p, size_t* got) {
+  if ((*p = pool_take(device, bytes, s, got))) return hipSuccess;
+  hipError_t e = hipMalloc(p, bytes);
+  if (e == hipErrorOutOfMemory) {
+    (void)hipGetLastError();
+    if (pool_drain(device) > 0) {
+      (void)hipSetDevice(device);
+      e = hipMalloc(p, bytes);
+    }
+  }
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return e;
+  }
+  *got = bytes;
+  return hipSuccess;
 }
 
 // Grow the buffer's private workspace to at least `bytes`.
 int ensure_ws(rnt_buf* b, size_t bytes) {
   if (b->ws_bytes >= bytes) return RNT_OK;
   const int dev = b->ctx->t->device;
+  hipStream_t s = b->ctx->t->stream;
   if (b->ws) {
-    // the stream may still be using the old workspace
-    HIP_TRY(hipStreamSynchronize(b->ctx->t->stream), "hipStreamSynchronize");
-    ws_give(dev, b->ws, b->ws_bytes);
+    pool_give(dev, b->ws, b->ws_bytes, s);  // the stream may still be using it
     b->ws = nullptr;
     b->ws_bytes = 0;
   }
   size_t got = 0;
-  if (void* p = ws_take(dev, bytes, &got)) {
-    b->ws = p;
-    b->ws_bytes = got;
-    return RNT_OK;
-  }
-  hipError_t e = hipMalloc(&b->ws, bytes);
-  if (e == hipErrorOutOfMemory) {
-    (void)hipGetLastError();
-    ws_drain(dev);
-    e = hipMalloc(&b->ws, bytes);
-  }
-  if (e != hipSuccess) {
-    b->ws = nullptr;
+  if (hipError_t e = pool_malloc(dev, bytes, s, &b->ws, &got); e != hipSuccess)
     return hip_fail(e, "hipMalloc(workspace)");
-  }
-  b->ws_bytes = bytes;
+  b->ws_bytes = got;
   return RNT_OK;
 }
 
 int ensure_stage(rnt_buf* b, size_t bytes) {
   if (b->stage_bytes >= bytes) return RNT_OK;
+  const int dev = b->ctx->t->device;
+  hipStream_t s = b->ctx->t->stream;
   if (b->stage) {
-    HIP_TRY(hipStreamSynchronize(b->ctx->t->stream), "hipStreamSynchronize");
-    HIP_TRY(hipFree(b->stage), "hipFree");
+    pool_give(dev, b->stage, b->stage_bytes, s);
     b->stage = nullptr;
     b->stage_bytes = 0;
   }
-  HIP_TRY(hipMalloc(&b->stage, bytes), "hipMalloc(stage)");
-  b->stage_bytes = bytes;
+  size_t got = 0;
+  if (hipError_t e = pool_malloc(dev, bytes, s, &b->stage, &got); e != hipSuccess)
+    return hip_fail(e, "hipMalloc(stage)");
+  b->stage_bytes = got;
   return RNT_OK;
 }
 
-// Staging for uploads/downloads is cached per buffer, except very large
-// ones (a 256-poly batch at N=2^16, L=16 stages 2 GiB of u64).
+// Staging for uploads/downloads stays with its buffer, except very large
+// ones (a 256-poly batch at N=2^16, L=16 stages 2 GiB of u64), which go back
+// to the cache.
 void trim_stage(rnt_buf* b) {
   if (b->stage_bytes > ((size_t)256 << 20)) {
-    (void)hipFree(b->stage);
+    pool_give(b->ctx->t->device, b->stage, b->stage_bytes, b->ctx->t->stream);
     b->stage = nullptr;
     b->stage_bytes = 0;
   }
@@ -277,20 +371,10 @@ rnt::Tables::~Tables() {
     (void)hipStreamSynchronize(stream);
     (void)hipStreamDestroy(stream);
   }
-  for (int i = 0; i < kAux; ++i) {
-    if (aux[i]) {
-      (void)hipStreamSynchronize(aux[i]);
-      (void)hipStreamDestroy(aux[i]);
-    }
-    if (join_ev[i]) (void)hipEventDestroy(join_ev[i]);
-  }
-  if (fork_ev) (void)hipEventDestroy(fork_ev);
   for (auto& e : resc_ext) (void)hipFree(e.second);
   for (auto& e : crt_cache) (void)hipFree(e.second.dev);
   (void)hipFree(tw_fwd);
   (void)hipFree(tw_inv);
-  (void)hipFree(mtw_fwd);
-  (void)hipFree(mtw_inv);
   (void)hipFree(sfft_tw);
   (void)hipFree(lconst);
   (void)hipFree(resc);
@@ -311,6 +395,14 @@ static long env_long(const char* name, long dflt);
 // diagnostics
 // ---------------------------------------------------------------------------
 extern "C" int rnt_abi_version(void) { return RNT_ABI_VERSION; }
+extern "C" int rnt_last_error_detail(uint64_t fields[2]) {
+  if (fields) {
+    fields[0] = g_last_detail.a;
+    fields[1] = g_last_detail.b;
+  }
+  return g_last_detail.status;
+}
+
 extern "C" const char* rnt_last_error(void) { return g_last_error.c_str(); }
 extern "C" const char* rnt_status_string(int s) {
   switch (s) {
@@ -354,9 +446,11 @@ extern "C" int rnt_generate_primes(uint32_t bit_size, size_t count, uint64_t deg
 extern "C" int rnt_find_psi(uint64_t modulus, uint64_t degree, uint64_t* psi) {
   if (!psi) return fail(RNT_ERR_BAD_ARGUMENT, "null out");
   if (degree == 0 || (degree & (degree - 1)))
-    return fail(RNT_ERR_INVALID_DEGREE, "ring degree must be a power of two, got %" PRIu64, degree);
+    return fail_fields(RNT_ERR_INVALID_DEGREE, degree, 0, "ring degree must be a power of two, got %" PRIu64,
+                       degree);
   if (!rnt::host::is_ntt_friendly(modulus, degree))
-    return fail(RNT_ERR_NON_NTT_FRIENDLY, "modulus %" PRIu64 " is not NTT-friendly for degree %" PRIu64,
+    return fail_fields(RNT_ERR_NON_NTT_FRIENDLY, modulus, degree,
+                       "modulus %" PRIu64 " is not NTT-friendly for degree %" PRIu64,
                 modulus, degree);
   *psi = rnt::host::find_psi(modulus, degree);
   return RNT_OK;
@@ -376,13 +470,11 @@ int build_tables(rnt::Tables* t) {
   std::vector<rnt::LimbConst<W>> lc(L);
   std::vector<W> resc(L * L, 0), rescp(L * L, 0);
   std::vector<uint64_t> pw(n), ipw(n);
-  // Montgomery-form twiddles for the whole-plane kernels (rnt_plane.hip)
-  const bool mont_tabs = wbits == 32;
-  std::vector<uint32_t> mtw(mont_tabs ? L * n : 0), mitw(mont_tabs ? L * n : 0);
   for (size_t l = 0; l < L; ++l) {
     const uint64_t q = t->moduli[l];
     const uint64_t psi = find_psi(q, n);
-    if (psi == 0) return fail(RNT_ERR_NON_NTT_FRIENDLY, "no primitive 2N-th root mod %" PRIu64, q);
+    if (psi == 0)
+      return fail_fields(RNT_ERR_NON_NTT_FRIENDLY, q, n, "no primitive 2N-th root mod %" PRIu64, q);
     t->psi.push_back(psi);
     const uint64_t psi_inv = invmod(psi, q);
     uint64_t a = 1, b = 1;
@@ -400,13 +492,6 @@ int build_tables(rnt::Tables* t) {
       const uint64_t e = brv(g, t->log_n);
       T[g] = {(W)pw[e], (W)shoup_companion(pw[e], q, wbits)};
       I[g] = {(W)ipw[e], (W)shoup_companion(ipw[e], q, wbits)};
-    }
-    if (mont_tabs) {
-      const uint64_t r32 = (uint64_t)((((u128)1) << 32) % q);
-      for (size_t g = 0; g < n; ++g) {
-        mtw[l * n + g] = (uint32_t)mulmod((uint64_t)T[g].w, r32, q);
-        mitw[l * n + g] = (uint32_t)mulmod((uint64_t)I[g].w, r32, q);
-      }
     }
     rnt::LimbConst<W>& c = lc[l];
     c.q = (W)q;
@@ -426,17 +511,6 @@ int build_tables(rnt::Tables* t) {
     c.c1r_p = (W)shoup_companion(ninvr, q, wbits);
     c.c2r = (W)mulmod(w1, ninvr, q);
     c.c2r_p = (W)shoup_companion(c.c2r, q, wbits);
-    c.qneg = (W)(W(0) - c.qinv);
-    const uint64_t ninvrr = mulmod(ninvr, r, q);
-    c.mc1 = (W)ninvrr;
-    c.mc2 = (W)mulmod(w1, ninvrr, q);
-    {
-      // q = k * 2^s + 1; the 32-bit path uses s capped so that 32 - s <= 24
-      unsigned sh = (unsigned)__builtin_ctzll(q - 1);
-      if (sh > 31) sh = 31;
-      c.s = (W)sh;
-      c.k = (W)((q - 1) >> sh);
-    }
     for (size_t i = 0; i < l; ++i) {
       const uint64_t qi = t->moduli[i];
       const uint64_t inv = invmod(q % qi, qi);
@@ -454,13 +528,6 @@ int build_tables(rnt::Tables* t) {
   HIP_TRY(hipMalloc(&t->resc_p, L * L * sizeof(W)), "hipMalloc(tables)");
   HIP_TRY(hipMemcpy(t->tw_fwd, tw.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
   HIP_TRY(hipMemcpy(t->tw_inv, itw.data(), tb, hipMemcpyHostToDevice), "hipMemcpy");
-  if (mont_tabs) {
-    const size_t mb = L * n * sizeof(uint32_t);
-    HIP_TRY(hipMalloc(&t->mtw_fwd, mb), "hipMalloc(tables)");
-    HIP_TRY(hipMalloc(&t->mtw_inv, mb), "hipMalloc(tables)");
-    HIP_TRY(hipMemcpy(t->mtw_fwd, mtw.data(), mb, hipMemcpyHostToDevice), "hipMemcpy");
-    HIP_TRY(hipMemcpy(t->mtw_inv, mitw.data(), mb, hipMemcpyHostToDevice), "hipMemcpy");
-  }
   HIP_TRY(hipMemcpy(t->lconst, lc.data(), L * sizeof(rnt::LimbConst<W>), hipMemcpyHostToDevice),
           "hipMemcpy");
   HIP_TRY(hipMemcpy(t->resc, resc.data(), L * L * sizeof(W), hipMemcpyHostToDevice), "hipMemcpy");
@@ -480,14 +547,14 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
   if (count == 0) return fail(RNT_ERR_EMPTY_BASIS, "RNS basis must contain at least one modulus");
   if (!moduli) return fail(RNT_ERR_BAD_ARGUMENT, "null moduli");
   if (log_n > (uint32_t)rnt::kMaxLogN)
-    return fail(RNT_ERR_INVALID_DEGREE, "ring degree 2^%u exceeds this backend's maximum 2^%d",
-                log_n, rnt::kMaxLogN);
+    return fail_fields(RNT_ERR_INVALID_DEGREE, log_n < 64 ? 1ull << log_n : 0, 0,
+                       "ring degree 2^%u exceeds this backend's maximum 2^%d", log_n, rnt::kMaxLogN);
   const uint64_t n = 1ull << log_n;
   bool wide = false, lazy30 = true;
   for (size_t i = 0; i < count; ++i) {
     if (!rnt::host::is_ntt_friendly(moduli[i], n))
-      return fail(RNT_ERR_NON_NTT_FRIENDLY,
-                  "modulus %" PRIu64 " is not NTT-friendly for degree %" PRIu64, moduli[i], n);
+      return fail_fields(RNT_ERR_NON_NTT_FRIENDLY, moduli[i], n,
+                         "modulus %" PRIu64 " is not NTT-friendly for degree %" PRIu64, moduli[i], n);
     if (moduli[i] >= (1ull << 63))
       return fail(RNT_ERR_BAD_ARGUMENT,
                   "modulus %" PRIu64 " >= 2^63 (the reference's add_mod overflows)", moduli[i]);
@@ -508,6 +575,9 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     {
       const long jg = env_long("RNT_DEC_JG", 0);  // A/B knob: 0 = auto, else 1..1024
       t->dec_jg = (uint32_t)(jg < 0 ? 0 : jg > 1024 ? 1024 : jg);
+      // key-switch scratch cap (S = [L][L][Bc][N] words per chunk), MiB
+      const long mb = env_long("RNT_KS_WS_MB", 4096);
+      t->ks_ws_bytes = (size_t)(mb > 0 ? mb : 4096) << 20;
     }
     t->log_n = log_n;
     t->n = (size_t)n;
@@ -542,8 +612,8 @@ extern "C" int rnt_ctx_drop_last(const rnt_ctx* ctx, size_t drop_count, rnt_ctx*
   if (!ctx || !out) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
   *out = nullptr;
   if (drop_count >= ctx->L)
-    return fail(RNT_ERR_INVALID_MOD_DROP, "invalid mod-drop count %zu for %zu channels",
-                drop_count, ctx->L);
+    return fail_fields(RNT_ERR_INVALID_MOD_DROP, drop_count, ctx->L,
+                       "invalid mod-drop count %zu for %zu channels", drop_count, ctx->L);
   try {
     rnt_ctx* c = new rnt_ctx;
     c->t = ctx->t;
@@ -613,16 +683,17 @@ extern "C" int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out) 
   const_cast<rnt_ctx*>(ctx)->refs.fetch_add(1);
   b->n_polys = n_polys;
   const size_t bytes = poly_words(b) * word_bytes(ctx->t.get());
-  hipError_t e = hipMalloc(&b->data, bytes);
+  hipStream_t s = ctx->t->stream;
+  hipError_t e = pool_malloc(ctx->t->device, bytes, s, &b->data, &b->data_bytes);
   if (e != hipSuccess) {
     ctx_release(ctx);
     delete b;
     return hip_fail(e, "hipMalloc(buffer)");
   }
-  e = hipMemsetAsync(b->data, 0, bytes, ctx->t->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->t->stream);
+  // zero (RnsPoly::zero), queued on the context stream like every op
+  e = hipMemsetAsync(b->data, 0, bytes, s);
   if (e != hipSuccess) {
-    (void)hipFree(b->data);
+    pool_give(ctx->t->device, b->data, b->data_bytes, s);
     ctx_release(ctx);
     delete b;
     return hip_fail(e, "hipMemset(buffer)");
@@ -631,18 +702,26 @@ extern "C" int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out) 
   return RNT_OK;
 }
 
+// No host wait: the blocks go to the device cache with an event on the
+// context stream, behind every op queued on this buffer.
 extern "C" int rnt_buf_free(rnt_buf* b) {
   if (!b) return RNT_OK;
   if (b->ctx) {
-    (void)hipSetDevice(b->ctx->t->device);
-    (void)hipStreamSynchronize(b->ctx->t->stream);
+    const int dev = b->ctx->t->device;
+    hipStream_t s = b->ctx->t->stream;
+    (void)hipSetDevice(dev);
+    if (b->owns) pool_give(dev, b->data, b->data_bytes, s);
+    pool_give(dev, b->ws, b->ws_bytes, s);
+    pool_give(dev, b->stage, b->stage_bytes, s);
   }
-  if (b->owns) (void)hipFree(b->data);
-  if (b->ctx) ws_give(b->ctx->t->device, b->ws, b->ws_bytes);  // stream drained above
-  else (void)hipFree(b->ws);
-  (void)hipFree(b->stage);
   ctx_release(b->ctx);
   delete b;
+  return RNT_OK;
+}
+
+extern "C" int rnt_pool_trim(int device, size_t* freed_bytes) {
+  const size_t f = pool_drain(device);
+  if (freed_bytes) *freed_bytes = f;
   return RNT_OK;
 }
 
@@ -686,8 +765,8 @@ extern "C" int rnt_upload(rnt_buf* b, const uint64_t* host, size_t n_polys, size
   if (!host) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_upload: null host pointer");
   // from_channels order (poly.rs:78-93): channel count, then reducedness.
   if (channels != b->ctx->L)
-    return fail(RNT_ERR_CHANNEL_COUNT, "channel count mismatch: expected %zu, got %zu", b->ctx->L,
-                channels);
+    return fail_fields(RNT_ERR_CHANNEL_COUNT, b->ctx->L, channels,
+                       "channel count mismatch: expected %zu, got %zu", b->ctx->L, channels);
   if (n_polys != b->n_polys)
     return fail(RNT_ERR_BAD_ARGUMENT, "rnt_upload: buffer holds %zu polys, got %zu", b->n_polys,
                 n_polys);
@@ -710,8 +789,9 @@ extern "C" int rnt_upload(rnt_buf* b, const uint64_t* host, size_t n_polys, size
     (void)hipMemsetAsync(b->data, 0, words * word_bytes(k.t), k.s);
     (void)hipStreamSynchronize(k.s);
     b->in_ntt = 0;
-    return fail(RNT_ERR_NON_REDUCED, "coefficient %" PRIu64 " is not reduced modulo %" PRIu64,
-                host[bad], b->ctx->t->moduli[ch]);
+    return fail_fields(RNT_ERR_NON_REDUCED, host[bad], b->ctx->t->moduli[ch],
+                       "coefficient %" PRIu64 " is not reduced modulo %" PRIu64, host[bad],
+                       b->ctx->t->moduli[ch]);
   }
   b->in_ntt = in_ntt ? 1 : 0;
   trim_stage(b);
@@ -792,65 +872,9 @@ extern "C" int rnt_ntt_inv(rnt_buf* b) {
   return RNT_OK;
 }
 
-// Polys per launch chunk of the coefficient-domain product.  0 / unset
-// RNT_MUL_CHUNK_MB: whole batch; otherwise chunks of about that many MiB of
-// a-operand data (experiment knob for Infinity-Cache residency).
-// Batch pipelining of rnt_mul: the batch is cut into `chunks` slices whose
-// three launches go round-robin onto `streams` streams, so one slice's
-// HBM-bound column passes can overlap another's VALU-bound row pass.
-// RNT_MUL_CHUNKS / RNT_MUL_STREAMS override the defaults (A/B tuning).
-struct MulPlan {
-  size_t chunk;   // polys per slice
-  int streams;    // 1 = the context stream only
-  bool resident;  // slices go through a reused per-stream scratch
-};
 static long env_long(const char* name, long dflt) {
   const char* e = getenv(name);
   return e ? atol(e) : dflt;
-}
-static MulPlan mul_plan(size_t B) {
-  static const long chunks = env_long("RNT_MUL_CHUNKS", 1);
-  static const long streams = env_long("RNT_MUL_STREAMS", 1);
-  static const long resident = env_long("RNT_MUL_RESIDENT", 0);
-  MulPlan p;
-  const size_t c = chunks > 1 ? (size_t)chunks : 1;
-  p.chunk = std::max<size_t>(1, (B + c - 1) / c);
-  p.resident = resident > 0;
-  if (p.resident) p.chunk = std::min<size_t>(B, (size_t)resident);
-  p.streams = (int)std::max(1L, std::min<long>(streams, rnt::Tables::kAux));
-  if (p.chunk >= B) p.streams = 1;
-  return p;
-}
-
-// Auxiliary streams forked from the context stream (created on first use).
-static hipError_t aux_fork(rnt::Tables* t, int n) {
-  std::lock_guard<std::mutex> g(t->aux_mu);
-  hipError_t e = hipSuccess;
-  if (!t->fork_ev) e = hipEventCreateWithFlags(&t->fork_ev, hipEventDisableTiming);
-  for (int i = 0; i < n && e == hipSuccess; ++i) {
-    if (!t->aux[i]) e = hipStreamCreateWithFlags(&t->aux[i], hipStreamNonBlocking);
-    if (e == hipSuccess && !t->join_ev[i])
-      e = hipEventCreateWithFlags(&t->join_ev[i], hipEventDisableTiming);
-  }
-  if (e == hipSuccess) e = hipEventRecord(t->fork_ev, t->stream);
-  for (int i = 0; i < n && e == hipSuccess; ++i) e = hipStreamWaitEvent(t->aux[i], t->fork_ev, 0);
-  return e;
-}
-static hipError_t aux_join(rnt::Tables* t, int n) {
-  hipError_t e = hipSuccess;
-  for (int i = 0; i < n && e == hipSuccess; ++i) {
-    e = hipEventRecord(t->join_ev[i], t->aux[i]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(t->stream, t->join_ev[i], 0);
-  }
-  return e;
-}
-
-// RNT_PLANE=1 enables the whole-plane product path (rnt_plane.hip).  It is
-// off by default: measured 92k vs 112k poly-muls/s for the three-launch path
-// ("whole-plane experiment").
-static bool plane_enabled() {
-  static const bool on = env_long("RNT_PLANE", 0) != 0;
-  return on;
 }
 
 extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
@@ -868,62 +892,18 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
     out->in_ntt = 1;
     return RNT_OK;
   }
-  // poly.rs:307-329: fwd(a), fwd(b), pointwise, inv -- three fused launches,
-  // issued per chunk of polys so a chunk's intermediates can stay resident
-  // in the Infinity Cache between the launches.
+  // poly.rs:307-329: fwd(a), fwd(b), pointwise, inv -- three fused launches
+  // over the whole batch: column passes of both operands (b's into the
+  // workspace), the row kernel (both forward row passes, Montgomery
+  // pointwise product, inverse rows), the inverse column pass.
   const uint64_t ls = limb_stride(out);
-  const size_t wb = word_bytes(k.t);
-  const size_t B = out->n_polys;
-  if (plane_enabled() && rnt::plane_supported(k.t)) {
-    // whole-plane path (rnt_plane.hip): b^ into the workspace, then a * b^
-    if (int rc = ensure_ws(out, poly_words(out) * wb)) return rc;
-    LAUNCH(k.t, rnt::K_PLANE_FWD, rnt::launch_plane_fwd(k, out->ws, ls, b->data, ls), "plane forward");
-    LAUNCH(k.t, rnt::K_PLANE_MUL, rnt::launch_plane_mul(k, out->data, ls, a->data, ls, out->ws, ls),
-           "plane mul");
-    out->in_ntt = 0;
-    return RNT_OK;
-  }
-  const MulPlan plan = mul_plan(B);
-  const size_t n = k.t->n;
-  // resident: per stream a [2][L][chunk][N] scratch that every slice reuses,
-  // so the intermediates are rewritten in place in the Infinity Cache
-  const size_t scratch_words = 2 * k.L * plan.chunk * n;
-  if (plan.resident) {
-    if (int rc = ensure_ws(out, scratch_words * plan.streams * wb)) return rc;
-  } else if (int rc = ensure_ws(out, poly_words(out) * wb)) {
-    return rc;
-  }
-  rnt::Tables* tm = const_cast<rnt::Tables*>(k.t);
-  if (plan.streams > 1) HIP_TRY(aux_fork(tm, plan.streams), "stream fork");
-  int si = 0;
-  for (size_t p0 = 0; p0 < B; p0 += plan.chunk, si = (si + 1) % plan.streams) {
-    rnt::Launch kc = k;
-    kc.B = std::min(plan.chunk, B - p0);
-    kc.s = plan.streams > 1 ? tm->aux[si] : k.s;
-    const size_t off = p0 * n * wb;
-    char* o = (char*)out->data + off;
-    char* w = (char*)out->ws + off;
-    const char* pa = (const char*)a->data + off;
-    const char* pb = (const char*)b->data + off;
-    if (plan.resident) {
-      char* s0 = (char*)out->ws + (size_t)si * scratch_words * wb;
-      char* s1 = s0 + scratch_words / 2 * wb;
-      const uint64_t sls = (uint64_t)kc.B * n;
-      LAUNCH_ON(kc.t, kc.s, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, s0, pa, s1, pb, ls, sls, true),
-                "column forward");
-      LAUNCH_ON(kc.t, kc.s, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, s0, s1, sls, true), "row mul");
-      LAUNCH_ON(kc.t, kc.s, rnt::K_COL_INV, rnt::launch_col_inv(kc, o, ls, s0, sls, 1, nullptr, true),
-                "column inverse");
-      continue;
-    }
-    // lazy: the Harvey 30-bit variant when every q < 2^30 (Tables::lazy30)
-    LAUNCH_ON(kc.t, kc.s, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, o, pa, w, pb, ls, ls, true),
-              "column forward");
-    LAUNCH_ON(kc.t, kc.s, rnt::K_ROW_MUL, rnt::launch_row(kc, 2, o, w, ls, true), "row mul");
-    LAUNCH_ON(kc.t, kc.s, rnt::K_COL_INV, rnt::launch_col_inv(kc, o, ls, o, ls, 1, nullptr, true),
-              "column inverse");
-  }
-  if (plan.streams > 1) HIP_TRY(aux_join(tm, plan.streams), "stream join");
+  if (int rc = ensure_ws(out, poly_words(out) * word_bytes(k.t))) return rc;
+  // lazy: the Harvey 30-bit variant when every q < 2^30 (Tables::lazy30)
+  LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, out->data, a->data, out->ws, b->data, ls, ls, true),
+         "column forward");
+  LAUNCH(k.t, rnt::K_ROW_MUL, rnt::launch_row(k, 2, out->data, out->ws, ls, true), "row mul");
+  LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, out->data, ls, out->data, ls, 1, nullptr, true),
+         "column inverse");
   out->in_ntt = 0;
   return RNT_OK;
 }
@@ -965,7 +945,7 @@ extern "C" int rnt_rescale(rnt_buf* out, const rnt_buf* in) {
   if (int rc = check_buf(in, "rnt_rescale")) return rc;
   const size_t L = in->ctx->L;
   if (L < 2)  // poly.rs:191-197
-    return fail(RNT_ERR_INVALID_MOD_DROP, "invalid mod-drop count 1 for %zu channels", L);
+    return fail_fields(RNT_ERR_INVALID_MOD_DROP, 1, L, "invalid mod-drop count 1 for %zu channels", L);
   if (out->ctx->t != in->ctx->t || out->ctx->L != L - 1)
     return fail(RNT_ERR_BASIS_MISMATCH, "rescale: output basis is not drop_last(1) of the input's");
   if (out->n_polys != in->n_polys)
@@ -1035,7 +1015,7 @@ extern "C" int rnt_rescale_ext(rnt_buf* out, const rnt_buf* in, const void* last
   // the owner of q_last drops it; every other shard keeps all its limbs
   const size_t keep = (L > 0 && t->moduli[L - 1] == q_last) ? L - 1 : L;
   if (keep == 0)
-    return fail(RNT_ERR_INVALID_MOD_DROP, "rescale: nothing left after dropping the last limb");
+    return fail_fields(RNT_ERR_INVALID_MOD_DROP, 1, L, "rescale: nothing left after dropping the last limb");
   if (out->ctx->t != in->ctx->t || out->ctx->L != keep)
     return fail(RNT_ERR_BASIS_MISMATCH, "rnt_rescale_ext: output basis must keep %zu limbs of the input's", keep);
   if (out->n_polys != in->n_polys)
@@ -1400,8 +1380,8 @@ extern "C" int rnt_key_prepare(rnt_buf* key_a, rnt_buf* key_b) {
   // one poly per SOURCE limb: the basis' own channel count for rnt_keyswitch,
   // the global count for a limb shard's rnt_keyswitch_ext (checked there)
   if (key_a->n_polys != key_b->n_polys)
-    return fail(RNT_ERR_CHANNEL_COUNT, "gadget key halves differ: %zu vs %zu polys", key_a->n_polys,
-                key_b->n_polys);
+    return fail_fields(RNT_ERR_CHANNEL_COUNT, key_a->n_polys, key_b->n_polys,
+                       "gadget key halves differ: %zu vs %zu polys", key_a->n_polys, key_b->n_polys);
   if (int rc = rnt_ntt_fwd(key_a)) return rc;
   return rnt_ntt_fwd(key_b);
 }
@@ -1414,7 +1394,9 @@ int check_key(const rnt_buf* d, const rnt_buf* key_a, const rnt_buf* key_b) {
   if (key_a->ctx != d->ctx || key_b->ctx != d->ctx)
     return fail(RNT_ERR_BASIS_MISMATCH, "key-switch: key and ciphertext belong to different bases");
   if (key_a->n_polys != d->ctx->L || key_b->n_polys != d->ctx->L)
-    return fail(RNT_ERR_CHANNEL_COUNT, "gadget key must hold one poly per channel (%zu)", d->ctx->L);
+    return fail_fields(RNT_ERR_CHANNEL_COUNT, d->ctx->L,
+                       key_a->n_polys != d->ctx->L ? key_a->n_polys : key_b->n_polys,
+                       "gadget key must hold one poly per channel (%zu)", d->ctx->L);
   if (!key_a->in_ntt || !key_b->in_ntt)
     return fail(RNT_ERR_DOMAIN_MISMATCH, "key-switch: keys must be prepared (rnt_key_prepare)");
   return RNT_OK;
@@ -1425,18 +1407,9 @@ int check_key(const rnt_buf* d, const rnt_buf* key_a, const rnt_buf* key_b) {
 // rows are read once per chunk from HBM (the batch hits them in cache, see
 // row_pos_pfast), so bigger chunks cut key traffic per ciphertext; 4 GiB is
 // a small slice of the 288 GB.
-static size_t ks_ws_cap() {
-  static const size_t cap = [] {
-    const char* e = getenv("RNT_KS_WS_MB");
-    const long mb = e ? atol(e) : 4096L;
-    return (size_t)(mb > 0 ? mb : 4096L) << 20;
-  }();
-  return cap;
-}
-
 size_t ks_chunk(const rnt::Tables* t, size_t L, size_t B) {
   const size_t per = L * L * t->n * (t->wide ? 8 : 4);
-  size_t c = ks_ws_cap();
+  size_t c = t->ks_ws_bytes;
   c = per ? c / per : B;
   if (c < 1) c = 1;
   return std::min(c, B);
@@ -1507,7 +1480,9 @@ extern "C" int rnt_keyswitch_ext(rnt_buf* acc0, rnt_buf* acc1, const void* src, 
   if (key_a->ctx != acc0->ctx || key_b->ctx != acc0->ctx)
     return fail(RNT_ERR_BASIS_MISMATCH, "key-switch: key and accumulator belong to different bases");
   if (key_a->n_polys != src_limbs || key_b->n_polys != src_limbs)
-    return fail(RNT_ERR_CHANNEL_COUNT, "gadget key must hold one poly per source limb (%zu)", src_limbs);
+    return fail_fields(RNT_ERR_CHANNEL_COUNT, src_limbs,
+                       key_a->n_polys != src_limbs ? key_a->n_polys : key_b->n_polys,
+                       "gadget key must hold one poly per source limb (%zu)", src_limbs);
   if (!key_a->in_ntt || !key_b->in_ntt)
     return fail(RNT_ERR_DOMAIN_MISMATCH, "key-switch: keys must be prepared (rnt_key_prepare)");
   const rnt_buf* seeds[2] = {init0, init1};
@@ -1522,7 +1497,7 @@ extern "C" int rnt_keyswitch_ext(rnt_buf* acc0, rnt_buf* acc1, const void* src, 
   rnt::Launch k = launch_for(acc0);
   const size_t Lt = k.L, Ls = src_limbs, n = k.t->n, wb = word_bytes(k.t), B = acc0->n_polys;
   // polys per chunk: S is [Lt][Ls][Bc][N]
-  size_t bc = std::max<size_t>(1, ks_ws_cap() / std::max<size_t>(1, Lt * Ls * n * wb));
+  size_t bc = std::max<size_t>(1, k.t->ks_ws_bytes / std::max<size_t>(1, Lt * Ls * n * wb));
   bc = std::min(bc, B);
   if (int rc = ensure_ws(acc0, (Lt * Ls + 2 * Lt) * bc * n * wb)) return rc;
   const uint64_t src_ls = (uint64_t)B * n, full_ls = limb_stride(acc0);

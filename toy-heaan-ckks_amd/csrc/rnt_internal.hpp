@@ -30,10 +30,7 @@ namespace rnt {
 constexpr int kMaxLogN = 17;
 constexpr int kRowElems = 16;  // elements per thread per operand in the row pass
 // threads per row-pass workgroup (at least one row's C/16 threads)
-#ifndef RNT_ROW_THREADS
-#define RNT_ROW_THREADS 256
-#endif
-constexpr int kRowThreads = RNT_ROW_THREADS;
+constexpr int kRowThreads = 256;
 
 template <class W>
 struct LimbConst {
@@ -50,12 +47,6 @@ struct LimbConst {
   W c1r_p;
   W c2r;     // psi_inv_rev[1] * n^-1 * 2^w
   W c2r_p;
-  W k;       // q = k * 2^s + 1 (32-bit path: s >= 8, see rnt_modarith.hpp)
-  W s;
-  // whole-plane kernels (rnt_plane.hip, u32 only): Montgomery constants
-  W qneg;    // -q^-1 mod 2^w
-  W mc1;     // n^-1 * 2^2w mod q: last inverse stage after a Montgomery product
-  W mc2;     // psi_inv_rev[1] * n^-1 * 2^2w mod q
 };
 
 // A twiddle and its Shoup companion, interleaved so one load fetches both.
@@ -87,6 +78,7 @@ struct Tables {
   int wide = 0;            // 0: W = u32, 1: W = u64
   bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path
   uint32_t dec_jg = 0;     // key-switch decomposition: target limbs per workgroup (0 = auto)
+  size_t ks_ws_bytes = (size_t)4096 << 20;  // key-switch scratch cap per chunk (RNT_KS_WS_MB)
   uint32_t log_n = 0;
   size_t n = 0;
   size_t L = 0;            // channel count of the root basis
@@ -95,19 +87,9 @@ struct Tables {
   void* tw_fwd = nullptr;   // [L][N] Tw<W>{psi^{brv(g)}, companion}, heap order g in [1, N)
   void* tw_inv = nullptr;   // [L][N] Tw<W>{psi^{-brv(g)}, companion}
   void* lconst = nullptr;   // [L] LimbConst<W>
-  // [L][N] u32 psi^{+-brv(g)} * 2^32 mod q (Montgomery form; u32 bases only)
-  void* mtw_fwd = nullptr;
-  void* mtw_inv = nullptr;
   void* resc = nullptr;     // [L][L]: resc[l][i] = (q_l mod q_i)^-1 mod q_i, i < l
   void* resc_p = nullptr;   // [L][L] Shoup companions
   hipStream_t stream = nullptr;
-  // Auxiliary streams for chunked pipelines (rnt_mul): created on first
-  // use, forked from / joined back into `stream` with events.
-  static constexpr int kAux = 4;
-  hipStream_t aux[kAux] = {};
-  hipEvent_t fork_ev = nullptr;
-  hipEvent_t join_ev[kAux] = {};
-  std::mutex aux_mu;
   // rnt_rescale_ext constants per external last modulus: device arrays
   // {inv[L], invp[L]} with inv[l] = (q_last mod q_l)^-1 mod q_l.
   std::mutex resc_mu;
@@ -126,7 +108,7 @@ struct Tables {
 enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
-  K_PLANE_FWD, K_PLANE_MUL, K_SFFT, K_SAMPLE, K_COUNT
+  K_SFFT, K_SAMPLE, K_COUNT
 };
 
 struct Prof {
@@ -157,6 +139,7 @@ struct rnt_buf {
   const rnt_ctx* ctx = nullptr;
   size_t n_polys = 0;
   void* data = nullptr;       // [L][B][N] words
+  size_t data_bytes = 0;      // size of the block holding `data` (owned buffers)
   int in_ntt = 0;
   // lazily grown per-buffer workspace (buffers are never used by two
   // threads at once, so this needs no lock)
@@ -204,13 +187,6 @@ hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_
 // Montgomery factor 2^w.  addend (optional, coefficient domain, out layout).
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
                           uint64_t in_ls, int rfold, const void* addend, bool lazy = false);
-// Whole-plane product path (rnt_plane.hip; u32 bases at N = 2^16):
-// bhat <- forward transform of b in a private order; out <- a * b.
-bool plane_supported(const Tables* t);
-hipError_t launch_plane_fwd(const Launch& k, void* bhat, uint64_t bhat_ls, const void* b,
-                            uint64_t b_ls);
-hipError_t launch_plane_mul(const Launch& k, void* out, uint64_t out_ls, const void* a,
-                            uint64_t a_ls, const void* bhat, uint64_t bhat_ls);
 // Elementwise over k.L*k.B*N contiguous words: op 0 add, 1 sub, 2 neg,
 // 3 pointwise mul (canonical a*b mod q), 4 Montgomery product (a*b*2^-w).
 hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a,

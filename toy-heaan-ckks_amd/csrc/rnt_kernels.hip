@@ -80,14 +80,9 @@ __device__ __forceinline__ auto mod_for(const LimbConst<W>& lc) {
 // limb's twiddle table): loads/stores take a 32-bit per-lane element offset
 // plus a wave-uniform one that lands in the instruction's SGPR soffset, so
 // strided column access costs no VALU address arithmetic.
-// Cache-policy bits (`aux`) of the plane loads and stores; the planes are
-// streamed once per launch (2 = nt).
-#ifndef RNT_BUF_LD_AUX
-#define RNT_BUF_LD_AUX 0
-#endif
-#ifndef RNT_BUF_ST_AUX
-#define RNT_BUF_ST_AUX 0
-#endif
+// Cache-policy bits (`aux`) of the plane loads and stores: the default
+// policy (non-temporal was within run-to-run spread).
+constexpr int kBufAux = 0;
 // Measurement builds only (tools/build_variant.sh -DRNT_MEAS=...; never the
 // shipped library): 1 = the product kernels (k_colt_fwd, k_row<2>,
 // k_colt_inv) move no plane data through memory (synthetic loads, stores
@@ -124,23 +119,23 @@ struct BufView {
   __device__ __forceinline__ W ld(uint32_t v, uint32_t s) const {
     if constexpr (kMeas == 1) return meas_val<W>(v, s);
     if constexpr (sizeof(W) == 4) {
-      return __builtin_amdgcn_raw_buffer_load_b32(r, v * 4u, s * 4u, RNT_BUF_LD_AUX);
+      return __builtin_amdgcn_raw_buffer_load_b32(r, v * 4u, s * 4u, kBufAux);
     } else {
-      return __builtin_bit_cast(W, __builtin_amdgcn_raw_buffer_load_b64(r, v * 8u, s * 8u, RNT_BUF_LD_AUX));
+      return __builtin_bit_cast(W, __builtin_amdgcn_raw_buffer_load_b64(r, v * 8u, s * 8u, kBufAux));
     }
   }
   // four consecutive words (the compiler does not merge the raw buffer
   // builtins into wide loads by itself)
   __device__ __forceinline__ void ld4(W (&o)[4], uint32_t v, uint32_t s) const {
     if constexpr (sizeof(W) == 4) {
-      const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, v * 4u, s * 4u, RNT_BUF_LD_AUX);
+      const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, v * 4u, s * 4u, kBufAux);
       o[0] = q[0];
       o[1] = q[1];
       o[2] = q[2];
       o[3] = q[3];
     } else {
-      const auto a = __builtin_amdgcn_raw_buffer_load_b128(r, v * 8u, s * 8u, RNT_BUF_LD_AUX);
-      const auto b = __builtin_amdgcn_raw_buffer_load_b128(r, v * 8u + 16u, s * 8u, RNT_BUF_LD_AUX);
+      const auto a = __builtin_amdgcn_raw_buffer_load_b128(r, v * 8u, s * 8u, kBufAux);
+      const auto b = __builtin_amdgcn_raw_buffer_load_b128(r, v * 8u + 16u, s * 8u, kBufAux);
       o[0] = (uint64_t)a[0] | ((uint64_t)a[1] << 32);
       o[1] = (uint64_t)a[2] | ((uint64_t)a[3] << 32);
       o[2] = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
@@ -152,10 +147,10 @@ struct BufView {
       if (x != (W)0xffffffffu) return;
     }
     if constexpr (sizeof(W) == 4) {
-      __builtin_amdgcn_raw_buffer_store_b32(x, r, v * 4u, s * 4u, RNT_BUF_ST_AUX);
+      __builtin_amdgcn_raw_buffer_store_b32(x, r, v * 4u, s * 4u, kBufAux);
     } else {
       using V2 = decltype(__builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, 0));
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, x), r, v * 8u, s * 8u, RNT_BUF_ST_AUX);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V2, x), r, v * 8u, s * 8u, kBufAux);
     }
   }
 };
@@ -368,15 +363,10 @@ k_ks_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32
 // threads x E registers.  Passes run from the top bits down: full radix-16
 // passes on bits [bb, bb+4), then (if LOGX % 4) a partial pass on bits
 // [0, REM) with register bits [0, 4).  LOGX < 4: one thread holds it all.
-// LOGX = 9 (the N = 2^17 rows) may instead run three radix-8 passes (3+3+3
-// rather than 4+4+1, whose last exchange buys a single stage).
-#ifndef RNT_ROW_RADIX8
-#define RNT_ROW_RADIX8 0
-#endif
 template <int LOGX>
 struct PassSched {
   static constexpr int LOGX_ = LOGX;
-  static constexpr int LOGE = LOGX < 4 ? LOGX : (RNT_ROW_RADIX8 && LOGX == 9) ? 3 : 4;
+  static constexpr int LOGE = LOGX < 4 ? LOGX : 4;
   static constexpr int E = 1 << LOGE;
   static constexpr int LOG_T = LOGX - LOGE;
   static constexpr int T = 1 << LOG_T;
@@ -404,7 +394,7 @@ struct RowGeo : PassSched<LOG_C> {
   using S = PassSched<LOG_C>;
   static constexpr int LOGC = LOG_C;
   static constexpr int C = 1 << LOG_C;
-  // one pad word per 2^PADSH: 16 (radix-16 passes) or 8 (radix-8)
+  // one pad word per 2^PADSH words (16 for the radix-16 passes)
   static constexpr int PADSH = S::LOGE == 3 ? 3 : 4;
   static constexpr int PADC = C + (C >> PADSH);
   static constexpr int THREADS = S::T > kRowThreads ? S::T : kRowThreads;
@@ -553,51 +543,27 @@ __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0,
   }
 }
 
-// Row kernels with several operands exchange them one after the other
-// through a single LDS region: half (or a third) of the LDS per workgroup,
-// so occupancy is bounded by VGPRs rather than LDS, at two extra barriers.
-#ifndef RNT_SEQ_XCHG
-#define RNT_SEQ_XCHG 1
-#endif
-constexpr bool kSeqXchg = RNT_SEQ_XCHG;
 // Minimum resident waves per SIMD requested for the row kernels (caps their
-// VGPR budget at 512 / kRowMinWaves).
-#ifndef RNT_ROW_MIN_WAVES
-#define RNT_ROW_MIN_WAVES 6
-#endif
-constexpr int kRowMinWaves = RNT_ROW_MIN_WAVES;
+// VGPR budget at 512 / kRowMinWaves) and for the key-switch rows.
+constexpr int kRowMinWaves = 6;
+constexpr int kKsMinWaves = 4;
 
-// Move NOPS register sets from distribution BF to BT through LDS.
+// Move NOPS register sets from distribution BF to BT through LDS.  Several
+// operands go one after the other through a single LDS region, so occupancy
+// is bounded by VGPRs rather than LDS, at two barriers per operand.
 template <class G, class W, int NOPS, int BF, int BT>
 __device__ __forceinline__ void xchg(W (&x)[NOPS][G::E], W* lds, uint32_t slot, uint32_t tau) {
   const uint32_t wb = G::lds_off(slot, G::base(tau, BF));
   const uint32_t rb = G::lds_off(slot, G::base(tau, BT));
-  if constexpr (kSeqXchg && NOPS > 1) {
-#pragma unroll
-    for (int o = 0; o < NOPS; ++o) {
-#pragma unroll
-      for (int i = 0; i < G::E; ++i) lds[wb + G::lds_ioff(i, BF)] = x[o][i];
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < G::E; ++i) x[o][i] = lds[rb + G::lds_ioff(i, BT)];
-      __syncthreads();
-    }
-    return;
-  }
 #pragma unroll
   for (int o = 0; o < NOPS; ++o) {
-    W* reg = lds + o * G::REGION;
 #pragma unroll
-    for (int i = 0; i < G::E; ++i) reg[wb + G::lds_ioff(i, BF)] = x[o][i];
+    for (int i = 0; i < G::E; ++i) lds[wb + G::lds_ioff(i, BF)] = x[o][i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < G::E; ++i) x[o][i] = lds[rb + G::lds_ioff(i, BT)];
+    __syncthreads();
   }
-  __syncthreads();
-#pragma unroll
-  for (int o = 0; o < NOPS; ++o) {
-    const W* reg = lds + o * G::REGION;
-#pragma unroll
-    for (int i = 0; i < G::E; ++i) x[o][i] = reg[rb + G::lds_ioff(i, BT)];
-  }
-  __syncthreads();
 }
 
 // Per-thread transform coordinates: `slot` (which transform of the
@@ -934,11 +900,8 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
 // Key-switch rows.  Row = (target limb j, poly p, row r).  For every source
 // limb i: forward rows of S[j][i][p], multiply-accumulate with the
 // NTT-resident keys; then the inverse rows of both accumulators.
-#ifndef RNT_KS_MIN_WAVES
-#define RNT_KS_MIN_WAVES 4
-#endif
 template <class W, int LOG_C>
-__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? RNT_KS_MIN_WAVES : 1)
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kKsMinWaves : 1)
 k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
           const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
           const W* __restrict__ init0, const W* __restrict__ init1, uint64_t init_ls,
@@ -1268,7 +1231,8 @@ static hipError_t allow_lds(K kernel, size_t bytes) {
 template <class W, int LOG_C>
 static size_t row_lds(int nops) {
   using G = RowGeo<LOG_C>;
-  return (size_t)(kSeqXchg ? 1 : nops) * G::RPW * G::PADC * sizeof(W);
+  (void)nops;  // operands share one region (xchg)
+  return (size_t)G::RPW * G::PADC * sizeof(W);
 }
 
 #define RNT_DISPATCH_LOGRT(LOGR, MACRO) \

@@ -38,12 +38,9 @@ __host__ __device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) {
 // into VCC / an SGPR pair) + v_cndmask_b32, two full-rate instructions
 // (tools/oprate2.hip: 2.1 cycles each per wave64 on one SIMD), where the
 // min(x, x - q) form costs v_sub (2.2) + v_min_u32 (4.1, half rate).
-#ifndef RNT_BORROW_SELECT
-#define RNT_BORROW_SELECT 1
-#endif
 template <class W>
 __host__ __device__ __forceinline__ W csub(W x, W q) {
-#if defined(__HIP_DEVICE_COMPILE__) && RNT_BORROW_SELECT
+#if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (sizeof(W) == 4) {
     W y;
     const bool borrow = __builtin_sub_overflow(x, q, &y);
@@ -62,7 +59,7 @@ __host__ __device__ __forceinline__ W add_mod(W a, W b, W q) {
 // a, b in [0, q) -> a - b mod q
 template <class W>
 __host__ __device__ __forceinline__ W sub_mod(W a, W b, W q) {
-#if defined(__HIP_DEVICE_COMPILE__) && RNT_BORROW_SELECT
+#if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (sizeof(W) == 4) {
     W d;
     const bool borrow = __builtin_sub_overflow(a, b, &d);

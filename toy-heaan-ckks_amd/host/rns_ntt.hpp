@@ -46,16 +46,37 @@ enum class RnsNttErrorKind {
   BadArgument = RNT_ERR_BAD_ARGUMENT,
 };
 
+// The variant and its fields, as the reference's struct variants carry them
+// (InvalidDegree{degree}, NonNttFriendlyModulus{modulus, degree},
+// InvalidModDrop{drop_count, channel_count}, ChannelCountMismatch{expected,
+// actual}, NonReducedCoefficient{coefficient, modulus}); fields a variant
+// does not have stay 0.
 class RnsNttError : public std::runtime_error {
  public:
-  RnsNttError(int status, const char* msg)
+  RnsNttError(int status, const char* msg, uint64_t f0 = 0, uint64_t f1 = 0)
       : std::runtime_error(std::string(rnt_status_string(status)) + ": " + (msg ? msg : "")),
-        kind((RnsNttErrorKind)status) {}
+        kind((RnsNttErrorKind)status) {
+    switch (kind) {
+      case RnsNttErrorKind::InvalidDegree: degree = f0; break;
+      case RnsNttErrorKind::NonNttFriendlyModulus: modulus = f0; degree = f1; break;
+      case RnsNttErrorKind::InvalidModDrop: drop_count = f0; channel_count = f1; break;
+      case RnsNttErrorKind::ChannelCountMismatch: expected = f0; actual = f1; break;
+      case RnsNttErrorKind::NonReducedCoefficient: coefficient = f0; modulus = f1; break;
+      default: break;
+    }
+  }
   RnsNttErrorKind kind;
+  uint64_t degree = 0, modulus = 0, drop_count = 0, channel_count = 0, expected = 0, actual = 0,
+           coefficient = 0;
 };
 
+// Throws the failing call's variant with the fields rnt_last_error_detail
+// reports for it.
 inline void check(int status) {
-  if (status != RNT_OK) throw RnsNttError(status, rnt_last_error());
+  if (status == RNT_OK) return;
+  uint64_t f[2] = {0, 0};
+  if (rnt_last_error_detail(f) != status) f[0] = f[1] = 0;
+  throw RnsNttError(status, rnt_last_error(), f[0], f[1]);
 }
 
 template <size_t N>
@@ -76,7 +97,8 @@ class RnsBasis : public std::enable_shared_from_this<RnsBasis<N>> {
   // RnsBasis::new (basis.rs:97-106): InvalidDegree / EmptyBasis /
   // NonNttFriendlyModulus like the reference.
   static BasisRef<N> create(const std::vector<uint64_t>& moduli, int device = 0) {
-    if (((size_t)1 << log2_exact(N)) != N) throw RnsNttError(RNT_ERR_INVALID_DEGREE, "N is not a power of two");
+    if (((size_t)1 << log2_exact(N)) != N)
+      throw RnsNttError(RNT_ERR_INVALID_DEGREE, "N is not a power of two", N);
     rnt_ctx* c = nullptr;
     check(rnt_ctx_create(log2_exact(N), moduli.data(), moduli.size(), device, &c));
     return BasisRef<N>(new RnsBasis(c));
@@ -219,7 +241,8 @@ class RnsPoly {
   }
   RnsPoly rescale() const {
     if (basis_->channel_count() < 2)
-      throw RnsNttError(RNT_ERR_INVALID_MOD_DROP, "rescale needs at least two channels");
+      throw RnsNttError(RNT_ERR_INVALID_MOD_DROP, "rescale needs at least two channels", 1,
+                        basis_->channel_count());
     return rescale_into(basis_->drop_last(1));
   }
   // mod_drop_last (poly.rs:169-177)

@@ -44,6 +44,7 @@ __all__ = [
     "Plaintext",
     "CkksEncoder",
     "DeviceRng",
+    "pool_trim",
 ]
 
 
@@ -65,6 +66,15 @@ def device_count() -> int:
     r = ctypes.c_int(0)
     check(load().rnt_device_count(ctypes.byref(r)))
     return int(r.value)
+
+
+def pool_trim(device: int = -1) -> int:
+    """Release the device block cache's idle blocks (of one device, or all
+    with -1) back to HIP; returns the bytes released.  Call it when another
+    allocator (torch's) runs out of memory before retrying."""
+    freed = ctypes.c_size_t(0)
+    check(load().rnt_pool_trim(int(device), ctypes.byref(freed)))
+    return int(freed.value)
 
 
 def generate_primes(bit_size: int, count: int, degree: int) -> list[int]:
@@ -121,7 +131,8 @@ class RnsBasis:
     def __init__(self, moduli: Sequence[int], degree: int, device: int = 0):
         lib = load()
         if degree <= 0 or degree & (degree - 1):
-            raise RnsNttError(_lib.INVALID_DEGREE, f"ring degree must be a power of two, got {degree}")
+            raise RnsNttError(_lib.INVALID_DEGREE, f"ring degree must be a power of two, got {degree}",
+                              {"degree": degree})
         log_n = degree.bit_length() - 1
         arr = np.ascontiguousarray(np.array(list(moduli), dtype=np.uint64)) if len(moduli) else np.zeros(1, np.uint64)
         h = ctypes.c_void_p()
@@ -382,7 +393,8 @@ class RnsPoly:
     def rescale(self) -> "RnsPoly":
         if self.basis.channel_count() < 2:
             raise RnsNttError(_lib.INVALID_MOD_DROP,
-                              f"invalid mod-drop count 1 for {self.basis.channel_count()} channels")
+                              f"invalid mod-drop count 1 for {self.basis.channel_count()} channels",
+                              {"drop_count": 1, "channel_count": self.basis.channel_count()})
         return self.rescale_into(self.basis.drop_last(1))
 
     def mod_drop_last(self, drop_count: int) -> "RnsPoly":

@@ -43,13 +43,36 @@ STATUS_NAMES = {
 }
 
 
-class RnsNttError(Exception):
-    """Mirror of RnsNttError (errors.rs:4-20) plus the C-ABI's extra codes."""
+# the fields of each reference variant, in rnt_last_error_detail's order
+FIELD_NAMES = {
+    1: ("degree",),
+    2: (),
+    3: ("modulus", "degree"),
+    4: ("drop_count", "channel_count"),
+    5: ("expected", "actual"),
+    6: ("coefficient", "modulus"),
+}
 
-    def __init__(self, code: int, message: str):
+
+class RnsNttError(Exception):
+    """Mirror of RnsNttError (errors.rs:4-20) plus the C-ABI's extra codes.
+
+    ``kind`` is the variant name and ``fields`` its payload, e.g.
+    ``NonReducedCoefficient`` carries ``{"coefficient": c, "modulus": q}``;
+    each field is also an attribute (``err.coefficient``)."""
+
+    def __init__(self, code: int, message: str, fields: dict | None = None):
         self.code = code
         self.kind = STATUS_NAMES.get(code, "Unknown")
+        self.fields = dict(fields or {})
+        for k, v in self.fields.items():
+            setattr(self, k, v)
         super().__init__(f"{self.kind}: {message}")
+
+    def __eq__(self, other):  # variant equality, like the reference's PartialEq
+        return isinstance(other, RnsNttError) and (self.code, self.fields) == (other.code, other.fields)
+
+    __hash__ = Exception.__hash__
 
 
 _P = c_void_p
@@ -60,6 +83,8 @@ _I64P = POINTER(c_int64)
 SIGNATURES = {
     "rnt_abi_version": (c_int, []),
     "rnt_last_error": (c_char_p, []),
+    "rnt_last_error_detail": (c_int, [_U64P]),
+    "rnt_pool_trim": (c_int, [c_int, POINTER(c_size_t)]),
     "rnt_status_string": (c_char_p, [c_int]),
     "rnt_device_count": (c_int, [POINTER(c_int)]),
     "rnt_profile_enable": (c_int, [_P, c_int]),
@@ -139,7 +164,16 @@ def load(path: str | None = None) -> ctypes.CDLL:
     return lib
 
 
+def last_error_fields(status: int) -> dict:
+    """The reference variant's fields of the last failing call on this
+    thread (rnt_last_error_detail), named as in errors.rs:4-20."""
+    raw = (c_uint64 * 2)()
+    if load().rnt_last_error_detail(raw) != status:
+        return {}
+    return {name: int(raw[i]) for i, name in enumerate(FIELD_NAMES.get(status, ()))}
+
+
 def check(status: int) -> None:
     if status != OK:
         msg = load().rnt_last_error()
-        raise RnsNttError(status, msg.decode() if msg else "")
+        raise RnsNttError(status, msg.decode() if msg else "", last_error_fields(status))

@@ -188,7 +188,15 @@ class GpuBackend:
             basis.sync()
 
     def _empty(self, basis, shape):
-        return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
+        try:
+            return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
+        except self.torch.cuda.OutOfMemoryError:
+            # the library's device block cache may hold the memory torch needs
+            from . import pool_trim
+
+            if pool_trim(self.device) == 0:
+                raise
+            return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
 
     def _wrap(self, basis, t, B, ntt=False):
         from . import RnsPoly
@@ -341,13 +349,15 @@ class LimbShardedPipeline:
         q_last = self.moduli[-1]
         B = self.backend.batch(c0)
         owner = self.rank == self.owner_last
+        # every rank knows the owner's count: all raise together, before the
+        # collective, instead of the others waiting in it
+        if self.counts[self.owner_last] < 2:
+            raise ValueError("rescale would leave the owner of the last limb with no limbs")
         planes = self.backend.new_planes(self.basis, 2, B)
         if owner:
             planes[0].copy_(self.backend.last_limb(c0))
             planes[1].copy_(self.backend.last_limb(c1))
         self.comm.broadcast(planes, self.owner_last)  # the rescale join
-        if owner and len(self.limbs) < 2:
-            raise ValueError("rescale would leave the owner of the last limb with no limbs")
         out_basis = self.backend.drop_last(self.basis) if owner else self.basis
         r0 = self.backend.rescale(self.basis, out_basis, c0, planes[0], q_last)
         r1 = self.backend.rescale(self.basis, out_basis, c1, planes[1], q_last)
