@@ -897,21 +897,65 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
   }
 }
 
-// Key-switch rows.  Row = (target limb j, poly p, row r).  For every source
-// limb i: forward rows of S[j][i][p], multiply-accumulate with the
-// NTT-resident keys; then the inverse rows of both accumulators.
+// Padded LDS position of key word w: 4 pad words per 64, so the 16-byte
+// reads of 16 lanes at 64-byte strides (a row's E = 16 consecutive words per
+// thread) start on 16 distinct 4-bank groups, and 16-byte alignment holds.
+__device__ __forceinline__ uint32_t ks_pad(uint32_t w) { return w + ((w >> 6) << 2); }
+// 16 bytes of LDS into registers (p is 16-byte aligned by construction:
+// ks_pad keeps every thread's run of E words on a 16-byte boundary).
+template <class W>
+__device__ __forceinline__ void ks_lds_read16(W (&o)[16 / sizeof(W)], const W* p) {
+  const uint4 v = *(const uint4*)p;
+  if constexpr (sizeof(W) == 4) {
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  } else {
+    o[0] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    o[1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  }
+}
+
+// Key-switch rows.  A workgroup owns row r of target limb j for RPW
+// consecutive polys p (grid: (j, r) major, poly group minor, dealt so the
+// workgroups of one (j, r) share an XCD).  For every source limb i: forward
+// rows of S[j][i][p], multiply-accumulate with the NTT-resident keys; then
+// the inverse rows of both accumulators.  The key rows of (i, j, r) are the
+// same for every poly of the workgroup, so its threads load them once per i,
+// cooperatively and together with the S rows, into a double-buffered LDS
+// slot, and the accumulate reads them back from LDS: one global round trip
+// per source limb instead of three (S, then key_b, then key_a), and 2 key
+// words per thread instead of 2E (A/B: profiles/r02_ab_ks_rows.txt).
 template <class W, int LOG_C>
 __global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kKsMinWaves : 1)
 k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
           const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
           const W* __restrict__ init0, const W* __restrict__ init1, uint64_t init_ls,
-          TabPtrs<W> tp, uint32_t log_n, uint32_t L, uint32_t B, uint64_t ls,
-          uint64_t rows_total) {
+          TabPtrs<W> tp, uint32_t log_n, uint32_t L, uint32_t B, uint64_t ls, uint32_t pgroups,
+          uint32_t nblocks) {
   using G = RowGeo<LOG_C>;
   constexpr int E = G::E;
+  constexpr int C = G::C;
+  constexpr int KPAD = C + (C >> 4);                            // padded key row (ks_pad)
+  constexpr int KPT = (2 * C + G::THREADS - 1) / G::THREADS;  // key words per thread per i
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
-  const RowPos rp = row_pos_pfast<G>(log_n, B, rows_total);  // rp.l == target limb j
+  W* kbuf = lds + G::REGION;  // [2 buffers][key_b row | key_a row]
+  // XCD-aware deal: hardware block b runs on XCD b % 8; consecutive logical
+  // blocks (one (j, r), successive poly groups) get the same b % 8
+  const uint32_t per_xcd = (nblocks + 7) / 8;
+  const uint32_t wg = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
+  if (wg >= nblocks) return;  // the whole workgroup: no barrier is left waiting
+  const uint32_t log_r = log_n - G::LOGC;
+  const uint32_t pg = wg % pgroups;
+  const uint32_t jr = wg / pgroups;
+  RowPos rp;
+  rp.xp.slot = G::slot_of(threadIdx.x);
+  rp.xp.tau = G::tau_of(threadIdx.x);
+  rp.r = jr & ((1u << log_r) - 1u);
+  rp.l = jr >> log_r;
+  const uint32_t p = pg * G::RPW + rp.xp.slot;
+  rp.active = p < B;
+  rp.p = rp.active ? p : B - 1;  // inactive slots read a valid row, store nothing
+  rp.xp.heap = (1u << log_n) + rp.r * (uint32_t)G::C;
   const uint64_t N = 1ull << log_n;
   const uint32_t j = rp.l;
   const uint64_t rowoff = (uint64_t)rp.r * G::C;
@@ -929,30 +973,56 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     acc[0][e] = init0 ? init0[ibase + pos] : (W)0;
     acc[1][e] = init1 ? init1[ibase + pos] : (W)0;
   }
-  // one source limb per iteration; not unrolled or pipelined by the
-  // compiler (that doubles the live registers and halves occupancy)
 #pragma unroll 1
   for (uint32_t i = 0; i < L; ++i) {
+    // this limb's key rows (key poly i, limb j, row r; limb stride key_ls)
+    // and S rows: one batch of loads, one wait
     const uint64_t sbase = (((uint64_t)j * L + i) * B + rp.p) * N + rowoff;
+    const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + rowoff;
+    W kr[KPT];
+#pragma unroll
+    for (int m = 0; m < KPT; ++m) {
+      const uint32_t w = threadIdx.x + (uint32_t)m * G::THREADS;
+      if (w < 2u * C) kr[m] = w < (uint32_t)C ? key_b[kbase + w] : key_a[kbase + w - C];
+    }
     W x[1][E];
 #pragma unroll
     for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
-    xf_fwd<G, W, 1>(x, rp.xp, lds, tw, mod_of(lc));
-    // keep the key loads below the transform: hoisted above it they stay
-    // live across all of it (the register peak that capped occupancy)
-    __builtin_amdgcn_sched_barrier(0);
-    // key poly i, limb j (key buffers hold L polys: limb stride key_ls)
-    const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + rowoff;
+    W* kb = kbuf + (i & 1u) * 2 * KPAD;
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const W kb = key_b[kbase + bl + ((uint32_t)e << G::BBL)];
-      acc[0][e] = add_mod<W>(acc[0][e], mont_mul<W>(x[0][e], kb, lc.q, lc.qinv), lc.q);
+    for (int m = 0; m < KPT; ++m) {
+      const uint32_t w = threadIdx.x + (uint32_t)m * G::THREADS;
+      if (w < 2u * C) kb[(w < (uint32_t)C ? 0 : KPAD) + ks_pad(w & (C - 1))] = kr[m];
     }
+    // the transform's LDS exchange ends in barriers that publish kb (and
+    // order the reads of this slot two limbs ago before this write); a
+    // single-pass row has none, so it gets one here
+    if constexpr (G::P < 2) __syncthreads();
+    xf_fwd<G, W, 1>(x, rp.xp, lds, tw, mod_of(lc));
     __builtin_amdgcn_sched_barrier(0);
+    // the last pass leaves a thread's E values at consecutive positions
+    // (G::BBL == 0): the keys come back 16 bytes at a time, one key after
+    // the other
+    static_assert(G::BBL == 0, "last row pass distribution");
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const W ka = key_a[kbase + bl + ((uint32_t)e << G::BBL)];
-      acc[1][e] = add_mod<W>(acc[1][e], mont_mul<W>(x[0][e], ka, lc.q, lc.qinv), lc.q);
+    for (int o = 0; o < 2; ++o) {
+      const W* kk = kb + o * KPAD + ks_pad(bl);
+      constexpr int V = 16 / sizeof(W);
+#pragma unroll
+      for (int e0 = 0; e0 < E; e0 += V) {
+        W kv[V];
+        if constexpr (E % V == 0) {
+          ks_lds_read16<W>(kv, kk + e0);
+        } else {
+#pragma unroll
+          for (int v = 0; v < V; ++v) kv[v] = e0 + v < E ? kk[e0 + v] : (W)0;
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+          if (e0 + v < E)
+            acc[o][e0 + v] = add_mod<W>(acc[o][e0 + v], mont_mul<W>(x[0][e0 + v], kv[v], lc.q, lc.qinv), lc.q);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   // the two accumulators' inverse rows one after the other (half the live
@@ -1529,16 +1599,21 @@ static hipError_t ks_rows_launch(const Launch& k, void* u0, void* u1, uint64_t l
                                  const void* init0, const void* init1, uint64_t init_ls) {
   using G = RowGeo<LOG_C>;
   const Geom g = geom_for(k.t->log_n);
-  const uint64_t rows = (uint64_t)k.L * k.B * g.r;
-  if (rows == 0) return hipSuccess;
-  const unsigned blocks = (unsigned)((rows + G::RPW - 1) / G::RPW);
-  const size_t lds = row_lds<W, LOG_C>(2);
+  if (k.L == 0 || k.B == 0) return hipSuccess;
+  // one workgroup per (target limb, row, group of RPW polys)
+  const uint64_t pgroups = (k.B + G::RPW - 1) / G::RPW;
+  const uint64_t blocks = (uint64_t)k.L * g.r * pgroups;
+  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+  const unsigned launched = (unsigned)((blocks + 7) / 8 * 8);  // whole XCD rounds
+  // exchange region + two padded {key_b, key_a} row buffers
+  const size_t lds = row_lds<W, LOG_C>(1) + 2 * 2 * (G::C + (G::C >> 4)) * sizeof(W);
   hipError_t e = allow_lds(k_ks_rows<W, LOG_C>, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_ks_rows<W, LOG_C>), dim3(blocks), dim3(G::THREADS), lds, k.s, (W*)u0,
+  hipLaunchKernelGGL((k_ks_rows<W, LOG_C>), dim3(launched), dim3(G::THREADS), lds, k.s, (W*)u0,
                      (W*)u1, (const W*)S, (const W*)key_a, (const W*)key_b, key_ls,
                      (const W*)init0, (const W*)init1, init_ls, tab_ptrs<W>(k.t), g.log_n,
-                     (uint32_t)k.src_limbs(), (uint32_t)k.B, ls, rows);
+                     (uint32_t)k.src_limbs(), (uint32_t)k.B, ls, (uint32_t)pgroups,
+                     (uint32_t)blocks);
   return hipGetLastError();
 }
 
