@@ -154,3 +154,4 @@ def test_small_keyswitch_scratch_chunks_every_ciphertext(gpu, monkeypatch):
     for p in range(B):
         w0, w1 = orc.keyswitch(Bo, c[1][p], ka, kb)
         assert np.array_equal(g0[p], w0[:Lt]) and np.array_equal(g1[p], w1[:Lt]), p
+

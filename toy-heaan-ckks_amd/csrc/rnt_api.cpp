@@ -1415,6 +1415,21 @@ size_t ks_chunk(const rnt::Tables* t, size_t L, size_t B) {
   return std::min(c, B);
 }
 
+// Decomposition + key-switch rows of one chunk (k.B polys, k.L target limbs,
+// k.src_limbs() source limbs at src) into the NTT-row accumulators U0/U1.
+// (Running them per group of target limbs, so each S slice could stay in the
+// Infinity Cache between the two kernels, was slower: profiles/r02_ab_ks_groups.txt.)
+int ks_decompose_rows(const rnt::Launch& k, char* S, const char* src, uint64_t src_ls, char* U0,
+                      char* U1, uint64_t u_ls, const rnt_buf* key_a, const rnt_buf* key_b,
+                      const char* i0, const char* i1, uint64_t init_ls) {
+  LAUNCH(k.t, rnt::K_KS_DECOMPOSE, rnt::launch_ks_decompose(k, S, src, src_ls), "ks decompose");
+  LAUNCH(k.t, rnt::K_KS_ROWS,
+         rnt::launch_ks_rows(k, U0, U1, u_ls, S, key_a->data, key_b->data, limb_stride(key_a), i0, i1,
+                             init_ls),
+         "ks rows");
+  return RNT_OK;
+}
+
 // Gadget sum for polys [p0, p0+bc) of d into out0/out1 (full-batch layout):
 // out0 = INV(sum_i NTT(alpha_i) key_b[i] + init0) (+ add0), etc.
 // ws layout: S | U0 | U1.
@@ -1429,11 +1444,11 @@ int ks_chunk_run(rnt::Launch k, void* ws, const rnt_buf* d, size_t p0, size_t bc
   char* U1 = U0 + L * bc * n * wb;
   const uint64_t cls = (uint64_t)bc * n;  // chunk-local limb stride
   const uint64_t d_ls = limb_stride(d);
-  LAUNCH(k.t, rnt::K_KS_DECOMPOSE, rnt::launch_ks_decompose(k, S, (const char*)d->data + p0 * n * wb, d_ls), "ks decompose");
   const char* i0 = with_init && init0 ? (const char*)init0 + p0 * n * wb : nullptr;
   const char* i1 = with_init && init1 ? (const char*)init1 + p0 * n * wb : nullptr;
-  LAUNCH(k.t, rnt::K_KS_ROWS, rnt::launch_ks_rows(k, U0, U1, cls, S, key_a->data, key_b->data, limb_stride(key_a), i0,
-                              i1, init_ls), "ks rows");
+  if (int rc = ks_decompose_rows(k, S, (const char*)d->data + p0 * n * wb, d_ls, U0, U1, cls, key_a,
+                                 key_b, i0, i1, init_ls))
+    return rc;
   const char* a0 = add0 ? (const char*)add0 + p0 * n * wb : nullptr;
   LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, (char*)out0 + p0 * n * wb, out_ls, U0, cls, 1, a0), "ks inverse");
   LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, (char*)out1 + p0 * n * wb, out_ls, U1, cls, 1, nullptr), "ks inverse");
@@ -1510,14 +1525,11 @@ extern "C" int rnt_keyswitch_ext(rnt_buf* acc0, rnt_buf* acc1, const void* src, 
     char* U0 = S + Lt * Ls * kc.B * n * wb;
     char* U1 = U0 + Lt * kc.B * n * wb;
     const size_t off = p0 * n * wb;
-    LAUNCH(kc.t, rnt::K_KS_DECOMPOSE,
-           rnt::launch_ks_decompose(kc, S, (const char*)src + off, src_ls), "ks decompose");
     const char* i0 = init0 ? (const char*)init0->data + off : nullptr;
     const char* i1 = init1 ? (const char*)init1->data + off : nullptr;
-    LAUNCH(kc.t, rnt::K_KS_ROWS,
-           rnt::launch_ks_rows(kc, U0, U1, cls, S, key_a->data, key_b->data, limb_stride(key_a), i0,
-                               i1, full_ls),
-           "ks rows");
+    if (int rc = ks_decompose_rows(kc, S, (const char*)src + off, src_ls, U0, U1, cls, key_a, key_b,
+                                   i0, i1, full_ls))
+      return rc;
     LAUNCH(kc.t, rnt::K_COL_INV,
            rnt::launch_col_inv(kc, (char*)acc0->data + off, full_ls, U0, cls, 1, nullptr), "ks inverse");
     LAUNCH(kc.t, rnt::K_COL_INV,
