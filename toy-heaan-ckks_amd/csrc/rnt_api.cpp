@@ -511,6 +511,11 @@ int build_tables(rnt::Tables* t) {
     c.c1r_p = (W)shoup_companion(ninvr, q, wbits);
     c.c2r = (W)mulmod(w1, ninvr, q);
     c.c2r_p = (W)shoup_companion(c.c2r, q, wbits);
+    const uint64_t ninvrt = mulmod(ninvr, 4 % q, q);
+    c.c1t = (W)ninvrt;
+    c.c1t_p = (W)shoup_companion(ninvrt, q, wbits);
+    c.c2t = (W)mulmod(w1, ninvrt, q);
+    c.c2t_p = (W)shoup_companion(c.c2t, q, wbits);
     for (size_t i = 0; i < l; ++i) {
       const uint64_t qi = t->moduli[i];
       const uint64_t inv = invmod(q % qi, qi);
@@ -902,7 +907,8 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, out->data, a->data, out->ws, b->data, ls, ls, true),
          "column forward");
   LAUNCH(k.t, rnt::K_ROW_MUL, rnt::launch_row(k, 2, out->data, out->ws, ls, true), "row mul");
-  LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, out->data, ls, out->data, ls, 1, nullptr, true),
+  LAUNCH(k.t, rnt::K_COL_INV,
+         rnt::launch_col_inv(k, out->data, ls, out->data, ls, rnt::mul_truncated(k.t) ? 2 : 1, nullptr, true),
          "column inverse");
   out->in_ntt = 0;
   return RNT_OK;

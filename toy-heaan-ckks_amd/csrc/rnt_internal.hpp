@@ -47,6 +47,10 @@ struct LimbConst {
   W c1r_p;
   W c2r;     // psi_inv_rev[1] * n^-1 * 2^w
   W c2r_p;
+  W c1t;     // 4 n^-1 * 2^w             (last stage after a product truncated two stages early)
+  W c1t_p;
+  W c2t;     // psi_inv_rev[1] * 4 n^-1 * 2^w
+  W c2t_p;
 };
 
 // A twiddle and its Shoup companion, interleaved so one load fetches both.
@@ -183,6 +187,10 @@ hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* ou
 // on x); 2: poly-mul rows: x <- INVrow(FWDrow(x) (.) FWDrow(y) * 2^-w).
 hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls,
                       bool lazy = false);
+// Whether rnt_mul's row kernel stops its transforms two stages early and
+// multiplies degree-3 residues (u32 canonical bases, row length 2^(4k));
+// its inverse column pass then takes rfold = 2.
+bool mul_truncated(const Tables* t);
 // Inverse column pass with n^-1 folded into the last stage; rfold adds the
 // Montgomery factor 2^w.  addend (optional, coefficient domain, out layout).
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,

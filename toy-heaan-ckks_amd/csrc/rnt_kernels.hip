@@ -312,7 +312,9 @@ k_col_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, u
   W x[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) x[i] = in[ib + (uint64_t)i * C];
-  if (rfold)
+  if (rfold == 2)
+    col_gs<W, LOG_R>(x, itw, mod_of(lc), lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p);
+  else if (rfold)
     col_gs<W, LOG_R>(x, itw, mod_of(lc), lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p);
   else
     col_gs<W, LOG_R>(x, itw, mod_of(lc), lc.c1, lc.c1_p, lc.c2, lc.c2_p);
@@ -470,13 +472,15 @@ struct Fold {
 // CT stages on bits [BB, BB+K) for NOPS operands sharing twiddles.  `node0`
 // = heap index base of register 0: (heap root of this transform) * 2^LOGX +
 // its transform-local index, so stage s's node is node0 >> (s+1) + (i >> ...).
-template <class W, int NOPS, int LOGE, int K, int BB, class TS, class MO>
+// SLMIN > 0 stops SLMIN stages early (the truncated product transform); the
+// last stage run then leaves its outputs canonical.
+template <class W, int NOPS, int LOGE, int K, int BB, class TS, class MO, int SLMIN = 0>
 __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0, const TS& tw,
                                         const MO& mo) {
   if constexpr (kMeas == 2) return;
   constexpr int E = 1 << LOGE;
 #pragma unroll
-  for (int sl = K - 1; sl >= 0; --sl) {
+  for (int sl = K - 1; sl >= SLMIN; --sl) {
     constexpr int H = E > 1 ? E / 2 : 1;
     const int cnt = H >> sl;  // distinct twiddles at this stage
     const uint32_t nb = node0 >> (BB + sl + 1);
@@ -490,7 +494,7 @@ __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0,
       if (i & d) continue;
       const int m = i >> (sl + 1);
       // inside a pass, outputs the next stage only multiplies stay unreduced
-      const bool lazy = sl > 0 && (i & (d >> 1));
+      const bool lazy = sl > SLMIN && (i & (d >> 1));
 #pragma unroll
       for (int o = 0; o < NOPS; ++o) {
         if (lazy)
@@ -504,14 +508,15 @@ __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0,
 
 // GS stages; with FOLD the transform's top stage (bit LOGX-1, distance N/2
 // of the whole network) applies the folded n^-1 constants instead.
-template <class W, int NOPS, int LOGE, int K, int BB, int LOGX, bool FOLD, class TS, class MO>
+template <class W, int NOPS, int LOGE, int K, int BB, int LOGX, bool FOLD, class TS, class MO,
+          int SLMIN = 0>
 __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0, const TS& itw,
                                         const MO& mo, const Fold<W>& f) {
   if constexpr (kMeas == 2) return;
   const W bias = gs_bias(mo);
   constexpr int E = 1 << LOGE;
 #pragma unroll
-  for (int sl = 0; sl < K; ++sl) {
+  for (int sl = SLMIN; sl < K; ++sl) {
     constexpr int H = E > 1 ? E / 2 : 1;
     const int d = 1 << sl;
     if (FOLD && BB + sl + 1 == LOGX) {
@@ -574,21 +579,21 @@ struct XPos {
   uint32_t heap;
 };
 
-template <class G, class W, int NOPS, int PP, class TS, class MO>
+template <class G, class W, int NOPS, int PP, int SLMIN = 0, class TS, class MO>
 __device__ __forceinline__ void fwd_pass(W (&x)[NOPS][G::E], const XPos& xp, W* lds, const TS& tw,
                                          const MO& q) {
   constexpr int BB = G::bb(PP);
   if constexpr (PP > 0) xchg<G, W, NOPS, G::bb(PP - 1), BB>(x, lds, xp.slot, xp.tau);
-  pass_ct<W, NOPS, G::LOGE, G::k(PP), BB>(x, xp.heap + G::base(xp.tau, BB), tw, q);
+  pass_ct<W, NOPS, G::LOGE, G::k(PP), BB, TS, MO, SLMIN>(x, xp.heap + G::base(xp.tau, BB), tw, q);
 }
 
-template <class G, class W, int NOPS, int PP, bool FOLD, class TS, class MO>
+template <class G, class W, int NOPS, int PP, bool FOLD, int SLMIN = 0, class TS, class MO>
 __device__ __forceinline__ void inv_pass(W (&x)[NOPS][G::E], const XPos& xp, W* lds, const TS& itw,
                                          const MO& q, const Fold<W>& f) {
   constexpr int BB = G::bb(PP);
   if constexpr (PP < G::P - 1) xchg<G, W, NOPS, G::bb(PP + 1), BB>(x, lds, xp.slot, xp.tau);
-  pass_gs<W, NOPS, G::LOGE, G::k(PP), BB, G::LOGX_, FOLD>(x, xp.heap + G::base(xp.tau, BB), itw, q,
-                                                          f);
+  pass_gs<W, NOPS, G::LOGE, G::k(PP), BB, G::LOGX_, FOLD, TS, MO, SLMIN>(
+      x, xp.heap + G::base(xp.tau, BB), itw, q, f);
 }
 
 // All forward passes (first-pass distribution in, last-pass out).
@@ -763,7 +768,8 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
   const ColAddr<G, G::BBL> al(cp, log_c);
   const LimbConst<W> lc = tp.lc[cp.l];
   const auto itw = col_twiddles<W, G::UNIFORM>(tp.itw + (uint64_t)cp.l * N, N);
-  const Fold<W> f = rfold ? Fold<W>{lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p}
+  const Fold<W> f = rfold == 2 ? Fold<W>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p}
+                  : rfold ? Fold<W>{lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p}
                           : Fold<W>{lc.c1, lc.c1_p, lc.c2, lc.c2_p};
   const BufView<W> src(in + ip, N), dst(out + op, N);
   W x[1][E];
@@ -829,6 +835,62 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
   }
 }
 
+// ---- the truncated product (rnt_mul's row kernel, u32 canonical bases) ----
+// The forward transforms stop two stages early: block b of 4 consecutive
+// device-order words then holds the residue of the operand mod X^4 - zeta_b,
+// zeta_b = psi_rev[N/4 + b]^2 = (-1)^b psi_rev[N/8 + b/2] (the heap's
+// children square to their parent's root, and the odd child carries -1).
+// The product of two such residues is a degree-3 negacyclic-style product;
+// the inverse transforms skip the same two stages, and the inverse column
+// pass folds 4/N instead of 1/N (LimbConst c1t/c2t).  Exact arithmetic, so
+// the coefficient-domain result is bit-identical to the full transform's.
+template <int LOG_C>
+struct Trunc {
+  static constexpr bool on = LOG_C >= 4 && LOG_C % 4 == 0;  // last row pass = a whole radix-16 pass
+};
+template <class W, int LOG_C, bool LZ>
+constexpr bool trunc_mul() {
+  return sizeof(W) == 4 && !LZ && Trunc<LOG_C>::on;
+}
+
+// (T * 2^-32) mod q for T < 4 q^2 (a sum of four products of canonical
+// residues, q < 2^31): m = T q^-1 mod 2^32 makes T - m q a multiple of 2^32,
+// and hi(T) - hi(m q) lies in (-q, 2q).
+__device__ __forceinline__ uint32_t redc_sum4(uint64_t T, uint32_t q, uint32_t qinv) {
+  const uint32_t m = (uint32_t)T * qinv;
+  uint32_t t;
+  const bool neg = __builtin_sub_overflow((uint32_t)(T >> 32), mulhi(m, q), &t);
+  return neg ? t + q : csub<uint32_t>(t, q);
+}
+
+// c = a b mod (X^4 - zeta) for canonical residues, result * 2^-32 (the
+// product path's Montgomery factor, folded out by the inverse column pass).
+__device__ __forceinline__ void mul_mod_x4(uint32_t (&c)[4], const uint32_t* a, const uint32_t* b,
+                                           uint32_t zeta, uint32_t zeta_p, uint32_t q,
+                                           uint32_t qinv) {
+  const Mod<uint32_t> m{q, 0u - q};
+  const uint32_t b1 = shoup_mul(b[1], zeta, zeta_p, m);
+  const uint32_t b2 = shoup_mul(b[2], zeta, zeta_p, m);
+  const uint32_t b3 = shoup_mul(b[3], zeta, zeta_p, m);
+  const uint64_t t0 = mad64(a[3], b1, mad64(a[2], b2, mad64(a[1], b3, mul64(a[0], b[0]))));
+  const uint64_t t1 = mad64(a[3], b2, mad64(a[2], b3, mad64(a[1], b[0], mul64(a[0], b[1]))));
+  const uint64_t t2 = mad64(a[3], b3, mad64(a[2], b[0], mad64(a[1], b[1], mul64(a[0], b[2]))));
+  const uint64_t t3 = mad64(a[3], b[0], mad64(a[2], b[1], mad64(a[1], b[2], mul64(a[0], b[3]))));
+  c[0] = redc_sum4(t0, q, qinv);
+  c[1] = redc_sum4(t1, q, qinv);
+  c[2] = redc_sum4(t2, q, qinv);
+  c[3] = redc_sum4(t3, q, qinv);
+}
+
+// rnt_mul runs the Harvey-lazy kernels exactly when lazy30_ok(); otherwise
+// its u32 row kernel truncates when the row length allows (Trunc<LOG_C>).
+bool lazy30_ok(const Tables* t);
+bool mul_truncated(const Tables* t) {
+  if (t->wide || lazy30_ok(t)) return false;
+  const Geom g = geom_for(t->log_n);
+  return g.log_c >= 4 && g.log_c % 4 == 0;
+}
+
 // mode 0: forward rows in place; 1: inverse rows in place;
 // 2: poly-mul rows: x <- INV(FWD(x) (.) FWD(y)) with Montgomery pointwise.
 template <class W, int MODE, int LOG_C, bool LZ = false>
@@ -855,8 +917,33 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
       v[1][i] = gload(yg, base + b0 + ((uint32_t)i << G::BB0));
     }
     const auto mo = mod_for<W, LZ>(lc);
-    xf_fwd<G, W, 2>(v, rp.xp, lds, tw, mo);
     W z[1][E];
+    if constexpr (trunc_mul<W, LOG_C, LZ>()) {
+      // every pass but the last in full, the last without its two stages
+      if constexpr (G::P > 1) fwd_pass<G, W, 2, 0>(v, rp.xp, lds, tw, mo);
+      if constexpr (G::P > 2) fwd_pass<G, W, 2, 1>(v, rp.xp, lds, tw, mo);
+      if constexpr (G::P > 3) fwd_pass<G, W, 2, 2>(v, rp.xp, lds, tw, mo);
+      fwd_pass<G, W, 2, G::P - 1, 2>(v, rp.xp, lds, tw, mo);
+      // blocks t of 4 registers: device positions r*C + tau*E + 4t (G::BBL == 0)
+      static_assert(G::BBL == 0 && E == 16, "truncated product layout");
+      const uint32_t zb = (uint32_t)(N >> 3) + ((rp.r * (uint32_t)G::C) >> 3) + (rp.xp.tau << 1);
+      const Tw<W> zw[2] = {tw[zb], tw[zb + 1]};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const Tw<W> w = zw[t >> 1];
+        const uint32_t zeta = (t & 1) ? (uint32_t)lc.q - w.w : w.w;  // (-1)^b psi_rev[N/8 + b/2]
+        const uint32_t zeta_p = (t & 1) ? ~w.p : w.p;                  // Shoup companion of q - w
+        uint32_t c[4];
+        mul_mod_x4(c, &v[0][4 * t], &v[1][4 * t], zeta, zeta_p, lc.q, lc.qinv);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) z[0][4 * t + k] = c[k];
+      }
+      inv_pass<G, W, 1, G::P - 1, false, 2>(z, rp.xp, lds, itw, mo, Fold<W>{});
+      if constexpr (G::P > 3) inv_pass<G, W, 1, 2, false>(z, rp.xp, lds, itw, mo, Fold<W>{});
+      if constexpr (G::P > 2) inv_pass<G, W, 1, 1, false>(z, rp.xp, lds, itw, mo, Fold<W>{});
+      if constexpr (G::P > 1) inv_pass<G, W, 1, 0, false>(z, rp.xp, lds, itw, mo, Fold<W>{});
+    } else {
+    xf_fwd<G, W, 2>(v, rp.xp, lds, tw, mo);
     if constexpr (LZ) {
       // [0, 4q) inputs -> [0, 2q); a b < 4q^2 < q 2^32, so the Montgomery
       // quotient leaves (ab + mq) / 2^32 < 2q: the GS passes' input range
@@ -872,6 +959,7 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
       for (int i = 0; i < E; ++i) z[0][i] = mont_mul<W>(v[0][i], v[1][i], lc.q, lc.qinv);
     }
     xf_inv<G, W, 1>(z, rp.xp, lds, itw, mo);
+    }
     if (rp.active) {
 #pragma unroll
       for (int i = 0; i < E; ++i) gstore(xg, base + b0 + ((uint32_t)i << G::BB0), z[0][i]);
