@@ -274,12 +274,20 @@ def run_polymul(args, comm, world, rank, local_rank):
         "kernels": kernels,
     }
     if "row_mul" in kernels:
-        # the row kernel is VALU-bound: its butterflies (both
-        # forward row transforms and the inverse one) per second of its time
-        log_c = args.log_n - max(args.log_n // 2, 4) if args.log_n >= 8 else args.log_n
-        rb = 3 * elem * log_c // 2 * args.steps / kernels["row_mul"]["launches"]
+        # the row kernel is VALU-bound: the butterflies it
+        # executes (both forward row transforms and the inverse one) per
+        # second of its time.  With the truncated transform (u32 canonical
+        # bases, rows of 2^(4k) words) each row transform runs
+        # two stages fewer and the degree-3 block products are not counted.
+        log_r = max(args.log_n // 2, 4) if args.log_n >= 8 else max(args.log_n - 4, 0)
+        log_c = args.log_n - log_r
+        lazy = max(lmod) < (1 << 30) and log_r >= 5
+        trunc = wb == 4 and not lazy and log_c >= 4 and log_c % 4 == 0
+        stages = log_c - 2 if trunc else log_c
+        rb = 3 * elem * stages // 2 * args.steps / kernels["row_mul"]["launches"]
         ra = rb / (kernels["row_mul"]["avg_ms"] * 1e-3)
         roofline["valu"] = {"kernel": "row_mul", "unit": "butterflies/s", "bfly_per_launch": rb,
+                            "row_stages_per_transform": stages, "truncated_transform": trunc,
                             "achieved": ra, "peak": VALU_PEAK_BFLY, "frac": ra / VALU_PEAK_BFLY}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
