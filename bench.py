@@ -58,7 +58,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", choices=("polymul", "ctmul", "rotate", "encode"), default="polymul")
     p.add_argument("--shard", choices=("limb", "batch"), default="limb")
-    p.add_argument("--batch", type=int, default=256, help="poly-mul pairs per GPU per step")
+    p.add_argument("--batch", type=int, default=1024, help="poly-mul pairs per GPU per step")
+    p.add_argument("--inputs", choices=("device", "host"), default="device",
+                   help="poly-mul operands: seeded uniform residues drawn on the device (Philox, "
+                        "rnt_sample_uniform) or 16 seeded host pairs tiled to the batch and uploaded")
     p.add_argument("--ct-batch", type=int, default=128, help="ciphertext pairs per GPU per step (ctmul)")
     p.add_argument("--rot-batch", type=int, default=8, help="ciphertexts per rotation (rotate)")
     p.add_argument("--enc-batch", type=int, default=64, help="plaintexts per step (encode)")
@@ -207,14 +210,21 @@ def run_polymul(args, comm, world, rank, local_rank):
     B = rn.RnsBasis(lmod, n, device=local_rank)
     wb = 4 if max(lmod) < (1 << 31) else 8
 
-    # synthetic inputs: 16 seeded unique pairs tiled to the batch
-    rng = np.random.default_rng(1234 + (rank if args.shard == "batch" else 0))
-    uniq = min(16, batch)
-    a_u = uniform(rng, mod, uniq, n)[:, limbs.start:limbs.stop]
-    b_u = uniform(rng, mod, uniq, n)[:, limbs.start:limbs.stop]
-    reps = (batch + uniq - 1) // uniq
-    a = rn.RnsPoly.from_channels(np.tile(a_u, (reps, 1, 1))[:batch], B)
-    b = rn.RnsPoly.from_channels(np.tile(b_u, (reps, 1, 1))[:batch], B)
+    if args.inputs == "device":
+        # seeded uniform residues drawn on the device: no host copy of the
+        # gigabytes of operands (a rank's draws depend on its local limbs)
+        drng = rn.DeviceRng(1234 + rank)
+        a = rn.RnsPoly.sample_uniform(B, drng, batch)
+        b = rn.RnsPoly.sample_uniform(B, drng, batch)
+    else:
+        # 16 seeded unique pairs tiled to the batch
+        rng = np.random.default_rng(1234 + (rank if args.shard == "batch" else 0))
+        uniq = min(16, batch)
+        a_u = uniform(rng, mod, uniq, n)[:, limbs.start:limbs.stop]
+        b_u = uniform(rng, mod, uniq, n)[:, limbs.start:limbs.stop]
+        reps = (batch + uniq - 1) // uniq
+        a = rn.RnsPoly.from_channels(np.tile(a_u, (reps, 1, 1))[:batch], B)
+        b = rn.RnsPoly.from_channels(np.tile(b_u, (reps, 1, 1))[:batch], B)
     out = rn.RnsPoly(B, batch)
     lib = rn.load()
 
@@ -242,11 +252,16 @@ def run_polymul(args, comm, world, rank, local_rank):
     ms_per_step = elapsed / args.steps * 1e3
     value = weak_throughput(args.batch, world, elapsed, args.steps)  # global poly-muls / s
 
-    # spot parity of the timed output (this rank's limbs of pair 0) vs the oracle
+    # spot parity of the timed output (this rank's limbs of the first and the
+    # last pair) vs the oracle
     parity_ok = True
     if rank == 0:
         orc = oracle()
-        parity_ok = bool(np.array_equal(out.channels()[0], orc.mul(orc.Basis(lmod, n), a_u[0], b_u[0])))
+        ob = orc.Basis(lmod, n)
+        for pi in sorted({0, batch - 1}):
+            got = out.channels_of(pi)[0]
+            want = orc.mul(ob, a.channels_of(pi)[0], b.channels_of(pi)[0])
+            parity_ok &= bool(np.array_equal(got, want))
 
     # roofline of the dominant kernel: its algorithmic bytes per launch (at
     # the device word width) / its average launch time, measured with HIP
@@ -306,7 +321,8 @@ def run_polymul(args, comm, world, rank, local_rank):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32" if wb == 4 else "u64",
-        "data": "synthetic (seeded uniform residues)",
+        "data": ("synthetic (seeded uniform residues drawn on the device)" if args.inputs == "device"
+                 else "synthetic (seeded uniform residues, 16 host pairs tiled)"),
         "config": {
             "workload": f"coefficient-domain RNS-NTT poly-mul c=a*b, N=2^{args.log_n}, L={L} x "
                         f"{args.prime_bits}-bit primes",

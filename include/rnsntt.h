@@ -146,6 +146,10 @@ int rnt_upload_coeffs(rnt_buf* buf, const int64_t* coeffs, size_t n_polys);
 /* RnsPoly::channels (poly.rs:119-121): copies uint64_t[n_polys][L][N] out,
  * in the buffer's current domain (natural order when NTT). */
 int rnt_download(const rnt_buf* buf, uint64_t* host, size_t n_polys);
+/* channels() of polys [first, first + count) of a batch: uint64_t[count][L][N],
+ * in the buffer's current domain (natural order when NTT).  A range outside
+ * the batch -> RNT_ERR_BAD_ARGUMENT. */
+int rnt_download_polys(const rnt_buf* buf, uint64_t* host, size_t first, size_t count);
 int rnt_copy(rnt_buf* dst, const rnt_buf* src); /* Clone */
 /* PolyRing::to_coeffs (poly.rs:404-427) for a batch: per coefficient the CRT
  * value centred in (-Q/2, Q/2] (reconstruct_centered_coeff, basis.rs:158-180)

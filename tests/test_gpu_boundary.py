@@ -155,3 +155,23 @@ def test_small_keyswitch_scratch_chunks_every_ciphertext(gpu, monkeypatch):
         w0, w1 = orc.keyswitch(Bo, c[1][p], ka, kb)
         assert np.array_equal(g0[p], w0[:Lt]) and np.array_equal(g1[p], w1[:Lt]), p
 
+
+
+def test_download_polys_reads_a_sub_batch(gpu):
+    """rnt_download_polys: channels() of a range of a batch, in either
+    domain; ranges outside the batch are BadArgument."""
+    rn = gpu
+    n, L, B = 1 << 12, 3, 5
+    mod = rn.generate_primes(31, L, n)
+    Bd = rn.RnsBasis(mod, n)
+    x = _rand(np.random.default_rng(3), mod, n, B)
+    p = rn.RnsPoly.from_channels(x, Bd)
+    assert np.array_equal(p.channels_of(1, 3), x[1:4])
+    assert np.array_equal(p.channels_of(4), x[4:5])
+    p.to_ntt_domain()
+    full = p.channels()
+    assert np.array_equal(p.channels_of(2, 2), full[2:4])
+    assert p.channels_of(5, 0).shape == (0, L, n)
+    with pytest.raises(rn.RnsNttError) as e:
+        p.channels_of(4, 2)
+    assert e.value.kind == "BadArgument"

@@ -839,6 +839,28 @@ extern "C" int rnt_download(const rnt_buf* cb, uint64_t* host, size_t n_polys) {
   return RNT_OK;
 }
 
+extern "C" int rnt_download_polys(const rnt_buf* cb, uint64_t* host, size_t first, size_t count) {
+  rnt_buf* b = const_cast<rnt_buf*>(cb);  // staging only; contents unchanged
+  if (int rc = check_buf(b, "rnt_download_polys")) return rc;
+  if (!host) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_download_polys: null host pointer");
+  if (first > b->n_polys || count > b->n_polys - first)
+    return fail(RNT_ERR_BAD_ARGUMENT, "rnt_download_polys: polys [%zu, %zu) outside a batch of %zu",
+                first, first + count, b->n_polys);
+  if (count == 0) return RNT_OK;
+  if (int rc = set_device(b->ctx)) return rc;
+  rnt::Launch k = launch_for(b);
+  k.B = count;
+  const size_t n = k.t->n, words = count * b->ctx->L * n;
+  if (int rc = ensure_stage(b, words * 8)) return rc;
+  const char* src = (const char*)b->data + first * n * word_bytes(k.t);
+  LAUNCH(k.t, rnt::K_EXPORT, rnt::launch_export(k, (uint64_t*)b->stage, src, b->in_ntt, limb_stride(b)),
+         "export");
+  HIP_TRY(hipMemcpyAsync(host, b->stage, words * 8, hipMemcpyDeviceToHost, k.s), "hipMemcpy D2H");
+  HIP_TRY(hipStreamSynchronize(k.s), "hipStreamSynchronize");
+  trim_stage(b);
+  return RNT_OK;
+}
+
 extern "C" int rnt_copy(rnt_buf* dst, const rnt_buf* src) {
   if (int rc = check_buf(dst, "rnt_copy")) return rc;
   if (int rc = check_buf(src, "rnt_copy")) return rc;

@@ -216,7 +216,9 @@ hipError_t launch_automorphism(const Launch& k, void* out, const void* in, uint6
 hipError_t launch_import(const Launch& k, void* dst, const uint64_t* stage, int to_brv,
                          unsigned long long* err_index);
 hipError_t launch_import_coeffs(const Launch& k, void* dst, const int64_t* stage);
-hipError_t launch_export(const Launch& k, uint64_t* stage, const void* src, int from_brv);
+// k.B polys starting at src; ls = limb stride in words (0: k.B * N)
+hipError_t launch_export(const Launch& k, uint64_t* stage, const void* src, int from_brv,
+                         uint64_t ls = 0);
 // Key-switch pieces.  S: [L_target][L_source][k.B][N] scratch (chunk-local).
 hipError_t launch_ks_decompose(const Launch& k, void* S, const void* d, uint64_t d_ls);
 // u0 rows <- INVrow(sum_i FWDrow(S[j][i]) (.) key_b[i][j] (+ init0)), u1 with

@@ -1626,10 +1626,11 @@ static hipError_t import_coeffs_t(const Launch& k, void* dst, const int64_t* sta
 }
 
 template <class W>
-static hipError_t export_t(const Launch& k, uint64_t* stage, const void* src, int from_brv) {
+static hipError_t export_t(const Launch& k, uint64_t* stage, const void* src, int from_brv,
+                           uint64_t ls) {
   const uint64_t total = ((uint64_t)k.B * k.L) << k.t->log_n;
   if (total == 0) return hipSuccess;
-  const uint64_t ls = (uint64_t)k.B << k.t->log_n;
+  if (ls == 0) ls = (uint64_t)k.B << k.t->log_n;
   hipLaunchKernelGGL((k_export<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, stage,
                      (const W*)src, k.t->log_n, (uint32_t)k.L, ls, from_brv, total);
   return hipGetLastError();
@@ -1942,9 +1943,10 @@ hipError_t launch_import(const Launch& k, void* dst, const uint64_t* stage, int 
 hipError_t launch_import_coeffs(const Launch& k, void* dst, const int64_t* stage) {
   RNT_WIDE(import_coeffs_t<uint32_t>(k, dst, stage), import_coeffs_t<uint64_t>(k, dst, stage));
 }
-hipError_t launch_export(const Launch& k, uint64_t* stage, const void* src, int from_brv) {
-  RNT_WIDE(export_t<uint32_t>(k, stage, src, from_brv),
-           export_t<uint64_t>(k, stage, src, from_brv));
+hipError_t launch_export(const Launch& k, uint64_t* stage, const void* src, int from_brv,
+                         uint64_t ls) {
+  RNT_WIDE(export_t<uint32_t>(k, stage, src, from_brv, ls),
+           export_t<uint64_t>(k, stage, src, from_brv, ls));
 }
 hipError_t launch_ks_decompose(const Launch& k, void* S, const void* d, uint64_t d_ls) {
   RNT_WIDE(ks_decompose_t<uint32_t>(k, S, d, d_ls), ks_decompose_t<uint64_t>(k, S, d, d_ls));

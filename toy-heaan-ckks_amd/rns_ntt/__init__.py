@@ -334,6 +334,12 @@ class RnsPoly:
         check(load().rnt_download(self._h, _u64p(out), self.n_polys))
         return out[0] if self.n_polys == 1 else out
 
+    def channels_of(self, first: int, count: int = 1) -> np.ndarray:
+        """[count][L][N]: channels of polys first .. first+count-1 of the batch."""
+        out = np.zeros((count, self.basis.channel_count(), self.basis.degree), dtype=np.uint64)
+        check(load().rnt_download_polys(self._h, _u64p(out), int(first), int(count)))
+        return out
+
     def is_ntt_domain(self) -> bool:
         r = ctypes.c_int(0)
         check(load().rnt_buf_is_ntt(self._h, ctypes.byref(r)))

@@ -109,6 +109,7 @@ SIGNATURES = {
     "rnt_upload": (c_int, [_P, _U64P, c_size_t, c_size_t, c_int]),
     "rnt_upload_coeffs": (c_int, [_P, _I64P, c_size_t]),
     "rnt_download": (c_int, [_P, _U64P, c_size_t]),
+    "rnt_download_polys": (c_int, [_P, _U64P, c_size_t, c_size_t]),
     "rnt_copy": (c_int, [_P, _P]),
     "rnt_to_coeffs": (c_int, [_P, c_void_p, c_size_t]),
     "rnt_crt_centered": (c_int, [_P, c_void_p, c_size_t, c_size_t]),
