@@ -115,8 +115,15 @@ int rnt_ctx_channel_count(const rnt_ctx* ctx, size_t* count); /* basis.rs:116-11
 int rnt_ctx_moduli(const rnt_ctx* ctx, uint64_t* out);       /* basis.rs:108-110 */
 int rnt_ctx_total_bits(const rnt_ctx* ctx, uint32_t* bits);  /* basis.rs:140-145 */
 int rnt_ctx_psi(const rnt_ctx* ctx, size_t limb, uint64_t* psi);
-/* The context's HIP stream (hipStream_t) for event timing / interop. */
+/* The HIP stream (hipStream_t) the context's ops are queued on. */
 int rnt_ctx_stream(const rnt_ctx* ctx, void** stream);
+/* Queue later ops on the caller's `stream` (a hipStream_t of the context's
+ * device; NULL restores the context's own stream), ordered after everything
+ * already queued.  Applies to every context sharing the tables (drop_last
+ * views).  Call it while no other thread issues ops on those contexts; a
+ * caller's stream must outlive the context or be replaced first.  This is
+ * SURVEY §8b's per-op stream: set it around the ops that belong on it. */
+int rnt_ctx_set_stream(const rnt_ctx* ctx, void* stream);
 int rnt_sync(const rnt_ctx* ctx);
 
 /* ---- buffers == batches of RnsPoly ------------------------------------ */

@@ -175,3 +175,48 @@ def test_download_polys_reads_a_sub_batch(gpu):
     with pytest.raises(rn.RnsNttError) as e:
         p.channels_of(4, 2)
     assert e.value.kind == "BadArgument"
+
+
+def test_ops_follow_a_caller_stream(gpu):
+    """rnt_ctx_set_stream: with torch's stream bound, a product over wrapped
+    torch tensors waits for the torch work queued before it (a device sleep,
+    then the operand copies) and torch reads the result on the same stream,
+    with no host wait in between.  NULL restores the basis' own stream."""
+    import torch
+
+    rn = gpu
+    lib = rn.load()
+    n, L, B = 1 << 12, 4, 4
+    mod = rn.generate_primes(31, L, n)
+    Bd, Bo = rn.RnsBasis(mod, n), orc.Basis(mod, n)
+    own = Bd.stream()
+    rng = np.random.default_rng(21)
+    a_h, b_h = _rand(rng, mod, n, B), _rand(rng, mod, n, B)
+    want = np.stack([orc.mul(Bo, a_h[i], b_h[i]) for i in range(B)])
+    dev = torch.device("cuda", Bd.device)
+    # device layout [L][B][N] of 32-bit words (residues < 2^31 fit int32)
+    lay = lambda x: torch.from_numpy(np.ascontiguousarray(x.transpose(1, 0, 2)).astype(np.int32))  # noqa: E731
+    a_src, b_src = lay(a_h).to(dev), lay(b_h).to(dev)
+    torch.cuda.synchronize(dev)
+    a_t, b_t = torch.zeros_like(a_src), torch.zeros_like(b_src)
+    out_t = torch.zeros_like(a_src)
+    a = rn.RnsPoly.wrap(Bd, a_t.data_ptr(), B, owner=a_t)
+    b = rn.RnsPoly.wrap(Bd, b_t.data_ptr(), B, owner=b_t)
+    out = rn.RnsPoly.wrap(Bd, out_t.data_ptr(), B, owner=out_t)
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(20_000_000)  # the operands land well after the launch
+        a_t.copy_(a_src)
+        b_t.copy_(b_src)
+    Bd.set_stream(s)
+    assert Bd.stream() == s.cuda_stream
+    rn.check(lib.rnt_mul(out.handle, a.handle, b.handle))
+    with torch.cuda.stream(s):
+        res = out_t.clone()
+    s.synchronize()
+    got = res.cpu().numpy().astype(np.uint64).transpose(1, 0, 2)
+    assert np.array_equal(got, want)
+    Bd.set_stream(None)
+    assert Bd.stream() == own
+    # the own stream is ordered after the caller's: a download sees the product
+    assert np.array_equal(out.channels(), want)

@@ -367,9 +367,10 @@ int to_coeff_into(const rnt_buf* src, void* dst) {
 
 rnt::Tables::~Tables() {
   (void)hipSetDevice(device);
-  if (stream) {
-    (void)hipStreamSynchronize(stream);
-    (void)hipStreamDestroy(stream);
+  if (stream && stream != own_stream) (void)hipStreamSynchronize(stream);  // a caller's stream
+  if (own_stream) {
+    (void)hipStreamSynchronize(own_stream);
+    (void)hipStreamDestroy(own_stream);
   }
   for (auto& e : resc_ext) (void)hipFree(e.second);
   for (auto& e : crt_cache) (void)hipFree(e.second.dev);
@@ -590,7 +591,8 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     t->moduli.assign(moduli, moduli + count);
     int rc = wide ? build_tables<uint64_t>(t.get()) : build_tables<uint32_t>(t.get());
     if (rc != RNT_OK) return rc;
-    HIP_TRY(hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking), "hipStreamCreate");
+    HIP_TRY(hipStreamCreateWithFlags(&t->own_stream, hipStreamNonBlocking), "hipStreamCreate");
+    t->stream = t->own_stream;
     rnt_ctx* c = new rnt_ctx;
     c->t = std::move(t);
     c->L = count;
@@ -663,6 +665,31 @@ extern "C" int rnt_ctx_stream(const rnt_ctx* ctx, void** stream) {
   *stream = (void*)ctx->t->stream;
   return RNT_OK;
 }
+// Later ops go to `stream` (NULL: the context's own) after everything queued
+// so far: the new stream waits on an event recorded on the old one.
+extern "C" int rnt_ctx_set_stream(const rnt_ctx* ctx, void* stream) {
+  if (!ctx) return fail(RNT_ERR_BAD_ARGUMENT, "null ctx");
+  if (int rc = set_device(ctx)) return rc;
+  rnt::Tables* t = ctx->t.get();
+  hipStream_t next = stream ? (hipStream_t)stream : t->own_stream;
+  if (next == t->stream) return RNT_OK;
+  if (stream) {
+    hipDevice_t dev = -1;
+    HIP_TRY(hipStreamGetDevice(next, &dev), "hipStreamGetDevice");
+    if (dev != t->device)
+      return fail(RNT_ERR_BAD_ARGUMENT, "stream is on device %d, the context on device %d", (int)dev,
+                  t->device);
+  }
+  hipEvent_t ev;
+  HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  hipError_t e = hipEventRecord(ev, t->stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(next, ev, 0);
+  (void)hipEventDestroy(ev);  // released once it completes
+  if (e != hipSuccess) return hip_fail(e, "rnt_ctx_set_stream");
+  t->stream = next;
+  return RNT_OK;
+}
+
 extern "C" int rnt_sync(const rnt_ctx* ctx) {
   if (!ctx) return fail(RNT_ERR_BAD_ARGUMENT, "null ctx");
   if (int rc = set_device(ctx)) return rc;

@@ -93,7 +93,8 @@ struct Tables {
   void* lconst = nullptr;   // [L] LimbConst<W>
   void* resc = nullptr;     // [L][L]: resc[l][i] = (q_l mod q_i)^-1 mod q_i, i < l
   void* resc_p = nullptr;   // [L][L] Shoup companions
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // where every op is queued (rnt_ctx_set_stream)
+  hipStream_t own_stream = nullptr;  // created with the context
   // rnt_rescale_ext constants per external last modulus: device arrays
   // {inv[L], invp[L]} with inv[l] = (q_last mod q_l)^-1 mod q_l.
   std::mutex resc_mu;

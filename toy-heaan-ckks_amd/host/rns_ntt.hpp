@@ -135,6 +135,13 @@ class RnsBasis : public std::enable_shared_from_this<RnsBasis<N>> {
   }
   rnt_ctx* ctx() const { return ctx_; }
   void sync() const { check(rnt_sync(ctx_)); }
+  // hipStream_t the ops are queued on; set_stream(nullptr) restores the own one
+  void* stream() const {
+    void* s = nullptr;
+    check(rnt_ctx_stream(ctx_, &s));
+    return s;
+  }
+  void set_stream(void* s) const { check(rnt_ctx_set_stream(ctx_, s)); }
 
  private:
   explicit RnsBasis(rnt_ctx* c) : ctx_(c) {}

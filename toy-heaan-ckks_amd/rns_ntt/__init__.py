@@ -186,6 +186,14 @@ class RnsBasis:
         check(load().rnt_ctx_stream(self._h, ctypes.byref(r)))
         return int(r.value or 0)
 
+    def set_stream(self, stream=None) -> None:
+        """Queue later ops on ``stream`` (a raw hipStream_t address or a
+        ``torch.cuda.Stream``; None: the basis' own stream), after everything
+        queued so far.  Shared with every drop_last view of this basis."""
+        if stream is not None and not isinstance(stream, int):
+            stream = int(stream.cuda_stream)
+        check(load().rnt_ctx_set_stream(self._h, ctypes.c_void_p(stream or None)))
+
     def sync(self) -> None:
         check(load().rnt_sync(self._h))
 

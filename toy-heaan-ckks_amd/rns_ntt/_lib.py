@@ -101,6 +101,7 @@ SIGNATURES = {
     "rnt_ctx_total_bits": (c_int, [_P, POINTER(c_uint32)]),
     "rnt_ctx_psi": (c_int, [_P, c_size_t, _U64P]),
     "rnt_ctx_stream": (c_int, [_P, POINTER(_P)]),
+    "rnt_ctx_set_stream": (c_int, [_P, c_void_p]),
     "rnt_sync": (c_int, [_P]),
     "rnt_buf_alloc": (c_int, [_P, c_size_t, POINTER(_P)]),
     "rnt_buf_free": (c_int, [_P]),
@@ -156,6 +157,15 @@ def load(path: str | None = None) -> ctypes.CDLL:
             f"librnsntt.so not found at {path}: build it with `make` or "
             "`python -c 'import __graft_entry__ as g; g.build()'` (there is no CPU fallback)"
         )
+    # One HIP runtime per process: the torch wheel bundles its own
+    # libamdhip64.so.7, and whichever copy loads first serves both.  Loading
+    # /opt/rocm's first leaves torch without a GPU ("No HIP GPUs are
+    # available"), so when torch is installed it is imported before the
+    # library binds its runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
