@@ -37,6 +37,7 @@ METRIC = "RNS-NTT poly-muls/sec (N=2^16, 16 primes) at 1/2/4/8 GPUs; % HBM roofl
 CT_METRIC = "ct x ct -> relin -> rescale ciphertexts/sec (N=2^16, 16 primes, limb-sharded)"
 ROT_METRIC = "rotation key-switches/sec (N=2^17, 32 primes, power-of-two Galois offsets)"
 ENC_METRIC = "CKKS encode+decode round trips/sec (N=2^16, 16 primes, N/2 complex slots)"
+NTT_METRIC = "RNS-NTT forward+inverse transform pairs/sec (N=2^16, 16 primes)"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); ~6.3 TB/s achievable
 # VALU peak in radix-2 butterflies/s: all 1024 SIMDs (256 CUs
 # x 4) issue the canonical 31-bit CT butterfly -- 3 half-rate + 8 full-rate
@@ -56,7 +57,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=("polymul", "ctmul", "rotate", "encode"), default="polymul")
+    p.add_argument("--workload", choices=("polymul", "ctmul", "rotate", "encode", "ntt"), default="polymul")
     p.add_argument("--shard", choices=("limb", "batch"), default="limb")
     p.add_argument("--batch", type=int, default=1024, help="poly-mul pairs per GPU per step")
     p.add_argument("--inputs", choices=("device", "host"), default="device",
@@ -685,6 +686,105 @@ def run_encode(args, comm, world, rank, local_rank):
     }
 
 
+def run_ntt(args, comm, world, rank, local_rank):
+    """SURVEY §8a rows a4/a5 on their own: to_ntt_domain then to_coeff_domain
+    (poly.rs:136-166) of a batch of `--batch` polys over all limbs, in place.
+    One step = one forward and one inverse transform of the batch (column +
+    row launches each way); replicas at N > 1 (no collective)."""
+    import numpy as np
+
+    import rns_ntt as rn
+
+    n = 1 << args.log_n
+    L = args.limbs
+    mod = rn.generate_primes(args.prime_bits, L, n)
+    B = rn.RnsBasis(mod, n, device=local_rank)
+    wb = 4 if max(mod) < (1 << 31) else 8
+    batch = args.batch
+    x = rn.RnsPoly.sample_uniform(B, rn.DeviceRng(4321 + rank), batch)
+    first, last = x.channels_of(0)[0], x.channels_of(batch - 1)[0]
+
+    def step():
+        x.to_ntt_domain()
+        x.to_coeff_domain()
+
+    for _ in range(args.warmup):
+        step()
+    B.sync()
+    comm.barrier()
+    B.profile_enable(True)
+    B.sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    B.sync()
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = comm.max(t1 - t0)
+    kernels = {}
+    for k in ("col_fwd", "row_fwd", "row_inv", "col_inv"):
+        cnt, ms = B.profile_read(k)
+        if cnt:
+            kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
+    B.profile_enable(False)
+    # parity: the round trips returned the operands (bit-exact identity), and
+    # one more forward transform matches the oracle's natural-order NTT
+    parity_ok = bool(np.array_equal(x.channels_of(0)[0], first)
+                     and np.array_equal(x.channels_of(batch - 1)[0], last))
+    cpu = None
+    if rank == 0:
+        orc = oracle()
+        ob = orc.Basis(mod, n)
+        x.to_ntt_domain()
+        parity_ok &= bool(np.array_equal(x.channels_of(batch - 1)[0], orc.to_ntt(ob, last)))
+        if world == 1 and not args.no_cpu_baseline:
+            # the oracle's transforms (poly.rs:574-625) on one thread, as the
+            # reference runs them, on a bounded sample
+            done, el = 0, 0.0
+            while el < args.cpu_seconds / 2:
+                t = time.perf_counter()
+                orc.to_coeff(ob, orc.to_ntt(ob, first))
+                el += time.perf_counter() - t
+                done += 1
+            cpu = {"value": done / el, "unit": "transform pairs/s", "cores": 1, "kind": "port",
+                   "sample": f"{done} forward+inverse transforms of one poly (N={n}, L={L}) on one "
+                             f"thread, {el:.1f} s; oracle/oracle.c restating poly.rs:574-625",
+                   "host": host_info()}
+    # every launch moves its batch once in and once out: 2 L B N w bytes
+    alg = 2 * L * batch * n * wb
+    dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
+    achieved = alg / (kernels[dom]["avg_ms"] * 1e-3) / 1e9
+    value = batch * args.steps * world / elapsed
+    return {
+        "metric": NTT_METRIC,
+        "value": value,
+        "unit": "transform pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32" if wb == 4 else "u64",
+        "data": "synthetic (seeded uniform residues drawn on the device)",
+        "config": {
+            "workload": f"to_ntt_domain + to_coeff_domain in place, N=2^{args.log_n}, L={L} x "
+                        f"{args.prime_bits}-bit primes, {batch} polys per step",
+            "parallelism": f"replicas x{world}",
+            "parity_spot_check": parity_ok,
+        },
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic_for(dom, "ntt", batch, args.log_n, L),
+                     "alg_bytes_per_launch": alg,
+                     "whole_op_GBs": value / world * 4 * alg / batch / 1e9,
+                     "kernels": kernels},
+        "cpu_baseline": cpu,
+    }
+
+
 def run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod):
     """Config 5 limb-sharded: each rank owns L/world limbs of a
     global batch of rot_batch * world ciphertexts and a [L][L_r][N] slice of
@@ -759,12 +859,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
-    import rns_ntt  # noqa: F401  loads librnsntt.so (HIP runtime) before torch
+    import rns_ntt  # noqa: F401
     from rns_ntt.dist import Comm
 
     comm = Comm.from_env()
     run = {"polymul": run_polymul, "ctmul": run_ctmul, "rotate": run_rotate,
-           "encode": run_encode}[args.workload]
+           "encode": run_encode, "ntt": run_ntt}[args.workload]
     line = run(args, comm, world, rank, local_rank)
     if rank == 0:
         print(json.dumps(line), flush=True)
