@@ -858,6 +858,11 @@ def main():
         sys.exit(relaunch_with_torchrun(args))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("BENCH_ONE_DEVICE") == "1":
+        # rehearsal of the N-rank control plane on a one-GPU box: every rank
+        # on device 0 (poly-mul / ntt / encode only; RCCL refuses two ranks
+        # on one device)
+        local_rank = 0
 
     import rns_ntt  # noqa: F401
     from rns_ntt.dist import Comm
