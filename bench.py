@@ -77,6 +77,7 @@ def parse():
                    help="rotate: the log2(N/2) power-of-two offsets, or every offset 1..N/2-1 with "
                         "one resident key (SURVEY 8d sweep 2)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-power", action="store_true", help="skip the rocm-smi power/clock samples")
     return p.parse_args()
 
 
@@ -165,6 +166,54 @@ def cpu_baseline(mod, n, budget_s):
     }
 
 
+def power_probe(step, sync, device, seconds=3.0):
+    """Package power and graphics clock while `step` keeps the GPU busy for
+    `seconds` after the timed region: rocm-smi (read-only) sampled from a
+    thread, the first sample dropped as ramp-up.  Evidence for the power-cap
+    ceiling of DESIGN.md §4; None when rocm-smi is unavailable."""
+    import re
+    import statistics
+    import threading
+
+    def smi(*flags):
+        try:
+            return subprocess.run(["rocm-smi", "-d", str(device), *flags], capture_output=True,
+                                  text=True, timeout=15).stdout
+        except (OSError, subprocess.SubprocessError):
+            return ""
+
+    cap = re.search(r"Max Graphics Package Power \(W\):\s*([\d.]+)", smi("--showmaxpower"))
+    samples, stop = [], threading.Event()
+
+    def sampler():
+        while not stop.is_set():
+            out = smi("--showpower", "--showclocks")
+            w = re.search(r"Package Power \(W\):\s*([\d.]+)", out)
+            c = re.search(r"sclk clock level:[^(]*\((\d+)Mhz\)", out)
+            if not w:
+                return
+            samples.append((float(w.group(1)), int(c.group(1)) if c else None))
+
+    th = threading.Thread(target=sampler, daemon=True)
+    t_end = time.perf_counter() + seconds
+    th.start()
+    while time.perf_counter() < t_end:
+        for _ in range(8):
+            step()
+        sync()
+    stop.set()
+    th.join(timeout=20)
+    samples = samples[1:]
+    if not samples:
+        return None
+    clocks = [c for _, c in samples if c]
+    return {"package_w_median": statistics.median(w for w, _ in samples),
+            "sclk_mhz_median": statistics.median(clocks) if clocks else None,
+            "cap_w": float(cap.group(1)) if cap else None, "samples": len(samples),
+            "how": f"rocm-smi --showpower --showclocks on device {device} while the same step ran "
+                   f"{seconds:.0f} s more after the timed region"}
+
+
 def uniform(rng, mods, count, n):
     import numpy as np
 
@@ -249,6 +298,10 @@ def run_polymul(args, comm, world, rank, local_rank):
         if cnt:
             kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
     B.profile_enable(False)
+    power = None
+    if rank == 0 and not args.no_power:
+        power = power_probe(lambda: rn.check(lib.rnt_mul(out.handle, a.handle, b.handle)), B.sync,
+                            local_rank)
 
     ms_per_step = elapsed / args.steps * 1e3
     value = weak_throughput(args.batch, world, elapsed, args.steps)  # global poly-muls / s
@@ -336,6 +389,7 @@ def run_polymul(args, comm, world, rank, local_rank):
         },
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "power": power,
     }
 
 
@@ -728,6 +782,9 @@ def run_ntt(args, comm, world, rank, local_rank):
         if cnt:
             kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
     B.profile_enable(False)
+    power = None
+    if rank == 0 and not args.no_power:
+        power = power_probe(step, B.sync, local_rank)
     # parity: the round trips returned the operands (bit-exact identity), and
     # one more forward transform matches the oracle's natural-order NTT
     parity_ok = bool(np.array_equal(x.channels_of(0)[0], first)
@@ -782,6 +839,7 @@ def run_ntt(args, comm, world, rank, local_rank):
                      "whole_op_GBs": value / world * 4 * alg / batch / 1e9,
                      "kernels": kernels},
         "cpu_baseline": cpu,
+        "power": power,
     }
 
 

@@ -28,5 +28,5 @@ step bench 600 python bench.py --steps 20 --warmup 3
 step bench_ctmul 900 python bench.py --workload ctmul --ct-batch ${CT_BATCH:-128} --steps 3 --warmup 1
 step bench_rotate 900 python bench.py --workload rotate --rot-batch ${ROT_BATCH:-8} --steps 2 --warmup 1
 if [ "${PROFILE:-0}" = "1" ]; then
-  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof" -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/prof" -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-power
 fi

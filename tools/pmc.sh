@@ -7,7 +7,7 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 rocprofv3 -L > gpurun_out/pmc/counters_list.txt 2>&1 || true
 run() {  # run <tag> <counters...>
   local tag=$1; shift
-  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$ROOT/gpurun_out/pmc/$tag" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --batch 64 > gpurun_out/pmc/$tag.out 2> gpurun_out/pmc/$tag.err
+  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$ROOT/gpurun_out/pmc/$tag" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-power --batch 64 > gpurun_out/pmc/$tag.out 2> gpurun_out/pmc/$tag.err
   local rc=$?; echo "pmc $tag rc=$rc" >&2; [ $rc -lt 124 ] || exit $rc
 }
 run sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU

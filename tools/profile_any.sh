@@ -12,7 +12,7 @@ step() {
   timeout -k 10 600 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 bench.py $BARGS > "$OUT/$name.out" 2> "$OUT/$name.err"
   local rc=$?; echo "== $name rc=$rc" >&2; [ $rc -eq 0 ] || { tail -5 "$OUT/$name.err" >&2; exit $rc; }
 }
-BARGS="$* --no-cpu-baseline"
+BARGS="$* --no-cpu-baseline --no-power"
 step trace --kernel-trace --stats
 step fetch --pmc FETCH_SIZE
 step write --pmc WRITE_SIZE

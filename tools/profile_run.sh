@@ -20,7 +20,7 @@ step() {  # step <name> <seconds> <cmd...>
   echo "== $name rc=$rc" >&2
   if [ $rc -ne 0 ]; then tail -20 "$OUT/$name.err" >&2; exit $rc; fi
 }
-BENCH="bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline $*"
+BENCH="bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline --no-power $*"
 step trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH
 step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 $BENCH
 step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 $BENCH
