@@ -78,6 +78,9 @@ def parse():
                         "one resident key (SURVEY 8d sweep 2)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-power", action="store_true", help="skip the rocm-smi power/clock samples")
+    p.add_argument("--strong", action="store_true",
+                   help="poly-mul: --batch is the fixed global batch split over the ranks (strong "
+                        "scaling) instead of the per-GPU batch (weak, the default)")
     return p.parse_args()
 
 
@@ -244,17 +247,18 @@ def run_polymul(args, comm, world, rank, local_rank):
     import numpy as np
 
     import rns_ntt as rn
-    from rns_ntt.dist import limb_shard, weak_throughput
+    from rns_ntt.dist import limb_shard, shard
 
     n = 1 << args.log_n
     L = args.limbs
     mod = rn.generate_primes(args.prime_bits, L, n)
+    global_batch = args.batch if args.strong else args.batch * world
     if args.shard == "limb":
         limbs = limb_shard(L, world, rank)
-        batch = args.batch * world  # global batch, every rank holds its limbs of all of it
+        batch = global_batch  # every rank holds its limbs of the whole global batch
     else:
         limbs = range(L)
-        batch = args.batch
+        batch = shard(global_batch, world, rank)[1]  # its own pairs over all limbs
     lmod = mod[limbs.start:limbs.stop]
     Lr = len(lmod)
     B = rn.RnsBasis(lmod, n, device=local_rank)
@@ -302,9 +306,22 @@ def run_polymul(args, comm, world, rank, local_rank):
     if rank == 0 and not args.no_power:
         power = power_probe(lambda: rn.check(lib.rnt_mul(out.handle, a.handle, b.handle)), B.sync,
                             local_rank)
+    # the measured stream-copy bandwidth (report against it too):
+    # a device-to-device copy of one operand batch, read + write
+    copy_gbs = None
+    if rank == 0:
+        dst = rn.RnsPoly(B, batch)
+        rn.check(lib.rnt_copy(dst.handle, a.handle))
+        B.sync()
+        t = time.perf_counter()
+        for _ in range(5):
+            rn.check(lib.rnt_copy(dst.handle, a.handle))
+        B.sync()
+        copy_gbs = 5 * 2 * Lr * batch * n * wb / (time.perf_counter() - t) / 1e9
+        del dst
 
     ms_per_step = elapsed / args.steps * 1e3
-    value = weak_throughput(args.batch, world, elapsed, args.steps)  # global poly-muls / s
+    value = global_batch * args.steps / elapsed  # whole-job poly-muls / s (slowest rank's time)
 
     # spot parity of the timed output (this rank's limbs of the first and the
     # last pair) vs the oracle
@@ -340,6 +357,9 @@ def run_polymul(args, comm, world, rank, local_rank):
         "whole_op_GBs": per_gpu * 3 * L * n * wb / 1e9,
         "whole_op_frac": per_gpu * 3 * L * n * wb / 1e9 / HBM_PEAK_GBS,
         "whole_op_frac_u64_equiv": per_gpu * 3 * L * n * 8 / 1e9 / HBM_PEAK_GBS,
+        "stream_copy_GBs": copy_gbs,
+        "whole_op_frac_of_copy": per_gpu * 3 * L * n * wb / 1e9 / copy_gbs if copy_gbs else None,
+        "whole_op_frac_of_copy_u64_equiv": per_gpu * 3 * L * n * 8 / 1e9 / copy_gbs if copy_gbs else None,
         "kernels": kernels,
     }
     if "row_mul" in kernels:
@@ -372,7 +392,7 @@ def run_polymul(args, comm, world, rank, local_rank):
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "u32" if wb == 4 else "u64",
         "data": ("synthetic (seeded uniform residues drawn on the device)" if args.inputs == "device"
@@ -382,8 +402,8 @@ def run_polymul(args, comm, world, rank, local_rank):
                         f"{args.prime_bits}-bit primes",
             "N": n,
             "L": L,
-            "pairs_per_gpu_per_step": args.batch,
-            "global_batch": args.batch * world,
+            "pairs_per_gpu_per_step": global_batch / world,
+            "global_batch": global_batch,
             "parallelism": par,
             "parity_spot_check": parity_ok,
         },
@@ -405,13 +425,19 @@ def run_ctmul(args, comm, world, rank, local_rank):
     L = args.limbs
     mod = rn.generate_primes(31, L, n)
     torch.cuda.set_device(local_rank)
-    if world > 1:
+    # --shard limb (default): the north star's limb shard with RCCL joins;
+    # --shard batch: every rank runs the whole pipeline on its own
+    # ciphertexts over all limbs with a full key replica (SURVEY §8e's
+    # zero-collective fallback)
+    batch_shard = world > 1 and args.shard == "batch"
+    if world > 1 and not batch_shard:
         import torch.distributed as dist
 
         data_comm = TorchDistComm(dist.new_group(backend="nccl"))  # RCCL over xGMI
     else:
         data_comm = SingleComm()
-    B = args.ct_batch * world  # global ciphertext batch (weak scaling)
+    B_global = args.ct_batch * world  # weak scaling
+    B = args.ct_batch if batch_shard else B_global  # ciphertexts this rank's pipeline holds
     pipe = LimbShardedPipeline(mod, n, data_comm, GpuBackend(local_rank))
     rng = np.random.default_rng(77)
     uniq = min(4, B)
@@ -448,7 +474,7 @@ def run_ctmul(args, comm, world, rank, local_rank):
     t1 = time.perf_counter()
     comm.barrier()
     elapsed = comm.max(t1 - t0)
-    value = B * args.steps / elapsed
+    value = B_global * args.steps / elapsed
     kernels = {}
     for k in ("col_fwd", "tensor_rows", "col_inv", "ks_decompose", "ks_rows", "rescale", "elementwise"):
         cnt, ms = prof_basis.profile_read(k)
@@ -458,8 +484,8 @@ def run_ctmul(args, comm, world, rank, local_rank):
 
     parity_ok = None
     cpu = None
-    Lr = state0[2][rank]  # this rank's target limbs
-    if rank == 0 and world == 1:
+    Lr = state0[2][0 if batch_shard else rank]  # this rank's target limbs
+    if rank == 0 and (world == 1 or batch_shard):
         orc = oracle()
         ob = orc.Basis(mod, n)
         threads = usable_threads()
@@ -471,7 +497,7 @@ def run_ctmul(args, comm, world, rank, local_rank):
             o0, _ = orc.mul_ciphertexts_gadget(ob, cts[0][u], cts[1][u], cts[2][u], cts[3][u], key_a, key_b,
                                                threads=threads)
             parity_ok &= bool(np.array_equal(got[pi], orc.rescale(ob, o0)))
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:
             def t_pair(th):
                 t = time.perf_counter()
                 o0, o1 = orc.mul_ciphertexts_gadget(ob, cts[0][0], cts[1][0], cts[2][0], cts[3][0], key_a, key_b,
@@ -518,8 +544,9 @@ def run_ctmul(args, comm, world, rank, local_rank):
         "config": {
             "workload": f"ct x ct + gadget relin + rescale, N=2^{args.log_n}, L={L} x 31-bit primes",
             "ct_pairs_per_gpu_per_step": args.ct_batch,
-            "global_batch": B,
-            "parallelism": f"limb-sharded x{world}: RCCL all-gather of d2, broadcast of q_L limb",
+            "global_batch": B_global,
+            "parallelism": (f"batch-sharded x{world}: no collective, full key per GPU" if batch_shard else
+                            f"limb-sharded x{world}: RCCL all-gather of d2, broadcast of q_L limb"),
             "parity_spot_check": parity_ok,
             "parity_pairs": sorted({0, B - 1}),
         },
@@ -922,6 +949,13 @@ def main():
         # on one device)
         local_rank = 0
 
+    # the JSON line is the only thing on stdout: everything else written to
+    # fd 1 (gloo's and RCCL's connection messages, library prints) goes to
+    # stderr, and the line goes to a private copy of the original stdout
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
     import rns_ntt  # noqa: F401
     from rns_ntt.dist import Comm
 
@@ -930,7 +964,8 @@ def main():
            "encode": run_encode, "ntt": run_ntt}[args.workload]
     line = run(args, comm, world, rank, local_rank)
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        result_out.write(json.dumps(line) + "\n")
+        result_out.flush()
     comm.close()
 
 
