@@ -623,23 +623,6 @@ struct RowPos {
   bool active;
 };
 
-template <class G>
-__device__ __forceinline__ RowPos row_pos(uint32_t log_n, uint32_t B, uint64_t rows_total) {
-  RowPos rp;
-  rp.xp.slot = G::slot_of(threadIdx.x);
-  rp.xp.tau = G::tau_of(threadIdx.x);
-  uint64_t row = (uint64_t)blockIdx.x * G::RPW + rp.xp.slot;
-  rp.active = row < rows_total;
-  if (!rp.active) row = 0;
-  const uint32_t log_r = log_n - G::LOGC;
-  const uint64_t lp = row >> log_r;
-  rp.r = (uint32_t)(row & ((1u << log_r) - 1u));
-  rp.l = (uint32_t)(lp / B);
-  rp.p = (uint32_t)(lp - (uint64_t)rp.l * B);
-  rp.xp.heap = (1u << log_n) + rp.r * (uint32_t)G::C;  // (R + r) * C
-  return rp;
-}
-
 // Row coordinates with the poly index fastest: row = ((l * R + r) * B + p).
 // Consecutive rows of a workgroup then share (limb, row r), so whatever they
 // read per (limb, r) -- gadget-key rows, twiddles -- is fetched from HBM once
@@ -901,7 +884,9 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
-  const RowPos rp = row_pos<G>(log_n, B, rows_total);
+  // poly index fastest: a workgroup's rows share (limb, row r) and with it
+  // every twiddle, which then comes from L1 (profiles/r02_ab_row_pfast.txt)
+  const RowPos rp = row_pos_pfast<G>(log_n, B, rows_total);
   const uint64_t N = 1ull << log_n;
   const uint64_t base = (uint64_t)rp.l * ls + (uint64_t)rp.p * N + (uint64_t)rp.r * G::C;
   const LimbConst<W> lc = tp.lc[rp.l];
@@ -1139,7 +1124,7 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
-  const RowPos rp = row_pos<G>(log_n, B, rows_total);
+  const RowPos rp = row_pos_pfast<G>(log_n, B, rows_total);  // shared twiddles, as in k_row
   const uint64_t N = 1ull << log_n;
   const uint64_t base = (uint64_t)rp.l * ls + (uint64_t)rp.p * N + (uint64_t)rp.r * G::C;
   const LimbConst<W> lc = tp.lc[rp.l];
