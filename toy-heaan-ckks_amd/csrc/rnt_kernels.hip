@@ -1114,8 +1114,11 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   }
 }
 
+// 4 waves per SIMD (<= 128 VGPRs; unconstrained it takes 134-154 and runs
+// at 3): tensor_rows 1.74 -> 1.64 ms per 64 cts (profiles/r02_ab_tensor_waves.txt)
+constexpr int kTensorMinWaves = 4;
 template <class W, int LOG_C>
-__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS)
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kTensorMinWaves : 1)
 k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2row,
               const W* __restrict__ c0, const W* __restrict__ c1, const W* __restrict__ c0p,
               const W* __restrict__ c1p, TabPtrs<W> tp, uint32_t log_n, uint32_t B, uint64_t ls,
