@@ -778,7 +778,7 @@ template <class W, int LOG_R, int LOG_TC>
 __global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32_t log_n,
                  uint32_t log_c, uint32_t L, uint32_t B, uint64_t d_ls, uint32_t Lt,
-                 uint32_t jg) {
+                 uint32_t jg, uint32_t lift_csub) {
   using G = ColGeo<LOG_R, LOG_TC>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -807,8 +807,15 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
     const BufView<W> dst(S + (((uint64_t)j * L + i) * B + p) * N, N);
     const LimbConst<W> lc = tp.lc[j];
     W x[1][E];
+    // alpha_i mod q_j: one conditional subtraction when every word is below
+    // 2 q_j (u32 words, all target q_j > 2^30), else a Shoup reduction
+    if (lift_csub) {
 #pragma unroll
-    for (int e = 0; e < E; ++e) x[0][e] = shoup_mul<W>(raw[e], (W)1, lc.one_p, lc.q);
+      for (int e = 0; e < E; ++e) x[0][e] = csub<W>(raw[e], lc.q);
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) x[0][e] = shoup_mul<W>(raw[e], (W)1, lc.one_p, lc.q);
+    }
     // (the transform's LDS exchange ends in a barrier: the next j may reuse it)
     xf_fwd<G, W, 1>(x, cp.xp, lds, col_twiddles<W, G::UNIFORM>(tp.tw + (uint64_t)j * N, N),
                     mod_of(lc));
@@ -1643,13 +1650,20 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
       while (jg > 1 && ((uint32_t)k.L + jg - 1) / jg * (uint64_t)g0.x * Ls < 1024u) jg >>= 1;
     }
     const dim3 grid(((uint32_t)k.L + jg - 1) / jg, g0.x, Ls);
+    // u32 words hold residues of moduli < 2^31 (wider bases take u64), so
+    // alpha_i < 2^31 <= 2 q_j when every target modulus is >= 2^30: one
+    // conditional subtraction reduces it (the root basis' smallest modulus
+    // bounds every drop_last view's)
+    uint64_t qmin = ~0ull;
+    for (uint64_t q : k.t->moduli) qmin = q < qmin ? q : qmin;
+    const uint32_t lift_csub = sizeof(W) == 4 && qmin >= (1ull << 30) ? 1u : 0u;
     hipError_t e = hipSuccess;
 #define RNT_L2(R, TC)                                                                         \
   e = allow_lds(k_colt_decompose<W, R, TC>, col_lds<W, R, TC>());                             \
   if (e != hipSuccess) return e;                                                              \
   hipLaunchKernelGGL((k_colt_decompose<W, R, TC>), grid, dim3(ColGeo<R, TC>::THREADS),        \
                      (col_lds<W, R, TC>()), k.s, (W*)S, (const W*)d, tp, g.log_n, g.log_c,      \
-                     Ls, (uint32_t)k.B, d_ls, (uint32_t)k.L, jg)
+                     Ls, (uint32_t)k.B, d_ls, (uint32_t)k.L, jg, lift_csub)
 #define RNT_L(R)                          \
   if (col_log_tc(g) == 6) {               \
     RNT_L2(R, 6);                         \
