@@ -1039,7 +1039,6 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   const uint64_t N = 1ull << log_n;
   const uint32_t j = rp.l;
   const uint64_t rowoff = (uint64_t)rp.r * G::C;
-  const uint64_t obase = (uint64_t)j * ls + (uint64_t)rp.p * N + rowoff;
   const uint64_t ibase = (uint64_t)j * init_ls + (uint64_t)rp.p * N + rowoff;
   const LimbConst<W> lc = tp.lc[j];
   const Tw<W>* tw = tp.tw + (uint64_t)j * N;
@@ -1106,17 +1105,24 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     }
   }
   // the two accumulators' inverse rows one after the other (half the live
-  // registers of a two-operand pass)
+  // registers of a two-operand pass).  The thread coordinates pass through
+  // an opaque copy, so the inverse passes' twiddle and store addresses are
+  // derived here rather than computed before the loop and spilled across it
+  XPos xq = rp.xp;
+  uint32_t pq = rp.p;
+  asm volatile("" : "+v"(xq.tau), "+v"(pq));
+  const uint64_t oq = (uint64_t)j * ls + (uint64_t)pq * N + rowoff;
+  const uint32_t b0q = G::base(xq.tau, G::BB0);
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
     W v[1][E];
 #pragma unroll
     for (int e = 0; e < E; ++e) v[0][e] = acc[o][e];
-    xf_inv<G, W, 1>(v, rp.xp, lds, itw, mod_of(lc));
+    xf_inv<G, W, 1>(v, xq, lds, itw, mod_of(lc));
     W* uo = o == 0 ? u0 : u1;
     if (rp.active) {
 #pragma unroll
-      for (int e = 0; e < E; ++e) uo[obase + b0 + ((uint32_t)e << G::BB0)] = v[0][e];
+      for (int e = 0; e < E; ++e) uo[oq + b0q + ((uint32_t)e << G::BB0)] = v[0][e];
     }
   }
 }
