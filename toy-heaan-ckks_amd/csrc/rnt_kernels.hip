@@ -1217,17 +1217,22 @@ template <class W>
 __global__ void __launch_bounds__(256)
 k_rescale(W* __restrict__ out, const W* __restrict__ in, const W* __restrict__ lastp,
           const W* __restrict__ inv_t, const W* __restrict__ invp_t, TabPtrs<W> tp,
-          uint64_t ls_in, uint64_t ls_out, uint64_t poly_words, uint64_t total) {
-  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;
-  const uint32_t l = (uint32_t)(gid / poly_words);
-  const uint64_t off = gid - (uint64_t)l * poly_words;
-  const LimbConst<W> lc = tp.lc[l];
-  const W inv = inv_t[l];    // (q_last mod q_l)^-1 mod q_l
-  const W invp = invp_t[l];
-  const W ci = in[(uint64_t)l * ls_in + off];
-  const W cl = shoup_mul<W>(lastp[off], (W)1, lc.one_p, lc.q);  // canonical c_last mod q_l (R5)
-  out[(uint64_t)l * ls_out + off] = shoup_mul<W>(sub_mod<W>(ci, cl, lc.q), inv, invp, lc.q);
+          uint64_t ls_in, uint64_t ls_out, uint64_t poly_words, uint32_t limbs) {
+  // one thread per coefficient position over every kept limb: c_last is read
+  // once per position, not once per limb (the per-(limb, position) form read
+  // the last plane L - 1 times)
+  const uint64_t off = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (off >= poly_words) return;
+  const W last = lastp[off];
+#pragma unroll 4
+  for (uint32_t l = 0; l < limbs; ++l) {
+    const LimbConst<W> lc = tp.lc[l];
+    const W inv = inv_t[l];  // (q_last mod q_l)^-1 mod q_l
+    const W invp = invp_t[l];
+    const W ci = in[(uint64_t)l * ls_in + off];
+    const W cl = shoup_mul<W>(last, (W)1, lc.one_p, lc.q);  // canonical c_last mod q_l (R5)
+    out[(uint64_t)l * ls_out + off] = shoup_mul<W>(sub_mod<W>(ci, cl, lc.q), inv, invp, lc.q);
+  }
 }
 
 // XCD-aware deal for the gather kernels: hardware block b runs on XCD b % 8,
@@ -1563,9 +1568,9 @@ static hipError_t rescale_t(const Launch& k, void* out, const void* in) {
   if (total == 0) return hipSuccess;
   const TabPtrs<W> tp = tab_ptrs<W>(k.t);
   const uint64_t last = k.L - 1;
-  hipLaunchKernelGGL((k_rescale<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, (W*)out,
+  hipLaunchKernelGGL((k_rescale<W>), dim3(grid_for(pw, 256)), dim3(256), 0, k.s, (W*)out,
                      (const W*)in, (const W*)in + last * pw, tp.resc + last * tp.Lroot,
-                     tp.rescp + last * tp.Lroot, tp, pw, pw, pw, total);
+                     tp.rescp + last * tp.Lroot, tp, pw, pw, pw, (uint32_t)last);
   return hipGetLastError();
 }
 
@@ -1577,9 +1582,9 @@ static hipError_t rescale_ext_t(const Launch& k, void* out, const void* in, cons
   const uint64_t pw = (uint64_t)k.B << k.t->log_n;
   const uint64_t total = pw * k.L;
   if (total == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_rescale<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, (W*)out,
+  hipLaunchKernelGGL((k_rescale<W>), dim3(grid_for(pw, 256)), dim3(256), 0, k.s, (W*)out,
                      (const W*)in, (const W*)lastp, (const W*)inv, (const W*)invp, tab_ptrs<W>(k.t),
-                     pw, pw, pw, total);
+                     pw, pw, pw, (uint32_t)k.L);
   return hipGetLastError();
 }
 
