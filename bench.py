@@ -38,6 +38,7 @@ CT_METRIC = "ct x ct -> relin -> rescale ciphertexts/sec (N=2^16, 16 primes, lim
 ROT_METRIC = "rotation key-switches/sec (N=2^17, 32 primes, power-of-two Galois offsets)"
 ENC_METRIC = "CKKS encode+decode round trips/sec (N=2^16, 16 primes, N/2 complex slots)"
 NTT_METRIC = "RNS-NTT forward+inverse transform pairs/sec (N=2^16, 16 primes)"
+PW_METRIC = "NTT-domain pointwise poly-muls/sec (N=2^16, 16 primes)"
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); ~6.3 TB/s achievable
 # VALU peak in radix-2 butterflies/s: all 1024 SIMDs (256 CUs
 # x 4) issue the canonical 31-bit CT butterfly -- 3 half-rate + 8 full-rate
@@ -57,7 +58,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=("polymul", "ctmul", "rotate", "encode", "ntt"), default="polymul")
+    p.add_argument("--workload", choices=("polymul", "ctmul", "rotate", "encode", "ntt", "pointwise"), default="polymul")
     p.add_argument("--shard", choices=("limb", "batch"), default="limb")
     p.add_argument("--batch", type=int, default=1024, help="poly-mul pairs per GPU per step")
     p.add_argument("--inputs", choices=("device", "host"), default="device",
@@ -870,6 +871,81 @@ def run_ntt(args, comm, world, rank, local_rank):
     }
 
 
+def run_pointwise(args, comm, world, rank, local_rank):
+    """SURVEY §8d's secondary figure: MulAssign with both operands in the NTT
+    domain (poly.rs:297-306, a Montgomery pointwise product per residue),
+    `--batch` pairs per step, in place of the first operand's copy."""
+    import numpy as np
+
+    import rns_ntt as rn
+
+    n = 1 << args.log_n
+    L = args.limbs
+    mod = rn.generate_primes(args.prime_bits, L, n)
+    B = rn.RnsBasis(mod, n, device=local_rank)
+    wb = 4 if max(mod) < (1 << 31) else 8
+    batch = args.batch
+    drng = rn.DeviceRng(777 + rank)
+    a = rn.RnsPoly.sample_uniform(B, drng, batch)
+    b = rn.RnsPoly.sample_uniform(B, drng, batch)
+    a.to_ntt_domain()
+    b.to_ntt_domain()
+    out = rn.RnsPoly(B, batch)
+    lib = rn.load()
+    for _ in range(args.warmup):
+        rn.check(lib.rnt_mul(out.handle, a.handle, b.handle))
+    B.sync()
+    comm.barrier()
+    B.profile_enable(True)
+    B.sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rn.check(lib.rnt_mul(out.handle, a.handle, b.handle))
+    B.sync()
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = comm.max(t1 - t0)
+    cnt, ms = B.profile_read("elementwise")
+    B.profile_enable(False)
+    parity_ok = True
+    if rank == 0:
+        orc = oracle()
+        ob = orc.Basis(mod, n)
+        for pi in sorted({0, batch - 1}):
+            want = orc.mul(ob, a.channels_of(pi)[0], b.channels_of(pi)[0], ntt=True)
+            parity_ok &= bool(np.array_equal(out.channels_of(pi)[0], want))
+    alg = 3 * L * batch * n * wb  # read a, read b, write out
+    achieved = alg / (ms / cnt * 1e-3) / 1e9 if cnt else None
+    value = batch * args.steps * world / elapsed
+    return {
+        "metric": PW_METRIC,
+        "value": value,
+        "unit": "poly-muls/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32" if wb == 4 else "u64",
+        "data": "synthetic (seeded uniform residues drawn on the device, transformed)",
+        "config": {
+            "workload": f"NTT-domain MulAssign, N=2^{args.log_n}, L={L} x {args.prime_bits}-bit primes, "
+                        f"{batch} pairs per step",
+            "parallelism": f"replicas x{world}",
+            "parity_spot_check": parity_ok,
+        },
+        "roofline": {"bound": "hbm", "kernel": "elementwise", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                     "traffic": None, "alg_bytes_per_launch": alg,
+                     "kernels": {"elementwise": {"launches": cnt, "avg_ms": ms / cnt if cnt else None,
+                                                 "total_ms": ms}}},
+        "cpu_baseline": None,
+    }
+
+
 def run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod):
     """Config 5 limb-sharded: each rank owns L/world limbs of a
     global batch of rot_batch * world ciphertexts and a [L][L_r][N] slice of
@@ -961,7 +1037,8 @@ def main():
 
     comm = Comm.from_env()
     run = {"polymul": run_polymul, "ctmul": run_ctmul, "rotate": run_rotate,
-           "encode": run_encode, "ntt": run_ntt}[args.workload]
+           "encode": run_encode, "ntt": run_ntt,
+           "pointwise": run_pointwise}[args.workload]
     line = run(args, comm, world, rank, local_rank)
     if rank == 0:
         result_out.write(json.dumps(line) + "\n")

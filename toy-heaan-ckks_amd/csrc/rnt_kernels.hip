@@ -1188,28 +1188,44 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
 // elementwise / permutation kernels
 // ---------------------------------------------------------------------------
 
-template <class W>
+template <class W, int OP>
+__device__ __forceinline__ W elementwise_op(W x, W y, const LimbConst<W>& lc) {
+  if constexpr (OP == 0) return add_mod<W>(x, y, lc.q);
+  else if constexpr (OP == 1) return sub_mod<W>(x, y, lc.q);
+  else if constexpr (OP == 2) return x == 0 ? (W)0 : (W)(lc.q - x);
+  else if constexpr (OP == 3) return shoup_mul<W>(mont_mul<W>(x, y, lc.q, lc.qinv), lc.rmod, lc.rmod_p, lc.q);
+  else return mont_mul<W>(x, y, lc.q, lc.qinv);
+}
+
+// Coefficient-wise ops (poly.rs:254-306, 370-385).  Grid: x = chunks of one
+// limb's B*N words, y = limb, so the limb constants are wave-uniform (no
+// per-thread division).  VEC: every thread moves 16 bytes per operand
+// (callers check 16-byte alignment and a limb length divisible by it).
+template <class W, int OP, bool VEC>
 __global__ void __launch_bounds__(256)
-k_elementwise(W* __restrict__ out, const W* __restrict__ a, const W* __restrict__ b, int op,
-              TabPtrs<W> tp, uint64_t limb_words, uint64_t total) {
-  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;
-  const uint32_t l = (uint32_t)(gid / limb_words);
+k_elementwise(W* __restrict__ out, const W* __restrict__ a, const W* __restrict__ b,
+              TabPtrs<W> tp, uint64_t limb_words) {
+  constexpr int V = VEC ? 16 / (int)sizeof(W) : 1;
+  const uint32_t l = blockIdx.y;
+  const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * V;
+  if (i >= limb_words) return;
   const LimbConst<W> lc = tp.lc[l];
-  const W x = a[gid];
-  W r;
-  switch (op) {
-    case 0: r = add_mod<W>(x, b[gid], lc.q); break;
-    case 1: r = sub_mod<W>(x, b[gid], lc.q); break;
-    case 2: r = x == 0 ? (W)0 : (W)(lc.q - x); break;
-    case 3: {
-      const W m = mont_mul<W>(x, b[gid], lc.q, lc.qinv);
-      r = shoup_mul<W>(m, lc.rmod, lc.rmod_p, lc.q);
-      break;
-    }
-    default: r = mont_mul<W>(x, b[gid], lc.q, lc.qinv);
+  const uint64_t g = (uint64_t)l * limb_words + i;
+  if constexpr (VEC) {
+    const uint4 xa = *reinterpret_cast<const uint4*>(a + g);
+    uint4 xb = xa;
+    if constexpr (OP != 2) xb = *reinterpret_cast<const uint4*>(b + g);
+    W x[V], y[V], r[V];
+    __builtin_memcpy(x, &xa, 16);
+    __builtin_memcpy(y, &xb, 16);
+#pragma unroll
+    for (int v = 0; v < V; ++v) r[v] = elementwise_op<W, OP>(x[v], y[v], lc);
+    uint4 o;
+    __builtin_memcpy(&o, r, 16);
+    *reinterpret_cast<uint4*>(out + g) = o;
+  } else {
+    out[g] = elementwise_op<W, OP>(a[g], OP == 2 ? (W)0 : b[g], lc);
   }
-  out[gid] = r;
 }
 
 // rescale_into (poly.rs:212-225): out[l] = (c_l - (c_last mod q_l)) * q_last^-1.
@@ -1553,10 +1569,28 @@ template <class W>
 static hipError_t elementwise_t(const Launch& k, int op, void* out, const void* a,
                                 const void* b) {
   const uint64_t limb_words = (uint64_t)k.B << k.t->log_n;
-  const uint64_t total = limb_words * k.L;
-  if (total == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_elementwise<W>), dim3(grid_for(total, 256)), dim3(256), 0, k.s, (W*)out,
-                     (const W*)a, (const W*)b, op, tab_ptrs<W>(k.t), limb_words, total);
+  if (limb_words == 0 || k.L == 0) return hipSuccess;
+  constexpr int V = 16 / (int)sizeof(W);
+  const bool vec = limb_words % V == 0 && ((uintptr_t)out | (uintptr_t)a | (uintptr_t)b) % 16 == 0;
+  const uint64_t per = vec ? limb_words / V : limb_words;
+  const uint64_t bx = (per + 255) / 256;
+  if (bx > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  const dim3 grid((unsigned)bx, (unsigned)k.L);
+#define RNT_EW(OP)                                                                              \
+  if (vec)                                                                                      \
+    hipLaunchKernelGGL((k_elementwise<W, OP, true>), grid, dim3(256), 0, k.s, (W*)out,         \
+                       (const W*)a, (const W*)b, tab_ptrs<W>(k.t), limb_words);                \
+  else                                                                                          \
+    hipLaunchKernelGGL((k_elementwise<W, OP, false>), grid, dim3(256), 0, k.s, (W*)out,        \
+                       (const W*)a, (const W*)b, tab_ptrs<W>(k.t), limb_words);
+  switch (op) {
+    case 0: RNT_EW(0) break;
+    case 1: RNT_EW(1) break;
+    case 2: RNT_EW(2) break;
+    case 3: RNT_EW(3) break;
+    default: RNT_EW(4) break;
+  }
+#undef RNT_EW
   return hipGetLastError();
 }
 
