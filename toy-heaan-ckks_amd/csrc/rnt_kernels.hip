@@ -1251,11 +1251,12 @@ k_rescale(W* __restrict__ out, const W* __restrict__ in, const W* __restrict__ l
   }
 }
 
-// XCD-aware deal for the gather kernels: hardware block b runs on XCD b % 8,
-// and the grid is a multiple of 8, so logical block (b % 8) * (grid / 8) +
-// b / 8 gives every XCD a contiguous run of logical blocks -- whole polys,
-// whose scattered gathers then stay in that XCD's L2 instead of every XCD
-// fetching every poly.
+// Gather kernels: grid y = limb, x = the limb's B*N words (no per-thread
+// division).  XCD-aware deal along x: hardware block b of a row runs on XCD
+// b % 8 (gridDim.x is a multiple of 8), so logical block (b % 8) *
+// (gridDim.x / 8) + b / 8 gives every XCD a contiguous run of the limb --
+// whole polys, whose scattered gathers then stay in that XCD's L2 instead
+// of every XCD fetching every poly.
 __device__ __forceinline__ uint64_t xcd_gid() {
   const uint32_t per_xcd = gridDim.x >> 3;
   const uint32_t wg = (blockIdx.x & 7u) * per_xcd + (blockIdx.x >> 3);
@@ -1267,11 +1268,12 @@ template <class W>
 __global__ void __launch_bounds__(256)
 k_automorph_odd(W* __restrict__ out, const W* __restrict__ in, TabPtrs<W> tp, uint32_t log_n,
                 uint64_t ginv, uint64_t poly_words, uint64_t total) {
-  const uint64_t gid = xcd_gid();
-  if (gid >= total) return;
+  const uint64_t i = xcd_gid();
+  if (i >= poly_words) return;
   const uint64_t N = 1ull << log_n;
-  const uint32_t l = (uint32_t)(gid / poly_words);
-  const uint64_t jo = gid & (N - 1);
+  const uint32_t l = blockIdx.y;
+  const uint64_t gid = (uint64_t)l * poly_words + i;
+  const uint64_t jo = i & (N - 1);
   const uint64_t pbase = gid - jo;
   const uint64_t t = (jo * ginv) & (2 * N - 1);
   const W q = tp.lc[l].q;
@@ -1293,11 +1295,12 @@ template <class W>
 __global__ void __launch_bounds__(256)
 k_automorph_even(W* __restrict__ out, const W* __restrict__ in, TabPtrs<W> tp, uint32_t log_n,
                  uint32_t e, uint64_t hinv, uint64_t poly_words, uint64_t total) {
-  const uint64_t gid = xcd_gid();
-  if (gid >= total) return;
+  const uint64_t i = xcd_gid();
+  if (i >= poly_words) return;
   const uint64_t N = 1ull << log_n;
-  const uint32_t l = (uint32_t)(gid / poly_words);
-  const uint64_t jo = gid & (N - 1);
+  const uint32_t l = blockIdx.y;
+  const uint64_t gid = (uint64_t)l * poly_words + i;
+  const uint64_t jo = i & (N - 1);
   const uint64_t pbase = gid - jo;
   const uint64_t M = (2 * N) >> e;
   const W q = tp.lc[l].q;
@@ -1637,10 +1640,11 @@ static hipError_t automorphism_t(const Launch& k, void* out, const void* in, uin
   const uint64_t pw = (uint64_t)k.B * N;
   const uint64_t total = pw * k.L;
   if (total == 0) return hipSuccess;
-  const unsigned grid8 = (grid_for(total, 256) + 7u) & ~7u;  // xcd_gid() needs a multiple of 8
+  if (k.L > 65535) return hipErrorInvalidConfiguration;
+  const dim3 grid8((grid_for(pw, 256) + 7u) & ~7u, (unsigned)k.L);  // xcd_gid(): x a multiple of 8
   if (e & 1) {
     const uint64_t ginv = inv_mod_pow2(e, two_n);
-    hipLaunchKernelGGL((k_automorph_odd<W>), dim3(grid8), dim3(256), 0, k.s,
+    hipLaunchKernelGGL((k_automorph_odd<W>), grid8, dim3(256), 0, k.s,
                        (W*)out, (const W*)in, tab_ptrs<W>(k.t), k.t->log_n, ginv, pw, total);
   } else {
     uint32_t ex = 0;
@@ -1651,7 +1655,7 @@ static hipError_t automorphism_t(const Launch& k, void* out, const void* in, uin
     }
     const uint64_t M = two_n >> ex;
     const uint64_t hinv = inv_mod_pow2(h, M);
-    hipLaunchKernelGGL((k_automorph_even<W>), dim3(grid8), dim3(256), 0, k.s,
+    hipLaunchKernelGGL((k_automorph_even<W>), grid8, dim3(256), 0, k.s,
                        (W*)out, (const W*)in, tab_ptrs<W>(k.t), k.t->log_n, ex, hinv, pw, total);
   }
   return hipGetLastError();
