@@ -994,6 +994,25 @@ __device__ __forceinline__ void ks_lds_read16(W (&o)[16 / sizeof(W)], const W* p
   }
 }
 
+// Lazy multiply-accumulate of the u32 key-switch sum (q < 2^31): the
+// accumulator lives in [0, 2q) and a term is the Montgomery product without
+// its final subtraction, t = (x k + m q) / 2^32 in [0, 2q).  acc + t < 4q
+// needs 33 bits: the add's carry and the borrow of subtracting 2q decide the
+// select (acc + t >= 2q iff carry or no borrow), so a term costs the three
+// half-rate products plus add, subtract and select, where mont_mul + add_mod
+// took two more full-rate ops.  The sum is made canonical once, after the
+// source-limb loop.
+__device__ __forceinline__ uint32_t mac_lazy(uint32_t acc, uint32_t x, uint32_t k, uint32_t q,
+                                             uint32_t q2, uint32_t nqinv) {
+  const uint64_t T = mul64(x, k);
+  const uint32_t m = (uint32_t)T * nqinv;  // -T q^-1 mod 2^32
+  const uint32_t t = (uint32_t)(mad64(m, q, T) >> 32);
+  uint32_t s, d;
+  const bool carry = __builtin_add_overflow(acc, t, &s);
+  const bool borrow = __builtin_sub_overflow(s, q2, &d);
+  return (carry || !borrow) ? d : s;
+}
+
 // Key-switch rows.  A workgroup owns row r of target limb j for RPW
 // consecutive polys p (grid: (j, r) major, poly group minor, dealt so the
 // workgroups of one (j, r) share an XCD).  For every source limb i: forward
@@ -1045,6 +1064,11 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   const Tw<W>* itw = tp.itw + (uint64_t)j * N;
   const uint32_t b0 = G::base(rp.xp.tau, G::BB0);
   const uint32_t bl = G::base(rp.xp.tau, G::BBL);
+  // u32: the lazy [0, 2q) accumulation (mac_lazy); u64: mont_mul + add_mod
+  constexpr bool kLazy = sizeof(W) == 4;
+  W nqinv = (W)0 - lc.qinv;
+  asm volatile("" : "+s"(nqinv));  // keeps T * (-q^-1) one multiply (not -(T q^-1))
+  const W q2 = lc.q + lc.q;
   W acc[2][E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
@@ -1097,9 +1121,13 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
           for (int v = 0; v < V; ++v) kv[v] = e0 + v < E ? kk[e0 + v] : (W)0;
         }
 #pragma unroll
-        for (int v = 0; v < V; ++v)
-          if (e0 + v < E)
+        for (int v = 0; v < V; ++v) {
+          if (e0 + v >= E) continue;
+          if constexpr (kLazy)
+            acc[o][e0 + v] = mac_lazy(acc[o][e0 + v], x[0][e0 + v], kv[v], lc.q, q2, nqinv);
+          else
             acc[o][e0 + v] = add_mod<W>(acc[o][e0 + v], mont_mul<W>(x[0][e0 + v], kv[v], lc.q, lc.qinv), lc.q);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -1117,7 +1145,7 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   for (int o = 0; o < 2; ++o) {
     W v[1][E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) v[0][e] = acc[o][e];
+    for (int e = 0; e < E; ++e) v[0][e] = kLazy ? csub<W>(acc[o][e], lc.q) : acc[o][e];
     xf_inv<G, W, 1>(v, xq, lds, itw, mod_of(lc));
     W* uo = o == 0 ? u0 : u1;
     if (rp.active) {
@@ -1164,13 +1192,25 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
   }
   xf_fwd<G, W, 2>(b, rp.xp, lds, tw, mod_of(lc));
   W d2[1][E];
+  W nqi = (W)0 - lc.qinv;
+  asm volatile("" : "+v"(nqi));  // one multiply per REDC (see mont_mul_nq)
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const W q = lc.q, qi = lc.qinv;
-    const W d0 = mont_mul<W>(a[0][i], b[0][i], q, qi);
-    const W d1 = add_mod<W>(mont_mul<W>(a[0][i], b[1][i], q, qi),
-                            mont_mul<W>(a[1][i], b[0][i], q, qi), q);
-    d2[0][i] = mont_mul<W>(a[1][i], b[1][i], q, qi);
+    W d0, d1;
+    if constexpr (sizeof(W) == 4) {
+      d0 = mont_mul_nq(a[0][i], b[0][i], q, nqi);
+      // one REDC of the two-product sum: T < 2q^2 and T + m q < 2^64, the
+      // result (T + m q) / 2^32 < 2q (q < 2^31)
+      const uint64_t T = mad64(a[1][i], b[0][i], mul64(a[0][i], b[1][i]));
+      const uint32_t m = (uint32_t)T * nqi;
+      d1 = csub<uint32_t>((uint32_t)(mad64(m, q, T) >> 32), q);
+      d2[0][i] = mont_mul_nq(a[1][i], b[1][i], q, nqi);
+    } else {
+      d0 = mont_mul<W>(a[0][i], b[0][i], q, qi);
+      d1 = add_mod<W>(mont_mul<W>(a[0][i], b[1][i], q, qi), mont_mul<W>(a[1][i], b[0][i], q, qi), q);
+      d2[0][i] = mont_mul<W>(a[1][i], b[1][i], q, qi);
+    }
     if (rp.active) {
       const uint32_t pos = bl + ((uint32_t)i << G::BBL);
       d0hat[base + pos] = d0;

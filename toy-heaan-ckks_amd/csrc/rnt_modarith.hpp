@@ -146,6 +146,16 @@ __host__ __device__ __forceinline__ uint32_t mont_mul<uint32_t>(uint32_t a, uint
 #endif
 }
 
+// The same product with nqinv = -q^-1 mod 2^32 supplied by the caller.
+// hipcc rewrites t * (0 - qinv) as 0 - t * qinv, a v_sub per product; a
+// caller that hoists nqinv out of its loop behind an opaque copy keeps the
+// single multiply.
+__device__ __forceinline__ uint32_t mont_mul_nq(uint32_t a, uint32_t b, uint32_t q, uint32_t nqinv) {
+  const uint64_t t = mul64(a, b);
+  const uint32_t m = (uint32_t)t * nqinv;
+  return csub<uint32_t>((uint32_t)(mad64(m, q, t) >> 32), q);
+}
+
 template <>
 __host__ __device__ __forceinline__ uint64_t mont_mul<uint64_t>(uint64_t a, uint64_t b, uint64_t q,
                                                                  uint64_t qinv) {
