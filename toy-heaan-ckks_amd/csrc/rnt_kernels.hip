@@ -552,6 +552,11 @@ __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0,
 // VGPR budget at 512 / kRowMinWaves) and for the key-switch rows.
 constexpr int kRowMinWaves = 6;
 constexpr int kKsMinWaves = 4;
+// Key rows of the key-switch rows kernel go global -> LDS directly
+// (global_load_lds, no registers) for u32 rows of >= 64 words, except in the
+// WIDE (small-batch) grid below 2^9-word rows, where staging them through
+// registers measured faster (profiles/r02_ab_ks_small_batch.txt).
+constexpr int kKsGldsWideMinLogC = 9;
 
 // Move NOPS register sets from distribution BF to BT through LDS.  Several
 // operands go one after the other through a single LDS region, so occupancy
@@ -1023,7 +1028,7 @@ __device__ __forceinline__ uint32_t mac_lazy(uint32_t acc, uint32_t x, uint32_t 
 // slot, and the accumulate reads them back from LDS: one global round trip
 // per source limb instead of three (S, then key_b, then key_a), and 2 key
 // words per thread instead of 2E (A/B: profiles/r02_ab_ks_rows.txt).
-template <class W, int LOG_C>
+template <class W, int LOG_C, bool WIDE>
 __global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kKsMinWaves : 1)
 k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
           const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
@@ -1033,11 +1038,16 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   using G = RowGeo<LOG_C>;
   constexpr int E = G::E;
   constexpr int C = G::C;
-  constexpr int KPAD = C + (C >> 4);                            // padded key row (ks_pad)
-  constexpr int KPT = (2 * C + G::THREADS - 1) / G::THREADS;  // key words per thread per i
+  constexpr int KPAD = C + (C >> 4);  // padded key row (ks_pad)
+  // key rows staged per source limb: {key_b, key_a} of the workgroup's one
+  // row r (RPW polys), or of its RPW rows (WIDE: one poly)
+  constexpr int KROWS = WIDE ? G::RPW : 1;
+  constexpr int KPT = (2 * KROWS * C + G::THREADS - 1) / G::THREADS;  // key words per thread per i
+  constexpr bool kKeyGlds = sizeof(W) == 4 && C >= 64 && (!WIDE || LOG_C >= kKsGldsWideMinLogC);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
-  W* kbuf = lds + G::REGION;  // [2 buffers][key_b row | key_a row]
+  // [2 buffers][key_b row | key_a row], or WIDE: [key_b rows | key_a rows]
+  W* kbuf = lds + G::REGION;
   // XCD-aware deal: hardware block b runs on XCD b % 8; consecutive logical
   // blocks (one (j, r), successive poly groups) get the same b % 8
   const uint32_t per_xcd = (nblocks + 7) / 8;
@@ -1049,11 +1059,23 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   RowPos rp;
   rp.xp.slot = G::slot_of(threadIdx.x);
   rp.xp.tau = G::tau_of(threadIdx.x);
-  rp.r = jr & ((1u << log_r) - 1u);
-  rp.l = jr >> log_r;
-  const uint32_t p = pg * G::RPW + rp.xp.slot;
-  rp.active = p < B;
-  rp.p = rp.active ? p : B - 1;  // inactive slots read a valid row, store nothing
+  uint32_t rbase;  // first row of the workgroup's key rows
+  if constexpr (WIDE) {
+    // small batches: one poly (pg), rows r0 .. r0 + RPW - 1 (jr = (j, row group))
+    const uint32_t lg = log_r - (uint32_t)__builtin_ctz(G::RPW);
+    rbase = (jr & ((1u << lg) - 1u)) * G::RPW;
+    rp.r = rbase + rp.xp.slot;
+    rp.l = jr >> lg;
+    rp.active = true;
+    rp.p = pg;
+  } else {
+    rp.r = jr & ((1u << log_r) - 1u);
+    rbase = rp.r;
+    rp.l = jr >> log_r;
+    const uint32_t p = pg * G::RPW + rp.xp.slot;
+    rp.active = p < B;
+    rp.p = rp.active ? p : B - 1;  // inactive slots read a valid row, store nothing
+  }
   rp.xp.heap = (1u << log_n) + rp.r * (uint32_t)G::C;
   const uint64_t N = 1ull << log_n;
   const uint32_t j = rp.l;
@@ -1078,24 +1100,53 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   }
 #pragma unroll 1
   for (uint32_t i = 0; i < L; ++i) {
-    // this limb's key rows (key poly i, limb j, row r; limb stride key_ls)
-    // and S rows: one batch of loads, one wait
+    // this limb's key rows (key poly i, limb j, rows rbase ..; limb stride
+    // key_ls) and S rows: one batch of loads, one wait
     const uint64_t sbase = (((uint64_t)j * L + i) * B + rp.p) * N + rowoff;
-    const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + rowoff;
-    W kr[KPT];
-#pragma unroll
-    for (int m = 0; m < KPT; ++m) {
-      const uint32_t w = threadIdx.x + (uint32_t)m * G::THREADS;
-      if (w < 2u * C) kr[m] = w < (uint32_t)C ? key_b[kbase + w] : key_a[kbase + w - C];
-    }
+    const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + (WIDE ? (uint64_t)rbase * G::C : rowoff);
+    constexpr uint32_t KW = (uint32_t)(KROWS * C);  // words per key
     W x[1][E];
+    // WIDE keeps one key buffer: every thread's reads of the previous limb's
+    // keys finish before it is rewritten
+    if constexpr (WIDE) __syncthreads();
+    W* kb = WIDE ? kbuf : kbuf + (i & 1u) * 2 * KPAD;
+    if constexpr (kKeyGlds) {
+      // u32 rows of >= 64 words: the key rows go global -> LDS directly, one
+      // 64-word segment (one ks_pad run) per wave instruction, no registers
+      constexpr uint32_t SEG = KW / 64;  // segments per key
+      constexpr int WAVES = G::THREADS / 64;
+      const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
-    for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
-    W* kb = kbuf + (i & 1u) * 2 * KPAD;
+      for (int m = 0; m < (int)((2 * SEG + WAVES - 1) / WAVES); ++m) {
+        const uint32_t sg = wave + (uint32_t)m * WAVES;
+        if (sg < 2 * SEG) {
+          const uint32_t kk = sg >= SEG, rs = kk ? sg - SEG : sg;  // key, segment within it
+          const W* src = (kk ? key_a : key_b) + kbase + rs * 64u + lane;
+          W* dst = kb + kk * (KROWS * KPAD) + (rs / (C / 64)) * KPAD + ks_pad((rs % (C / 64)) * 64u);
+          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
+        }
+      }
 #pragma unroll
-    for (int m = 0; m < KPT; ++m) {
-      const uint32_t w = threadIdx.x + (uint32_t)m * G::THREADS;
-      if (w < 2u * C) kb[(w < (uint32_t)C ? 0 : KPAD) + ks_pad(w & (C - 1))] = kr[m];
+      for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
+    } else {
+      W kr[KPT];
+#pragma unroll
+      for (int m = 0; m < KPT; ++m) {
+        const uint32_t w = threadIdx.x + (uint32_t)m * G::THREADS;
+        if (w < 2u * KW) kr[m] = w < KW ? key_b[kbase + w] : key_a[kbase + w - KW];
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
+#pragma unroll
+      for (int m = 0; m < KPT; ++m) {
+        const uint32_t w = threadIdx.x + (uint32_t)m * G::THREADS;
+        if (w < 2u * KW) {
+          const uint32_t wk = w < KW ? w : w - KW;  // word within its key's rows
+          kb[(w < KW ? 0u : KROWS * KPAD) + (wk / C) * KPAD + ks_pad(wk & (C - 1))] = kr[m];
+        }
+      }
     }
     // the transform's LDS exchange ends in barriers that publish kb (and
     // order the reads of this slot two limbs ago before this write); a
@@ -1109,7 +1160,7 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     static_assert(G::BBL == 0, "last row pass distribution");
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
-      const W* kk = kb + o * KPAD + ks_pad(bl);
+      const W* kk = kb + o * KROWS * KPAD + (WIDE ? rp.xp.slot * KPAD : 0u) + ks_pad(bl);
       constexpr int V = 16 / sizeof(W);
 #pragma unroll
       for (int e0 = 0; e0 < E; e0 += V) {
@@ -1785,28 +1836,45 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
   return hipGetLastError();
 }
 
-template <class W, int LOG_C>
+template <class W, int LOG_C, bool WIDE>
 static hipError_t ks_rows_launch(const Launch& k, void* u0, void* u1, uint64_t ls, const void* S,
                                  const void* key_a, const void* key_b, uint64_t key_ls,
                                  const void* init0, const void* init1, uint64_t init_ls) {
   using G = RowGeo<LOG_C>;
   const Geom g = geom_for(k.t->log_n);
   if (k.L == 0 || k.B == 0) return hipSuccess;
-  // one workgroup per (target limb, row, group of RPW polys)
-  const uint64_t pgroups = (k.B + G::RPW - 1) / G::RPW;
-  const uint64_t blocks = (uint64_t)k.L * g.r * pgroups;
+  // one workgroup per (target limb, row, group of RPW polys), or WIDE: per
+  // (target limb, group of RPW rows, poly), the poly index fastest
+  const uint64_t pgroups = WIDE ? k.B : (k.B + G::RPW - 1) / G::RPW;
+  const uint64_t blocks = (uint64_t)k.L * (WIDE ? g.r / G::RPW : g.r) * pgroups;
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
   const unsigned launched = (unsigned)((blocks + 7) / 8 * 8);  // whole XCD rounds
-  // exchange region + two padded {key_b, key_a} row buffers
-  const size_t lds = row_lds<W, LOG_C>(1) + 2 * 2 * (G::C + (G::C >> 4)) * sizeof(W);
-  hipError_t e = allow_lds(k_ks_rows<W, LOG_C>, lds);
+  // exchange region + the key rows: two buffers of {key_b, key_a} rows, or
+  // WIDE one buffer of RPW rows of each
+  const size_t krows = WIDE ? 2 * G::RPW : 4;
+  const size_t lds = row_lds<W, LOG_C>(1) + krows * (G::C + (G::C >> 4)) * sizeof(W);
+  hipError_t e = allow_lds(k_ks_rows<W, LOG_C, WIDE>, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_ks_rows<W, LOG_C>), dim3(launched), dim3(G::THREADS), lds, k.s, (W*)u0,
-                     (W*)u1, (const W*)S, (const W*)key_a, (const W*)key_b, key_ls,
+  hipLaunchKernelGGL((k_ks_rows<W, LOG_C, WIDE>), dim3(launched), dim3(G::THREADS), lds, k.s,
+                     (W*)u0, (W*)u1, (const W*)S, (const W*)key_a, (const W*)key_b, key_ls,
                      (const W*)init0, (const W*)init1, init_ls, tab_ptrs<W>(k.t), g.log_n,
                      (uint32_t)k.src_limbs(), (uint32_t)k.B, ls, (uint32_t)pgroups,
                      (uint32_t)blocks);
   return hipGetLastError();
+}
+
+// Batches under half a workgroup's rows (B < RPW / 2; u32 rows of >= 64
+// words, whose key rows are staged without registers) take the WIDE grid:
+// the poly-per-slot grid would leave RPW - B of its RPW row slots idle.
+template <class W, int LOG_C>
+static hipError_t ks_rows_pick(const Launch& k, void* u0, void* u1, uint64_t ls, const void* S,
+                               const void* key_a, const void* key_b, uint64_t key_ls,
+                               const void* init0, const void* init1, uint64_t init_ls) {
+  using G = RowGeo<LOG_C>;
+  const Geom g = geom_for(k.t->log_n);
+  if (sizeof(W) == 4 && G::C >= 64 && 2 * k.B < (size_t)G::RPW && g.r % G::RPW == 0)
+    return ks_rows_launch<W, LOG_C, true>(k, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls);
+  return ks_rows_launch<W, LOG_C, false>(k, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls);
 }
 
 template <class W>
@@ -1815,7 +1883,7 @@ static hipError_t ks_rows_t(const Launch& k, void* u0, void* u1, uint64_t ls, co
                             const void* init0, const void* init1, uint64_t init_ls) {
   const Geom g = geom_for(k.t->log_n);
 #define RNT_L(C) \
-  return ks_rows_launch<W, C>(k, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls)
+  return ks_rows_pick<W, C>(k, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls)
   RNT_DISPATCH_LOGC(g.log_c, RNT_L)
 #undef RNT_L
   return hipErrorInvalidValue;
