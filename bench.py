@@ -654,12 +654,14 @@ def run_rotate(args, comm, world, rank, local_rank):
         ka, kb = check_key
         rn.check(lib.rnt_ct_rotate(out0.handle, out1.handle, c0.handle, c1.handle, offsets[ki],
                                    key.a.handle, key.b.handle))
-        g0, g1 = out0.channels(), out1.channels()
         parity_ok = True
         t = time.perf_counter()
         for pi in sorted({0, B - 1}):
+            # channels_of: [1][L][N] whatever the batch (channels() drops the
+            # batch axis of a one-poly buffer)
+            g0, g1 = out0.channels_of(pi)[0], out1.channels_of(pi)[0]
             w0, w1 = orc.rotate_ciphertext(ob, c0_h[pi], c1_h[pi], offsets[ki], ka, kb, threads=threads)
-            parity_ok &= bool(np.array_equal(g0[pi], w0) and np.array_equal(g1[pi], w1))
+            parity_ok &= bool(np.array_equal(g0, w0) and np.array_equal(g1, w1))
         sn = (time.perf_counter() - t) / len({0, B - 1})
         if world == 1 and not args.no_cpu_baseline:
             cpu = {"value": 1.0 / sn, "unit": "rotations/s", "cores": threads, "kind": "port",
