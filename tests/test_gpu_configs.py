@@ -153,3 +153,28 @@ def test_decomposition_groups(gpu, monkeypatch, jg):
     for p in (0, B - 1):
         w0, w1 = orc.keyswitch(Bo, c1[p], ka, kb, threads=T)
         assert np.array_equal(g0[p], w0[:Lt]) and np.array_equal(g1[p], w1[:Lt]), p
+
+
+@pytest.mark.parametrize("log_n,B", [(12, 1), (12, 3), (12, 40), (14, 2), (14, 9), (14, 33), (16, 1), (16, 5),
+                                     (16, 8), (16, 17), (17, 1), (17, 3), (17, 4)])
+def test_keyswitch_row_grids(gpu, log_n, B):
+    """rnt_keyswitch's rows kernel picks its grid by batch: one poly x RPW
+    rows per workgroup when 2B < RPW (RPW = 16 rows at N <= 2^16, 8 at
+    2^17), RPW polys x one row otherwise; key rows are staged through
+    registers or by direct global->LDS loads by row length and grid
+    (rnt_kernels.hip ks_rows_pick / kKeyGlds).  Every combination, first
+    and last poly of the batch, against the oracle's gadget sum
+    (engine.rs:505-528)."""
+    rn = gpu
+    n, L = 1 << log_n, 4
+    mod = rn.generate_primes(31, L, n)
+    Bd, Bo = rn.RnsBasis(mod, n), orc.Basis(mod, n)
+    rng = np.random.default_rng(900 + 31 * log_n + B)
+    d = _rand(rng, mod, n, B)  # [B][L][N]
+    ka, kb = _rand(rng, mod, n, L), _rand(rng, mod, n, L)
+    key = rn.RnsGadgetKey.from_channels(ka, kb, Bd)
+    a0, a1 = rn.keyswitch(rn.RnsPoly.from_channels(d, Bd), key)
+    for p in sorted({0, B - 1}):
+        w0, w1 = orc.keyswitch(Bo, d[p], ka, kb, threads=T)
+        assert np.array_equal(a0.channels_of(p)[0], w0), (log_n, B, p)
+        assert np.array_equal(a1.channels_of(p)[0], w1), (log_n, B, p)
