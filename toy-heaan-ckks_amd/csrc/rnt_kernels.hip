@@ -1028,7 +1028,7 @@ __device__ __forceinline__ uint32_t mac_lazy(uint32_t acc, uint32_t x, uint32_t 
 // slot, and the accumulate reads them back from LDS: one global round trip
 // per source limb instead of three (S, then key_b, then key_a), and 2 key
 // words per thread instead of 2E (A/B: profiles/r02_ab_ks_rows.txt).
-template <class W, int LOG_C, bool WIDE>
+template <class W, int LOG_C, int NP>
 __global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kKsMinWaves : 1)
 k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
           const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
@@ -1039,14 +1039,22 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   constexpr int E = G::E;
   constexpr int C = G::C;
   constexpr int KPAD = C + (C >> 4);  // padded key row (ks_pad)
-  // key rows staged per source limb: {key_b, key_a} of the workgroup's one
-  // row r (RPW polys), or of its RPW rows (WIDE: one poly)
-  constexpr int KROWS = WIDE ? G::RPW : 1;
+  // NP polys x KROWS consecutive rows per workgroup (NP = RPW: one row r
+  // for RPW polys; NP = 1: one poly, RPW rows); the key rows of a source
+  // limb are staged per workgroup, KROWS of each key
+  static_assert(NP >= 1 && G::RPW % NP == 0, "polys per workgroup");
+  constexpr int KROWS = G::RPW / NP;
+  constexpr bool WIDE = NP < G::RPW;
   constexpr int KPT = (2 * KROWS * C + G::THREADS - 1) / G::THREADS;  // key words per thread per i
-  constexpr bool kKeyGlds = sizeof(W) == 4 && C >= 64 && (!WIDE || LOG_C >= kKsGldsWideMinLogC);
+  constexpr bool kKeyGlds = sizeof(W) == 4 && C >= 64 && (NP > 1 || LOG_C >= kKsGldsWideMinLogC);
+  // two key buffers (the next limb's keys are written while the last ones
+  // may still be read) when they fit beside the exchange region in a
+  // quarter of the LDS; else one buffer and a barrier per limb
+  constexpr bool KDOUBLE =
+      (size_t)(G::REGION + 4 * KROWS * KPAD) * sizeof(W) <= 40u * 1024u || KROWS == 1;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
-  // [2 buffers][key_b row | key_a row], or WIDE: [key_b rows | key_a rows]
+  // [buffers][key_b rows | key_a rows]
   W* kbuf = lds + G::REGION;
   // XCD-aware deal: hardware block b runs on XCD b % 8; consecutive logical
   // blocks (one (j, r), successive poly groups) get the same b % 8
@@ -1061,13 +1069,14 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   rp.xp.tau = G::tau_of(threadIdx.x);
   uint32_t rbase;  // first row of the workgroup's key rows
   if constexpr (WIDE) {
-    // small batches: one poly (pg), rows r0 .. r0 + RPW - 1 (jr = (j, row group))
-    const uint32_t lg = log_r - (uint32_t)__builtin_ctz(G::RPW);
-    rbase = (jr & ((1u << lg) - 1u)) * G::RPW;
-    rp.r = rbase + rp.xp.slot;
+    // jr = (j, row group of KROWS rows); slot = row-in-group * NP + poly-in-group
+    const uint32_t lg = log_r - (uint32_t)__builtin_ctz(KROWS);
+    rbase = (jr & ((1u << lg) - 1u)) * KROWS;
+    rp.r = rbase + rp.xp.slot / NP;
     rp.l = jr >> lg;
-    rp.active = true;
-    rp.p = pg;
+    const uint32_t p = pg * NP + rp.xp.slot % NP;
+    rp.active = p < B;
+    rp.p = rp.active ? p : B - 1;
   } else {
     rp.r = jr & ((1u << log_r) - 1u);
     rbase = rp.r;
@@ -1106,10 +1115,10 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + (WIDE ? (uint64_t)rbase * G::C : rowoff);
     constexpr uint32_t KW = (uint32_t)(KROWS * C);  // words per key
     W x[1][E];
-    // WIDE keeps one key buffer: every thread's reads of the previous limb's
-    // keys finish before it is rewritten
-    if constexpr (WIDE) __syncthreads();
-    W* kb = WIDE ? kbuf : kbuf + (i & 1u) * 2 * KPAD;
+    // one key buffer: every thread's reads of the previous limb's keys
+    // finish before it is rewritten
+    if constexpr (!KDOUBLE) __syncthreads();
+    W* kb = KDOUBLE ? kbuf + (i & 1u) * 2 * KROWS * KPAD : kbuf;
     if constexpr (kKeyGlds) {
       // u32 rows of >= 64 words: the key rows go global -> LDS directly, one
       // 64-word segment (one ks_pad run) per wave instruction, no registers
@@ -1160,7 +1169,7 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     static_assert(G::BBL == 0, "last row pass distribution");
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
-      const W* kk = kb + o * KROWS * KPAD + (WIDE ? rp.xp.slot * KPAD : 0u) + ks_pad(bl);
+      const W* kk = kb + o * KROWS * KPAD + (WIDE ? (rp.xp.slot / NP) * KPAD : 0u) + ks_pad(bl);
       constexpr int V = 16 / sizeof(W);
 #pragma unroll
       for (int e0 = 0; e0 < E; e0 += V) {
@@ -1836,26 +1845,29 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
   return hipGetLastError();
 }
 
-template <class W, int LOG_C, bool WIDE>
+template <class W, int LOG_C, int NP>
 static hipError_t ks_rows_launch(const Launch& k, void* u0, void* u1, uint64_t ls, const void* S,
                                  const void* key_a, const void* key_b, uint64_t key_ls,
                                  const void* init0, const void* init1, uint64_t init_ls) {
   using G = RowGeo<LOG_C>;
+  constexpr int KROWS = G::RPW / NP;
+  constexpr size_t KPADB = (G::C + (G::C >> 4)) * sizeof(W);
   const Geom g = geom_for(k.t->log_n);
   if (k.L == 0 || k.B == 0) return hipSuccess;
-  // one workgroup per (target limb, row, group of RPW polys), or WIDE: per
-  // (target limb, group of RPW rows, poly), the poly index fastest
-  const uint64_t pgroups = WIDE ? k.B : (k.B + G::RPW - 1) / G::RPW;
-  const uint64_t blocks = (uint64_t)k.L * (WIDE ? g.r / G::RPW : g.r) * pgroups;
+  if (g.r % KROWS) return hipErrorInvalidValue;
+  // one workgroup per (target limb, group of KROWS rows, group of NP polys)
+  const uint64_t pgroups = (k.B + NP - 1) / NP;
+  const uint64_t blocks = (uint64_t)k.L * (g.r / KROWS) * pgroups;
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
   const unsigned launched = (unsigned)((blocks + 7) / 8 * 8);  // whole XCD rounds
-  // exchange region + the key rows: two buffers of {key_b, key_a} rows, or
-  // WIDE one buffer of RPW rows of each
-  const size_t krows = WIDE ? 2 * G::RPW : 4;
-  const size_t lds = row_lds<W, LOG_C>(1) + krows * (G::C + (G::C >> 4)) * sizeof(W);
-  hipError_t e = allow_lds(k_ks_rows<W, LOG_C, WIDE>, lds);
+  // exchange region + one or two buffers of {key_b, key_a} x KROWS rows
+  // (the kernel's KDOUBLE rule)
+  const size_t region = row_lds<W, LOG_C>(1);
+  const bool kdouble = region + 4 * KROWS * KPADB <= 40u * 1024u || KROWS == 1;
+  const size_t lds = region + (kdouble ? 4 : 2) * KROWS * KPADB;
+  hipError_t e = allow_lds(k_ks_rows<W, LOG_C, NP>, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_ks_rows<W, LOG_C, WIDE>), dim3(launched), dim3(G::THREADS), lds, k.s,
+  hipLaunchKernelGGL((k_ks_rows<W, LOG_C, NP>), dim3(launched), dim3(G::THREADS), lds, k.s,
                      (W*)u0, (W*)u1, (const W*)S, (const W*)key_a, (const W*)key_b, key_ls,
                      (const W*)init0, (const W*)init1, init_ls, tab_ptrs<W>(k.t), g.log_n,
                      (uint32_t)k.src_limbs(), (uint32_t)k.B, ls, (uint32_t)pgroups,
@@ -1863,18 +1875,42 @@ static hipError_t ks_rows_launch(const Launch& k, void* u0, void* u1, uint64_t l
   return hipGetLastError();
 }
 
-// Batches under half a workgroup's rows (B < RPW / 2; u32 rows of >= 64
-// words, whose key rows are staged without registers) take the WIDE grid:
-// the poly-per-slot grid would leave RPW - B of its RPW row slots idle.
+// Polys per workgroup: the poly-per-slot grid (NP = RPW) shares each key
+// row among RPW polys but leaves slots idle when RPW does not divide B.
+// u32 rows of >= 64 words pick, among NP = RPW and smaller powers of two
+// (2..8 for the configs' 2^8- and 2^9-word rows, 1 for every row length),
+// the one that fills the most row slots, the larger on a tie (more key
+// sharing).  B < RPW/2 used to run at B/RPW of the grid.
 template <class W, int LOG_C>
 static hipError_t ks_rows_pick(const Launch& k, void* u0, void* u1, uint64_t ls, const void* S,
                                const void* key_a, const void* key_b, uint64_t key_ls,
                                const void* init0, const void* init1, uint64_t init_ls) {
   using G = RowGeo<LOG_C>;
+  constexpr int RPW = G::RPW;
   const Geom g = geom_for(k.t->log_n);
-  if (sizeof(W) == 4 && G::C >= 64 && 2 * k.B < (size_t)G::RPW && g.r % G::RPW == 0)
-    return ks_rows_launch<W, LOG_C, true>(k, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls);
-  return ks_rows_launch<W, LOG_C, false>(k, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls);
+  int np = RPW;
+  if (sizeof(W) == 4 && G::C >= 64 && RPW > 1) {
+    double best = -1.0;
+    for (int c = RPW; c >= 1; c >>= 1) {
+      const bool have = c == RPW || c == 1 || ((LOG_C == 8 || LOG_C == 9) && c <= 8);
+      if (!have || g.r % (RPW / c)) continue;
+      const double fill = (double)k.B / (double)(((k.B + c - 1) / c) * c);
+      if (fill > best + 1e-9) { best = fill; np = c; }
+    }
+  }
+#define RNT_NP(V) \
+  if (np == (V) && RPW % (V) == 0) \
+    return ks_rows_launch<W, LOG_C, (RPW % (V) == 0 ? (V) : RPW)>(k, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls);
+  if constexpr (sizeof(W) == 4 && G::C >= 64 && RPW > 1) {
+    RNT_NP(1)
+    if constexpr (LOG_C == 8 || LOG_C == 9) {
+      RNT_NP(2)
+      RNT_NP(4)
+      RNT_NP(8)
+    }
+  }
+#undef RNT_NP
+  return ks_rows_launch<W, LOG_C, RPW>(k, u0, u1, ls, S, key_a, key_b, key_ls, init0, init1, init_ls);
 }
 
 template <class W>
