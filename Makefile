@@ -33,7 +33,12 @@ $(LIBDIR)/librnsntt.so: $(LIBDIR)/rnt_kernels.o $(LIBDIR)/rnt_encode.o $(LIBDIR)
 oracle/liboracle.so: oracle/oracle.c oracle/oracle.h
 	gcc $(CFLAGS) -shared oracle/oracle.c -o $@
 
+# ASan + UBSan variants of the oracle and of librnsntt's host code, and the
+# CPU tests run under them; log in profiles/r03_sanitizer_cpu.log
+asan:
+	tools/sanitize.sh
+
 clean:
 	rm -f $(LIBDIR)/*.o $(LIBDIR)/*.so oracle/liboracle.so
 
-.PHONY: all clean
+.PHONY: all clean asan

@@ -129,8 +129,18 @@ def host_info():
 
 
 def usable_threads() -> int:
-    """All the CPUs this job may use, capped at the GPU box's share of 16."""
-    return max(1, min(16, host_info()["affinity"] or 1))
+    """The CPU threads this job may use for the CPU baseline: the job's CPU
+    share as the GPU box sets it (OMP_NUM_THREADS, 16 per GPU on the
+    MI355X boxes, whose rules cap a job's worker pools at that share), else
+    every CPU in this process' affinity mask.  The host itself is reported
+    beside it (host_info: 2 x 64-core EPYC 9575F, 256 CPUs shared by the
+    host's 8 GPUs' jobs)."""
+    aff = host_info()["affinity"] or 1
+    try:
+        share = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        share = 0
+    return max(1, min(aff, share) if share > 0 else aff)
 
 
 def cpu_baseline(mod, n, budget_s):
@@ -157,6 +167,7 @@ def cpu_baseline(mod, n, budget_s):
     threads = usable_threads()
     d1, e1 = timed(1, budget_s / 2)
     dn, en = timed(threads, budget_s / 2)
+    host = host_info()
     return {
         "value": dn / en,
         "unit": "poly-muls/s",
@@ -164,9 +175,13 @@ def cpu_baseline(mod, n, budget_s):
         "kind": "port",
         "sample": f"{dn} coefficient-domain poly-muls (N={n}, L={len(mod)}), {threads} per pass over "
                   f"{threads} threads, {en:.1f} s wall; oracle/oracle.c restating poly.rs:307-329",
+        "cores_basis": (f"the job's CPU share (OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}, "
+                        f"affinity {host.get('affinity')} of {host.get('cpu_count')} CPUs)"
+                        if os.environ.get("OMP_NUM_THREADS") else
+                        f"every CPU of the affinity mask ({host.get('affinity')})"),
         "single_thread": {"value": d1 / e1, "cores": 1,
                           "sample": f"{d1} poly-muls on one thread, {e1:.1f} s wall"},
-        "host": host_info(),
+        "host": host,
     }
 
 
@@ -309,16 +324,20 @@ def run_polymul(args, comm, world, rank, local_rank):
                             local_rank)
     # the measured stream-copy bandwidth (report against it too):
     # a device-to-device copy of one operand batch, read + write
+    # (rnt_copy: a plain 16-byte-per-lane copy kernel, k_copy16, timed by its
+    # HIP events)
     copy_gbs = None
     if rank == 0:
         dst = rn.RnsPoly(B, batch)
         rn.check(lib.rnt_copy(dst.handle, a.handle))
         B.sync()
-        t = time.perf_counter()
+        B.profile_enable(True)
         for _ in range(5):
             rn.check(lib.rnt_copy(dst.handle, a.handle))
-        B.sync()
-        copy_gbs = 5 * 2 * Lr * batch * n * wb / (time.perf_counter() - t) / 1e9
+        cnt, cms = B.profile_read("copy")
+        B.profile_enable(False)
+        if cnt:
+            copy_gbs = cnt * 2 * Lr * batch * n * wb / (cms * 1e-3) / 1e9
         del dst
 
     ms_per_step = elapsed / args.steps * 1e3
@@ -335,32 +354,53 @@ def run_polymul(args, comm, world, rank, local_rank):
             want = orc.mul(ob, a.channels_of(pi)[0], b.channels_of(pi)[0])
             parity_ok &= bool(np.array_equal(got, want))
 
-    # roofline of the dominant kernel: its algorithmic bytes per launch (at
-    # the device word width) / its average launch time, measured with HIP
-    # events on the library stream
+    # roofline.  Headline (`frac`): the whole rnt_mul -- the metric's unit --
+    # as one launch of the path: its algorithmic bytes (read a, read b, write
+    # c at the device word width) over the summed average launch
+    # times of its kernels, each measured with HIP events on the library's
+    # stream (the same kernels rocprofv3 lists; their sum is within a few us
+    # of ms_per_step, so frac = whole-op bytes / ms_per_step / 8 TB/s).
+    # Per-kernel figures follow in `kernels_roofline`, each with the bound
+    # that really holds it (the row kernel is VALU-bound).
     elem = Lr * batch * n
+    launches = max(kernels[k]["launches"] for k in kernels)
+    op_ms = sum(kernels[k]["total_ms"] for k in kernels) / args.steps  # per rnt_mul
+    op_bytes = 3 * elem * wb
+    achieved = op_bytes / (op_ms * 1e-3) / 1e9
     step_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb}
-    dom = max(kernels, key=lambda k: kernels[k]["total_ms"])
-    alg_bytes = {k: step_bytes[k] * args.steps / max(kernels[k]["launches"], 1) for k in kernels}
-    achieved = alg_bytes[dom] / (kernels[dom]["avg_ms"] * 1e-3) / 1e9
     per_gpu = value / world
+    pmc = {k: traffic_for(k, "polymul", batch, args.log_n, Lr) if args.prime_bits == 31 else None
+           for k in kernels}
+    kroof = {}
+    for k, kv in kernels.items():
+        kb = step_bytes.get(k)
+        ent = {"avg_ms": kv["avg_ms"], "launches": kv["launches"], "alg_bytes_per_launch": kb,
+               "bound": "valu" if k == "row_mul" else "hbm", "pmc_bytes_per_launch": pmc.get(k)}
+        if kb:
+            ent["hbm_GBs"] = kb / (kv["avg_ms"] * 1e-3) / 1e9
+            ent["hbm_frac"] = ent["hbm_GBs"] / HBM_PEAK_GBS
+        kroof[k] = ent
+    traffic = sum(v for v in pmc.values() if v) if all(pmc.values()) else None
     roofline = {
         "bound": "hbm",
-        "kernel": dom,
+        "kernel": "rnt_mul (" + " + ".join(kernels) + ")",
         "achieved": achieved,
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
-        # the committed PMC passes were taken on the default 31-bit workload
-        "traffic": traffic_for(dom, "polymul", batch, args.log_n, Lr) if args.prime_bits == 31 else None,
-        "alg_bytes_per_launch": alg_bytes[dom],
-        # the metric's "% HBM roofline" (3*L*N*8 B per poly-mul)
-        "whole_op_GBs": per_gpu * 3 * L * n * wb / 1e9,
-        "whole_op_frac": per_gpu * 3 * L * n * wb / 1e9 / HBM_PEAK_GBS,
-        "whole_op_frac_u64_equiv": per_gpu * 3 * L * n * 8 / 1e9 / HBM_PEAK_GBS,
+        # HBM bytes per rnt_mul from the committed PMC passes of this shape
+        # (profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per kernel)
+        "traffic": traffic,
+        "traffic_source": "profiles/pmc_traffic.json (committed rocprofv3 --pmc passes, not this run)",
+        "alg_bytes_per_launch": op_bytes,
+        "launch_ms": op_ms,
+        "launches": launches,
+        # SURVEY §8d's u64 accounting (3*L*N*8 B per poly-mul) of the same rate
+        "frac_u64_equiv": per_gpu * 3 * L * n * 8 / 1e9 / HBM_PEAK_GBS,
+        "whole_op_GBs_wall": per_gpu * 3 * L * n * wb / 1e9,
         "stream_copy_GBs": copy_gbs,
-        "whole_op_frac_of_copy": per_gpu * 3 * L * n * wb / 1e9 / copy_gbs if copy_gbs else None,
-        "whole_op_frac_of_copy_u64_equiv": per_gpu * 3 * L * n * 8 / 1e9 / copy_gbs if copy_gbs else None,
+        "frac_of_copy": achieved / copy_gbs if copy_gbs else None,
+        "kernels_roofline": kroof,
         "kernels": kernels,
     }
     if "row_mul" in kernels:
@@ -376,9 +416,9 @@ def run_polymul(args, comm, world, rank, local_rank):
         stages = log_c - 2 if trunc else log_c
         rb = 3 * elem * stages // 2 * args.steps / kernels["row_mul"]["launches"]
         ra = rb / (kernels["row_mul"]["avg_ms"] * 1e-3)
-        roofline["valu"] = {"kernel": "row_mul", "unit": "butterflies/s", "bfly_per_launch": rb,
-                            "row_stages_per_transform": stages, "truncated_transform": trunc,
-                            "achieved": ra, "peak": VALU_PEAK_BFLY, "frac": ra / VALU_PEAK_BFLY}
+        kroof["row_mul"].update(valu_unit="butterflies/s", bfly_per_launch=rb,
+                                row_stages_per_transform=stages, truncated_transform=trunc,
+                                valu_achieved=ra, valu_peak=VALU_PEAK_BFLY, valu_frac=ra / VALU_PEAK_BFLY)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(mod, n, args.cpu_seconds)

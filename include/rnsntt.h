@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define RNT_ABI_VERSION 3
+#define RNT_ABI_VERSION 4
 
 /* Status codes.  1..6 mirror RnsNttError in order
  * (src/rings/backends/rns_ntt/errors.rs:4-20). */
@@ -51,7 +51,11 @@ enum {
   RNT_ERR_BASIS_MISMATCH = 8,      /* reference: debug_assert Arc::ptr_eq (poly.rs:260-263, 288-291) */
   RNT_ERR_DEVICE = 9,              /* HIP runtime error                   */
   RNT_ERR_OUT_OF_MEMORY = 10,
-  RNT_ERR_BAD_ARGUMENT = 11
+  RNT_ERR_BAD_ARGUMENT = 11,
+  /* A valid reference input beyond this backend's capacity (no reference
+   * variant: the reference accepts it).  Today only ring degrees above
+   * 2^17 (rnt_ctx_create); fields = {degree, max_degree}. */
+  RNT_ERR_UNSUPPORTED = 12
 };
 
 typedef struct rnt_ctx rnt_ctx; /* == Arc<RnsBasis<N>> (basis.rs:90-94) */
@@ -70,6 +74,7 @@ const char* rnt_status_string(int status);
  *   4 InvalidModDrop         fields = {drop_count, channel_count}
  *   5 ChannelCountMismatch   fields = {expected, actual}
  *   6 NonReducedCoefficient  fields = {coefficient, modulus}
+ *  12 Unsupported            fields = {degree, max_degree} (no reference variant)
  * and {0, 0} for the statuses 7..11, which have no reference variant.
  * 0 (and {0, 0}) if no call on this thread has failed. */
 int rnt_last_error_detail(uint64_t fields[2]);
@@ -83,7 +88,8 @@ int rnt_device_count(int* n);
  * context's stream is bracketed by HIP events; rnt_profile_read syncs and
  * returns, for one kernel name ("col_fwd", "row_fwd", "row_inv",
  * "row_mul", "col_inv", "elementwise", "rescale", "automorphism",
- * "ks_decompose", "ks_rows", "tensor_rows", "import", "export"), the
+ * "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt", "sfft",
+ * "sample", "copy"), the
  * launch count and summed device milliseconds since enabling. */
 int rnt_profile_enable(const rnt_ctx* ctx, int enable);
 int rnt_profile_read(const rnt_ctx* ctx, const char* kernel, uint64_t* launches,
@@ -101,7 +107,11 @@ int rnt_find_psi(uint64_t modulus, uint64_t degree, uint64_t* psi);
 
 /* ---- context == RnsBasis ---------------------------------------------- */
 /* RnsBasis::new (basis.rs:97-106) + NttTable::new per modulus (:20-84):
- * validates like the reference, builds the device tables on `device`. */
+ * validates like the reference (EmptyBasis, then per modulus InvalidDegree
+ * for a degree that is not a power of two and NonNttFriendlyModulus), builds
+ * the device tables on `device`.  A power-of-two degree above 2^17, which the
+ * reference accepts, is RNT_ERR_UNSUPPORTED (this backend's table and grid
+ * limit), never InvalidDegree. */
 int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t count,
                    int device, rnt_ctx** out);
 /* Releases the caller's handle; like dropping an Arc, the context (and its
@@ -128,7 +138,10 @@ int rnt_sync(const rnt_ctx* ctx);
 
 /* ---- buffers == batches of RnsPoly ------------------------------------ */
 /* Allocates device storage for n_polys polynomials over ctx's basis, all
- * zero, coefficient domain (RnsPoly::zero, poly.rs:36-43). */
+ * zero, coefficient domain (RnsPoly::zero, poly.rs:36-43).  The zeroing is
+ * queued on the context's stream (rnt_ctx_stream) like every op: a reader on
+ * another stream (e.g. through rnt_buf_device_ptr) must order itself after
+ * that stream or call rnt_sync first. */
 int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out);
 /* Frees without waiting for the device: the buffer's device blocks go to a
  * per-device cache behind an event on the context stream, and a later
@@ -173,7 +186,10 @@ int rnt_crt_centered(const rnt_buf* buf, uint64_t* host, size_t n_polys, size_t 
  * caller, e.g. RCCL through torch.distributed):
  * rnt_buf_wrap makes a NON-owning buffer over caller device memory laid out
  * [L][n_polys][N] in the context's word width (device-internal order when
- * in_ntt); rnt_buf_device_ptr exposes a buffer's storage and word width. */
+ * in_ntt); rnt_buf_device_ptr exposes a buffer's storage and word width.
+ * Library writes to that storage (including rnt_buf_alloc's zeroing) are
+ * queued on the context's stream: order external reads after it (or call
+ * rnt_sync). */
 int rnt_buf_wrap(const rnt_ctx* ctx, void* device_ptr, size_t n_polys, int in_ntt,
                  rnt_buf** out);
 int rnt_buf_device_ptr(const rnt_buf* buf, void** device_ptr, size_t* word_bytes);

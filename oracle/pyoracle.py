@@ -14,7 +14,9 @@ from ctypes import POINTER, c_double, c_int, c_int32, c_int64, c_size_t, c_uint3
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# ORACLE_LIB: an alternative build of the same source (tools/sanitize.sh's
+# ASan/UBSan variant)
+LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 
 _U64P = POINTER(c_uint64)
 _I64P = POINTER(c_int64)

@@ -26,7 +26,7 @@ def declared_functions():
 
 def test_library_loads_and_exports_every_declared_symbol():
     lib = rns_ntt.load()
-    assert lib.rnt_abi_version() == 3
+    assert lib.rnt_abi_version() == 4
     names = declared_functions()
     assert len(names) >= 35
     for n in names:
@@ -38,9 +38,12 @@ def test_library_loads_and_exports_every_declared_symbol():
 def test_status_strings_mirror_rnsntt_error():
     lib = rns_ntt.load()
     want = ["ok", "InvalidDegree", "EmptyBasis", "NonNttFriendlyModulus", "InvalidModDrop",
-            "ChannelCountMismatch", "NonReducedCoefficient"]
+            "ChannelCountMismatch", "NonReducedCoefficient", "DomainMismatch", "BasisMismatch",
+            "DeviceError", "OutOfMemory", "BadArgument", "Unsupported"]
     for code, name in enumerate(want):
         assert lib.rnt_status_string(code).decode() == name
+        if code:
+            assert _lib.STATUS_NAMES[code] == name
 
 
 def test_generate_primes_matches_oracle_and_configs(vectors, manifest):
@@ -107,8 +110,14 @@ def test_ctx_validation_errors_without_gpu(kats):
     q18 = rns_ntt.generate_primes(31, 1, 1 << 18)[0]
     with pytest.raises(rns_ntt.RnsNttError) as e:
         rns_ntt.RnsBasis([q18], 1 << 18)
-    assert e.value.kind == "InvalidDegree"  # beyond this backend's 2^17 limit
-    assert e.value.fields == {"degree": 1 << 18}
+    # a valid degree the reference accepts, beyond this backend's 2^17 limit:
+    # the capacity status, not the reference's InvalidDegree (basis.rs:22-24)
+    assert e.value.kind == "Unsupported" and e.value.code == 12
+    assert e.value.fields == {"degree": 1 << 18, "max_degree": 1 << 17}
+    # EmptyBasis comes before the degree check (basis.rs:97-100)
+    with pytest.raises(rns_ntt.RnsNttError) as e:
+        rns_ntt.RnsBasis([], 12)
+    assert e.value.kind == "EmptyBasis"
 
 
 def test_error_detail_through_the_abi():
@@ -129,3 +138,80 @@ def test_error_detail_through_the_abi():
     a = rns_ntt.RnsNttError(6, "x", {"coefficient": 17, "modulus": 17})
     assert a == rns_ntt.RnsNttError(6, "y", {"coefficient": 17, "modulus": 17})
     assert a != rns_ntt.RnsNttError(6, "x", {"coefficient": 18, "modulus": 17})
+
+
+# ---- INTEGRATION.md's Rust extern block against include/rnsntt.h ----------
+
+_C_SCALARS = {"int": "c_int", "uint64_t": "u64", "int64_t": "i64", "uint32_t": "u32",
+              "int32_t": "i32", "size_t": "usize", "double": "f64", "char": "c_char",
+              "void": "c_void", "rnt_ctx": "rnt_ctx", "rnt_buf": "rnt_buf"}
+
+
+def _c_type_to_rust(ctype: str) -> str:
+    """`const uint64_t*` -> `*const u64`, `rnt_ctx**` -> `*mut *mut rnt_ctx`,
+    `uint64_t fields[2]` (array parameter) -> `*mut u64`."""
+    t = ctype.strip()
+    const = t.startswith("const ")
+    base = t[6:] if const else t
+    stars = base.count("*")
+    base = base.replace("*", "").strip()
+    rust = _C_SCALARS[base]
+    if stars == 0:
+        return rust
+    out = ("*const " if const else "*mut ") + rust
+    for _ in range(stars - 1):
+        out = "*mut " + out
+    return out
+
+
+def _header_prototypes():
+    text = open(os.path.join(REPO, "include", "rnsntt.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    protos = {}
+    for m in re.finditer(r"([A-Za-z_][\w\s\*]*?)\b(rnt_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", text):
+        ret, name, params = m.group(1).strip(), m.group(2), " ".join(m.group(3).split())
+        args = []
+        if params != "void":
+            for p in params.split(","):
+                p = p.strip()
+                arr = re.match(r"(.*?)\s*(\w+)\s*\[\d*\]$", p)
+                if arr:  # T name[k] decays to T*
+                    args.append(_c_type_to_rust(arr.group(1) + "*"))
+                else:
+                    pm = re.match(r"(.*?[\s\*])(\w+)$", p)
+                    args.append(_c_type_to_rust(pm.group(1)))
+        protos[name] = (_c_type_to_rust(ret), args)
+    return protos
+
+
+def _rust_block_prototypes():
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    block = re.search(r'extern "C" \{(.*?)\n\}', text, flags=re.S).group(1)
+    block = re.sub(r"//[^\n]*", "", block)
+    protos = {}
+    for m in re.finditer(r"pub fn (rnt_\w+)\((.*?)\)\s*(?:->\s*([^;]+))?;", block, flags=re.S):
+        name, params, ret = m.group(1), " ".join(m.group(2).split()), (m.group(3) or "()").strip()
+        args = [p.split(":", 1)[1].strip() for p in params.split(",") if p.strip()]
+        assert name not in protos, f"{name} declared twice in INTEGRATION.md"
+        protos[name] = (" ".join(ret.split()), [" ".join(a.split()) for a in args])
+    return protos
+
+
+def test_integration_rust_block_matches_header():
+    """Every function of include/rnsntt.h has exactly one line in
+    INTEGRATION.md's Rust extern block, with the same arity and the
+    corresponding argument and return types (the block must
+    carry rnt_to_coeffs, rnt_mod_drop_last, rnt_sub and the basis getters
+    the shim needs for traits.rs:28-64 and basis.rs:108-145)."""
+    c = _header_prototypes()
+    r = _rust_block_prototypes()
+    assert sorted(c) == declared_functions()
+    assert sorted(r) == sorted(c), (sorted(set(c) - set(r)), sorted(set(r) - set(c)))
+    for name, (ret, args) in c.items():
+        rret, rargs = r[name]
+        assert rret == ret, (name, rret, ret)
+        assert len(rargs) == len(args), (name, rargs, args)
+        assert rargs == args, (name, rargs, args)
+    for needed in ("rnt_to_coeffs", "rnt_mod_drop_last", "rnt_sub", "rnt_ctx_moduli",
+                   "rnt_ctx_total_bits", "rnt_ctx_channel_count"):
+        assert needed in r

@@ -155,15 +155,44 @@ def test_decomposition_groups(gpu, monkeypatch, jg):
         assert np.array_equal(g0[p], w0[:Lt]) and np.array_equal(g1[p], w1[:Lt]), p
 
 
-@pytest.mark.parametrize("log_n,B", [(12, 1), (12, 3), (12, 40), (14, 2), (14, 9), (14, 33), (16, 1), (16, 5),
-                                     (16, 8), (16, 17), (17, 1), (17, 3), (17, 4)])
-def test_keyswitch_row_grids(gpu, log_n, B):
-    """rnt_keyswitch's rows kernel picks its grid by batch: one poly x RPW
-    rows per workgroup when 2B < RPW (RPW = 16 rows at N <= 2^16, 8 at
-    2^17), RPW polys x one row otherwise; key rows are staged through
-    registers or by direct global->LDS loads by row length and grid
-    (rnt_kernels.hip ks_rows_pick / kKeyGlds).  Every combination, first
-    and last poly of the batch, against the oracle's gadget sum
+# (log_n, B) -> the grid ks_rows_pick chooses (NP polys x RPW/NP rows per
+# workgroup; RPW = 64, 32, 16, 8 rows at N = 2^12, 2^14, 2^16, 2^17): the
+# largest NP whose grid fills >= 90% of its row slots, else the best fill.
+# NP = 2/4/8 exist for 2^8- and 2^9-word rows (N = 2^16, 2^17) only.
+_KS_GRIDS = [(12, 1, 1), (12, 3, 1), (12, 40, 1), (12, 127, 64), (14, 2, 1), (14, 9, 1), (14, 33, 1),
+             (14, 63, 32), (16, 1, 1), (16, 2, 2), (16, 5, 1), (16, 8, 8), (16, 12, 4), (16, 16, 16),
+             (16, 17, 2), (16, 63, 16), (17, 1, 1), (17, 2, 2), (17, 3, 1), (17, 4, 4), (17, 6, 2),
+             (17, 8, 8)]
+
+
+def _ks_np(log_n, B):
+    """Python restatement of ks_rows_pick (rnt_kernels.hip) for the table."""
+    rpw = {12: 64, 14: 32, 16: 16, 17: 8}[log_n]
+    have = [c for c in (64, 32, 16, 8, 4, 2, 1) if c <= rpw and (c in (rpw, 1) or (log_n in (16, 17) and c <= 8))]
+    best, best_c = -1.0, rpw
+    for c in have:
+        fill = B / (-(-B // c) * c)
+        if fill >= 0.9:
+            return c
+        if fill > best + 1e-9:
+            best, best_c = fill, c
+    return best_c
+
+
+def test_keyswitch_grid_table_matches_picker():
+    assert [(ln, B, _ks_np(ln, B)) for ln, B, _ in _KS_GRIDS] == _KS_GRIDS
+
+
+@pytest.mark.parametrize("log_n,B,np_", _KS_GRIDS)
+def test_keyswitch_row_grids(gpu, log_n, B, np_):
+    """rnt_keyswitch's rows kernel picks its grid by batch (ks_rows_pick):
+    NP polys x RPW/NP consecutive rows per workgroup, the largest NP whose
+    grid fills at least 90% of its row slots (key rows shared by NP polys),
+    else the best-filled grid; key rows are staged through registers or by
+    direct global->LDS loads by row length and grid (kKeyGlds).  The table
+    runs every NP the picker can choose at each ring (NP = 1, 2, 4, 8 and
+    RPW), including odd large batches (63, 127) that keep the shared-key
+    grid, first and last poly of the batch, against the oracle's gadget sum
     (engine.rs:505-528)."""
     rn = gpu
     n, L = 1 << log_n, 4

@@ -113,7 +113,7 @@ struct Tables {
 enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
-  K_SFFT, K_SAMPLE, K_COUNT
+  K_SFFT, K_SAMPLE, K_COPY, K_COUNT
 };
 
 struct Prof {
@@ -200,6 +200,9 @@ hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const voi
 // 3 pointwise mul (canonical a*b mod q), 4 Montgomery product (a*b*2^-w).
 hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a,
                               const void* b);
+// Plain device copy of `bytes` (16-byte aligned pointers, bytes % 16 == 0):
+// every lane moves 4 x 16 B, loads before stores (Clone, rnt_copy).
+hipError_t launch_copy(hipStream_t s, void* dst, const void* src, uint64_t bytes);
 // k.L = limbs of the input; output has k.L - 1 (same poly count / stride B*N).
 hipError_t launch_rescale(const Launch& k, void* out, const void* in);
 // Centred CRT of every coefficient (coefficient-domain `in`, k.L limbs) into

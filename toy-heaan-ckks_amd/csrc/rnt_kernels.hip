@@ -982,12 +982,20 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
   }
 }
 
+// Words per padded LDS key row: C + C/16 (ks_pad's 4 per 64), rounded up to
+// a whole 16-byte unit (the host sizes the LDS with the same formula).
+template <class W>
+__host__ __device__ constexpr int ks_kpad_words(int c) {
+  constexpr int V = 16 / (int)sizeof(W);
+  return (c + (c >> 4) + V - 1) / V * V;
+}
 // Padded LDS position of key word w: 4 pad words per 64, so the 16-byte
 // reads of 16 lanes at 64-byte strides (a row's E = 16 consecutive words per
 // thread) start on 16 distinct 4-bank groups, and 16-byte alignment holds.
 __device__ __forceinline__ uint32_t ks_pad(uint32_t w) { return w + ((w >> 6) << 2); }
 // 16 bytes of LDS into registers (p is 16-byte aligned by construction:
-// ks_pad keeps every thread's run of E words on a 16-byte boundary).
+// key rows start on ks_kpad_words boundaries, and ks_pad keeps every
+// thread's run of E words within a row on a 16-byte boundary).
 template <class W>
 __device__ __forceinline__ void ks_lds_read16(W (&o)[16 / sizeof(W)], const W* p) {
   const uint4 v = *(const uint4*)p;
@@ -1038,7 +1046,10 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   using G = RowGeo<LOG_C>;
   constexpr int E = G::E;
   constexpr int C = G::C;
-  constexpr int KPAD = C + (C >> 4);  // padded key row (ks_pad)
+  // padded key row (ks_pad), rounded up to 16 bytes so every key row --
+  // hence every thread's 16-byte LDS read -- starts 16-byte aligned also for
+  // short rows (C = 16/32, where C + C/16 alone is 17 or 34 words)
+  constexpr int KPAD = ks_kpad_words<W>(C);
   // NP polys x KROWS consecutive rows per workgroup (NP = RPW: one row r
   // for RPW polys; NP = 1: one poly, RPW rows); the key rows of a source
   // limb are staged per workgroup, KROWS of each key
@@ -1137,8 +1148,17 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
                                            (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
         }
       }
+      // pin the order: the LDS-DMA key loads issue before the S loads, so the
+      // (in-order) vmcnt wait for x below also covers them; the exchange
+      // barriers after it then publish kb to the other waves
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
+      if constexpr (G::P < 2) {
+        // no exchange barrier follows: wait for this wave's DMA explicitly
+        // before the barrier below publishes kb
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     } else {
       W kr[KPT];
 #pragma unroll
@@ -1697,6 +1717,29 @@ static hipError_t elementwise_t(const Launch& k, int op, void* out, const void* 
   return hipGetLastError();
 }
 
+// Clone: 4 x 16 B per lane, all four loads issued before the stores.
+__global__ void __launch_bounds__(256)
+k_copy16(uint4* __restrict__ dst, const uint4* __restrict__ src, uint64_t n16) {
+  const uint64_t base = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  uint4 v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (base + u * 256 < n16) v[u] = src[base + u * 256];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (base + u * 256 < n16) dst[base + u * 256] = v[u];
+}
+
+hipError_t launch_copy(hipStream_t s, void* dst, const void* src, uint64_t bytes) {
+  const uint64_t n16 = bytes / 16;
+  if (n16 == 0) return hipSuccess;
+  const uint64_t blocks = (n16 + 1023) / 1024;
+  if (blocks > 0x7fffffffull) return hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL(k_copy16, dim3((unsigned)blocks), dim3(256), 0, s, (uint4*)dst,
+                     (const uint4*)src, n16);
+  return hipGetLastError();
+}
+
 // k.L = limbs of the INPUT; output has k.L - 1.
 template <class W>
 static hipError_t rescale_t(const Launch& k, void* out, const void* in) {
@@ -1851,7 +1894,7 @@ static hipError_t ks_rows_launch(const Launch& k, void* u0, void* u1, uint64_t l
                                  const void* init0, const void* init1, uint64_t init_ls) {
   using G = RowGeo<LOG_C>;
   constexpr int KROWS = G::RPW / NP;
-  constexpr size_t KPADB = (G::C + (G::C >> 4)) * sizeof(W);
+  constexpr size_t KPADB = (size_t)ks_kpad_words<W>(G::C) * sizeof(W);
   const Geom g = geom_for(k.t->log_n);
   if (k.L == 0 || k.B == 0) return hipSuccess;
   if (g.r % KROWS) return hipErrorInvalidValue;
@@ -1888,15 +1931,29 @@ static hipError_t ks_rows_pick(const Launch& k, void* u0, void* u1, uint64_t ls,
   using G = RowGeo<LOG_C>;
   constexpr int RPW = G::RPW;
   const Geom g = geom_for(k.t->log_n);
+  // NP = polys per workgroup (each key row is loaded once for NP polys).
+  // Take the largest NP whose grid fills at least 90% of its row slots:
+  // slot fill alone would pick NP = 1 (always 100% full, no key sharing,
+  // the most expensive grid) for every odd batch, e.g. a 63-poly last chunk
+  // of a 1023-ciphertext batch.  Below that fill (small batches, B < RPW
+  // mostly) the best-filled grid wins, the larger NP on a tie.
   int np = RPW;
   if (sizeof(W) == 4 && G::C >= 64 && RPW > 1) {
     double best = -1.0;
+    int best_np = RPW;
+    bool chosen = false;
     for (int c = RPW; c >= 1; c >>= 1) {
       const bool have = c == RPW || c == 1 || ((LOG_C == 8 || LOG_C == 9) && c <= 8);
       if (!have || g.r % (RPW / c)) continue;
       const double fill = (double)k.B / (double)(((k.B + c - 1) / c) * c);
-      if (fill > best + 1e-9) { best = fill; np = c; }
+      if (fill >= 0.9) {
+        np = c;
+        chosen = true;
+        break;
+      }
+      if (fill > best + 1e-9) { best = fill; best_np = c; }
     }
+    if (!chosen) np = best_np;
   }
 #define RNT_NP(V) \
   if (np == (V) && RPW % (V) == 0) \

@@ -44,6 +44,7 @@ enum class RnsNttErrorKind {
   Device = RNT_ERR_DEVICE,
   OutOfMemory = RNT_ERR_OUT_OF_MEMORY,
   BadArgument = RNT_ERR_BAD_ARGUMENT,
+  Unsupported = RNT_ERR_UNSUPPORTED,  // beyond the backend's capacity (N > 2^17)
 };
 
 // The variant and its fields, as the reference's struct variants carry them
@@ -62,12 +63,13 @@ class RnsNttError : public std::runtime_error {
       case RnsNttErrorKind::InvalidModDrop: drop_count = f0; channel_count = f1; break;
       case RnsNttErrorKind::ChannelCountMismatch: expected = f0; actual = f1; break;
       case RnsNttErrorKind::NonReducedCoefficient: coefficient = f0; modulus = f1; break;
+      case RnsNttErrorKind::Unsupported: degree = f0; max_degree = f1; break;
       default: break;
     }
   }
   RnsNttErrorKind kind;
   uint64_t degree = 0, modulus = 0, drop_count = 0, channel_count = 0, expected = 0, actual = 0,
-           coefficient = 0;
+           coefficient = 0, max_degree = 0;
 };
 
 // Throws the failing call's variant with the fields rnt_last_error_detail
@@ -97,6 +99,8 @@ class RnsBasis : public std::enable_shared_from_this<RnsBasis<N>> {
   // RnsBasis::new (basis.rs:97-106): InvalidDegree / EmptyBasis /
   // NonNttFriendlyModulus like the reference.
   static BasisRef<N> create(const std::vector<uint64_t>& moduli, int device = 0) {
+    if (moduli.empty())  // basis.rs:98-100 comes before NttTable::new's degree check
+      throw RnsNttError(RNT_ERR_EMPTY_BASIS, "RNS basis must contain at least one modulus");
     if (((size_t)1 << log2_exact(N)) != N)
       throw RnsNttError(RNT_ERR_INVALID_DEGREE, "N is not a power of two", N);
     rnt_ctx* c = nullptr;

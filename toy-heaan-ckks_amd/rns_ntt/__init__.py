@@ -125,15 +125,21 @@ class RnsBasis:
 
     ``RnsBasis(moduli, degree)`` validates like ``RnsBasis::new``
     (basis.rs:97-106): ``EmptyBasis`` for no moduli, ``InvalidDegree`` for a
-    non power-of-two degree, ``NonNttFriendlyModulus`` otherwise.
+    non power-of-two degree, ``NonNttFriendlyModulus`` otherwise; a valid
+    degree above 2^17 raises ``Unsupported`` (this backend's capacity).
     """
 
     def __init__(self, moduli: Sequence[int], degree: int, device: int = 0):
         lib = load()
-        if degree <= 0 or degree & (degree - 1):
+        # basis.rs:97-106 order: EmptyBasis first (rnt_ctx_create checks it),
+        # then per modulus NttTable::new's InvalidDegree (basis.rs:22-24: not a
+        # power of two) and NonNttFriendlyModulus.  A power-of-two degree
+        # above this backend's 2^17 is Unsupported (status 12), never
+        # InvalidDegree.
+        if len(moduli) and (degree <= 0 or degree & (degree - 1)):
             raise RnsNttError(_lib.INVALID_DEGREE, f"ring degree must be a power of two, got {degree}",
                               {"degree": degree})
-        log_n = degree.bit_length() - 1
+        log_n = degree.bit_length() - 1 if degree > 0 and not degree & (degree - 1) else 0
         arr = np.ascontiguousarray(np.array(list(moduli), dtype=np.uint64)) if len(moduli) else np.zeros(1, np.uint64)
         h = ctypes.c_void_p()
         check(lib.rnt_ctx_create(log_n, _u64p(arr), len(moduli), device, ctypes.byref(h)))
@@ -239,31 +245,47 @@ class RnsPoly:
 
     Mirrors ``RnsPoly<N>`` (poly.rs:25-570).  Operators follow the Rust ones:
     ``a *= b`` (MulAssign), ``a += b`` (AddAssign), ``-a`` (Neg).
+
+    An object is either the reference's single polynomial (built without a
+    batch count: ``RnsPoly(basis)``, ``from_channels([L][N])``,
+    ``from_coeffs([N])``, ``sample_*(...)`` without ``n_polys``) or a batch
+    (``RnsPoly(basis, B)``, ``from_channels([B][L][N])`` ...), and every
+    result of an op is of the same kind as its input.  Host views follow the
+    kind, never the batch size: ``channels()`` is [L][N] for a single
+    polynomial and [B][L][N] for a batch (also when B == 1);
+    ``channels_batch()`` is always [B][L][N].
     """
 
-    def __init__(self, basis: RnsBasis, n_polys: int = 1):
+    def __init__(self, basis: RnsBasis, n_polys: Optional[int] = None):
         lib = load()
         h = ctypes.c_void_p()
-        check(lib.rnt_buf_alloc(basis.handle, n_polys, ctypes.byref(h)))
+        count = 1 if n_polys is None else int(n_polys)
+        check(lib.rnt_buf_alloc(basis.handle, count, ctypes.byref(h)))
         self._h = h
         self.basis = basis
-        self.n_polys = n_polys
+        self.n_polys = count
+        self.batched = n_polys is not None
+
+    def _like(self, basis: Optional[RnsBasis] = None) -> "RnsPoly":
+        """A zero output of this object's kind and batch on ``basis``."""
+        return RnsPoly(basis or self.basis, self.n_polys if self.batched else None)
 
     # -- constructors (poly.rs:34-114) --------------------------------------
     @classmethod
-    def zero(cls, basis: RnsBasis, n_polys: int = 1) -> "RnsPoly":
+    def zero(cls, basis: RnsBasis, n_polys: Optional[int] = None) -> "RnsPoly":
         return cls(basis, n_polys)
 
     @classmethod
     def from_coeffs(cls, coeffs, basis: RnsBasis) -> "RnsPoly":
         """poly.rs:49-67; ``coeffs`` is [N] or [B][N] signed integers."""
         c = np.asarray(coeffs, dtype=np.int64)
-        if c.ndim == 1:
+        single = c.ndim == 1
+        if single:
             c = c[None, :]
         if c.shape[1] < basis.degree:
             raise ValueError(f"from_coeffs: need at least {basis.degree} coefficients, got {c.shape[1]}")
         c = np.ascontiguousarray(c[:, : basis.degree])
-        p = cls(basis, c.shape[0])
+        p = cls(basis, None if single else c.shape[0])
         check(load().rnt_upload_coeffs(p._h, _i64p(c), c.shape[0]))
         return p
 
@@ -274,12 +296,13 @@ class RnsPoly:
         Raises ChannelCountMismatch / NonReducedCoefficient like the reference.
         """
         ch = np.asarray(channels, dtype=np.uint64)
-        if ch.ndim == 2:
+        single = ch.ndim == 2
+        if single:
             ch = ch[None, :, :]
         if ch.ndim != 3 or ch.shape[2] != basis.degree:
             raise ValueError("from_channels: expected [L][N] or [B][L][N] with N == degree")
         ch = np.ascontiguousarray(ch)
-        p = cls(basis, ch.shape[0])
+        p = cls(basis, None if single else ch.shape[0])
         check(load().rnt_upload(p._h, _u64p(ch), ch.shape[0], ch.shape[1], 1 if in_ntt_domain else 0))
         return p
 
@@ -297,30 +320,31 @@ class RnsPoly:
         p._h = h
         p.basis = basis
         p.n_polys = n_polys
+        p.batched = True
         p._owner = owner
         return p
 
     # -- PolySampler (traits.rs:74-127; poly.rs:438-477), on the device -----
     @classmethod
-    def sample_uniform(cls, basis: RnsBasis, rng: DeviceRng, n_polys: int = 1) -> "RnsPoly":
+    def sample_uniform(cls, basis: RnsBasis, rng: DeviceRng, n_polys: Optional[int] = None) -> "RnsPoly":
         p = cls(basis, n_polys)
         check(load().rnt_sample_uniform(p._h, rng.seed, rng.next_stream()))
         return p
 
     @classmethod
-    def sample_gaussian(cls, std_dev: float, basis: RnsBasis, rng: DeviceRng, n_polys: int = 1) -> "RnsPoly":
+    def sample_gaussian(cls, std_dev: float, basis: RnsBasis, rng: DeviceRng, n_polys: Optional[int] = None) -> "RnsPoly":
         p = cls(basis, n_polys)
         check(load().rnt_sample_gaussian(p._h, float(std_dev), rng.seed, rng.next_stream()))
         return p
 
     @classmethod
-    def sample_tribits(cls, hamming_weight: int, basis: RnsBasis, rng: DeviceRng, n_polys: int = 1) -> "RnsPoly":
+    def sample_tribits(cls, hamming_weight: int, basis: RnsBasis, rng: DeviceRng, n_polys: Optional[int] = None) -> "RnsPoly":
         p = cls(basis, n_polys)
         check(load().rnt_sample_ternary(p._h, int(hamming_weight), rng.seed, rng.next_stream()))
         return p
 
     @classmethod
-    def sample_noise(cls, variance: float, basis: RnsBasis, rng: DeviceRng, n_polys: int = 1) -> "RnsPoly":
+    def sample_noise(cls, variance: float, basis: RnsBasis, rng: DeviceRng, n_polys: Optional[int] = None) -> "RnsPoly":
         """poly.rs:471-477: Gaussian with std_dev = sqrt(variance)."""
         return cls.sample_gaussian(float(np.sqrt(variance)), basis, rng, n_polys)
 
@@ -337,10 +361,16 @@ class RnsPoly:
         return self._h
 
     def channels(self) -> np.ndarray:
-        """[L][N] for a single polynomial, [B][L][N] for a batch."""
+        """poly.rs:119-121: [L][N] for a single polynomial, [B][L][N] for a
+        batch object (whatever its size; see the class docstring)."""
+        out = self.channels_batch()
+        return out if self.batched else out[0]
+
+    def channels_batch(self) -> np.ndarray:
+        """[B][L][N] always (B = 1 for a single polynomial)."""
         out = np.zeros((self.n_polys, self.basis.channel_count(), self.basis.degree), dtype=np.uint64)
         check(load().rnt_download(self._h, _u64p(out), self.n_polys))
-        return out[0] if self.n_polys == 1 else out
+        return out
 
     def channels_of(self, first: int, count: int = 1) -> np.ndarray:
         """[count][L][N]: channels of polys first .. first+count-1 of the batch."""
@@ -354,7 +384,7 @@ class RnsPoly:
         return bool(r.value)
 
     def clone(self) -> "RnsPoly":
-        p = RnsPoly(self.basis, self.n_polys)
+        p = self._like()
         check(load().rnt_copy(p._h, self._h))
         return p
 
@@ -379,28 +409,28 @@ class RnsPoly:
         return self
 
     def __mul__(self, rhs: "RnsPoly") -> "RnsPoly":
-        out = RnsPoly(self.basis, self.n_polys)
+        out = self._like()
         check(load().rnt_mul(out._h, self._h, rhs._h))
         return out
 
     def __add__(self, rhs: "RnsPoly") -> "RnsPoly":
-        out = RnsPoly(self.basis, self.n_polys)
+        out = self._like()
         check(load().rnt_add(out._h, self._h, rhs._h))
         return out
 
     def __sub__(self, rhs: "RnsPoly") -> "RnsPoly":
-        out = RnsPoly(self.basis, self.n_polys)
+        out = self._like()
         check(load().rnt_sub(out._h, self._h, rhs._h))
         return out
 
     def __neg__(self) -> "RnsPoly":
-        out = RnsPoly(self.basis, self.n_polys)
+        out = self._like()
         check(load().rnt_neg(out._h, self._h))
         return out
 
     # -- rescale / mod-drop (poly.rs:168-249) -------------------------------
     def rescale_into(self, new_basis: RnsBasis) -> "RnsPoly":
-        out = RnsPoly(new_basis, self.n_polys)
+        out = self._like(new_basis)
         check(load().rnt_rescale(out._h, self._h))
         return out
 
@@ -413,18 +443,18 @@ class RnsPoly:
 
     def mod_drop_last(self, drop_count: int) -> "RnsPoly":
         nb = self.basis.drop_last(drop_count)
-        out = RnsPoly(nb, self.n_polys)
+        out = self._like(nb)
         check(load().rnt_mod_drop_last(out._h, self._h))
         return out
 
     # -- automorphisms (poly.rs:482-570) ------------------------------------
     def automorphism(self, exponent: int) -> "RnsPoly":
-        out = RnsPoly(self.basis, self.n_polys)
+        out = self._like()
         check(load().rnt_automorphism(out._h, self._h, exponent))
         return out
 
     def rotate_slots(self, k: int) -> "RnsPoly":
-        out = RnsPoly(self.basis, self.n_polys)
+        out = self._like()
         check(load().rnt_rotate_slots(out._h, self._h, k))
         return out
 
@@ -435,11 +465,11 @@ class RnsPoly:
         the device (rnt_to_coeffs)."""
         out = np.zeros((self.n_polys, self.basis.degree), dtype=np.int64)
         check(load().rnt_to_coeffs(self._h, out.ctypes.data_as(ctypes.c_void_p), self.n_polys))
-        return out[0] if self.n_polys == 1 else out
+        return out if self.batched else out[0]
 
     def to_coeffs_exact(self) -> list:
         """The centred CRT values as Python ints for any Q (rnt_crt_centered):
-        [N] for one polynomial, [B][N] nested lists for a batch."""
+        [N] for a single polynomial, [B][N] nested lists for a batch object."""
         bits = sum(int(q).bit_length() for q in self.basis.moduli())
         words = max(1, (bits + 1 + 63) // 64)
         raw = np.zeros((self.n_polys, self.basis.degree, words), dtype=np.uint64)
@@ -455,7 +485,7 @@ class RnsPoly:
                     v -= 1 << (64 * words)
                 row.append(v)
             out.append(row)
-        return out[0] if self.n_polys == 1 else out
+        return out if self.batched else out[0]
 
     def __del__(self, _lib=_lib):  # module globals may be gone at interpreter exit
         h = getattr(self, "_h", None)
@@ -500,8 +530,7 @@ class Ciphertext:
 
 def keyswitch(d: RnsPoly, key: RnsGadgetKey) -> tuple[RnsPoly, RnsPoly]:
     """Gadget sum (engine.rs:505-528 / 429-452) on a coefficient-domain batch."""
-    acc0 = RnsPoly(d.basis, d.n_polys)
-    acc1 = RnsPoly(d.basis, d.n_polys)
+    acc0, acc1 = d._like(), d._like()
     check(load().rnt_keyswitch(acc0.handle, acc1.handle, d.handle, key.a.handle, key.b.handle))
     return acc0, acc1
 
@@ -510,8 +539,7 @@ def mul_ciphertexts_gadget(ct1: Ciphertext, ct2: Ciphertext, rlk: RnsGadgetKey) 
     """engine.rs:473-539."""
     assert ct1.logq == ct2.logq, "logq mismatch in gadget multiplication"
     basis = ct1.c0.basis
-    out0 = RnsPoly(basis, ct1.c0.n_polys)
-    out1 = RnsPoly(basis, ct1.c0.n_polys)
+    out0, out1 = ct1.c0._like(basis), ct1.c0._like(basis)
     check(load().rnt_ct_mul_relin(out0.handle, out1.handle, ct1.c0.handle, ct1.c1.handle,
                                   ct2.c0.handle, ct2.c1.handle, rlk.a.handle, rlk.b.handle))
     return Ciphertext(out0, out1, ct1.logp + ct2.logp, ct1.logq)
@@ -520,8 +548,7 @@ def mul_ciphertexts_gadget(ct1: Ciphertext, ct2: Ciphertext, rlk: RnsGadgetKey) 
 def rotate_ciphertext(ct: Ciphertext, rotk: RnsGadgetKey) -> Ciphertext:
     """engine.rs:412-463."""
     basis = ct.c0.basis
-    out0 = RnsPoly(basis, ct.c0.n_polys)
-    out1 = RnsPoly(basis, ct.c0.n_polys)
+    out0, out1 = ct.c0._like(basis), ct.c0._like(basis)
     check(load().rnt_ct_rotate(out0.handle, out1.handle, ct.c0.handle, ct.c1.handle,
                                int(rotk.rotation or 0), rotk.a.handle, rotk.b.handle))
     return Ciphertext(out0, out1, ct.logp, ct.logq)
@@ -532,8 +559,7 @@ def rescale_ciphertext(ct: Ciphertext) -> Ciphertext:
     q_last = ct.c0.basis.moduli()[-1]
     bits_dropped = q_last.bit_length()
     new_basis = ct.c0.basis.drop_last(1)
-    out0 = RnsPoly(new_basis, ct.c0.n_polys)
-    out1 = RnsPoly(new_basis, ct.c0.n_polys)
+    out0, out1 = ct.c0._like(new_basis), ct.c0._like(new_basis)
     check(load().rnt_ct_rescale(out0.handle, out1.handle, ct.c0.handle, ct.c1.handle))
     return Ciphertext(out0, out1, ct.logp - bits_dropped, ct.logq - bits_dropped)
 
@@ -589,7 +615,7 @@ class CkksEncoder:
         if n_values > self.degree // 2:
             raise ValueError(f"{_name}: {n_values} values exceed max slots {self.degree // 2}")
         buf = np.ascontiguousarray(rows)
-        poly = RnsPoly(basis, rows.shape[0])
+        poly = RnsPoly(basis, None if v.ndim <= 1 else rows.shape[0])
         check(load().rnt_encode(poly.handle, buf.ctypes.data_as(ctypes.c_void_p), n_values, self.scale_bits))
         return Plaintext(poly, self.scale_bits, n_values)
 
@@ -598,11 +624,11 @@ class CkksEncoder:
         return self.decode_complex(pt).real
 
     def decode_complex(self, pt: Plaintext) -> np.ndarray:
-        """ckks_encoder.rs:134-156 (rows for a batch of polys)."""
+        """ckks_encoder.rs:134-156 (one row per poly of a batch object)."""
         B = pt.poly.n_polys
         out = np.zeros((B, pt.slots), dtype=np.complex128)
         check(load().rnt_decode(pt.poly.handle, out.ctypes.data_as(ctypes.c_void_p), pt.slots, pt.scale_bits))
-        return out[0] if B == 1 else out
+        return out if pt.poly.batched else out[0]
 
 
 # ---------------------------------------------------------------------------
@@ -615,9 +641,8 @@ def ct_tensor(c0: RnsPoly, c1: RnsPoly, c0p: RnsPoly, c1p: RnsPoly,
     """Tensor product (engine.rs:480-493) on this basis' limbs: d0, d1 in the
     NTT domain (key-switch seeds), d2 in the coefficient domain (written into
     ``d2_out`` when given, e.g. a wrapped collective buffer)."""
-    basis, B = c0.basis, c0.n_polys
-    d0, d1 = RnsPoly(basis, B), RnsPoly(basis, B)
-    d2 = d2_out if d2_out is not None else RnsPoly(basis, B)
+    d0, d1 = c0._like(), c0._like()
+    d2 = d2_out if d2_out is not None else c0._like()
     check(load().rnt_ct_tensor(d0.handle, d1.handle, d2.handle, c0.handle, c1.handle,
                                c0p.handle, c1p.handle))
     return d0, d1, d2
@@ -643,6 +668,6 @@ def rescale_ext(x: RnsPoly, last_ptr: int, q_last: int, out_basis: RnsBasis,
                 out: Optional[RnsPoly] = None) -> RnsPoly:
     """rescale_into (poly.rs:187-228) by an external last limb: residues mod
     ``q_last`` ([n_polys][N] words, coefficient domain) at ``last_ptr``."""
-    o = out if out is not None else RnsPoly(out_basis, x.n_polys)
+    o = out if out is not None else x._like(out_basis)
     check(load().rnt_rescale_ext(o.handle, x.handle, ctypes.c_void_p(last_ptr), int(q_last)))
     return o

@@ -27,6 +27,7 @@ BASIS_MISMATCH = 8
 DEVICE = 9
 OUT_OF_MEMORY = 10
 BAD_ARGUMENT = 11
+UNSUPPORTED = 12  # beyond this backend's capacity (degree > 2^17); no reference variant
 
 STATUS_NAMES = {
     1: "InvalidDegree",
@@ -40,6 +41,7 @@ STATUS_NAMES = {
     9: "DeviceError",
     10: "OutOfMemory",
     11: "BadArgument",
+    12: "Unsupported",
 }
 
 
@@ -51,6 +53,7 @@ FIELD_NAMES = {
     4: ("drop_count", "channel_count"),
     5: ("expected", "actual"),
     6: ("coefficient", "modulus"),
+    12: ("degree", "max_degree"),
 }
 
 

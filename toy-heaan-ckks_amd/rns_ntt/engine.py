@@ -60,15 +60,18 @@ class CkksEngine:
         self.hamming_weight = hamming_weight if hamming_weight is not None else degree // 2
 
     # -- samplers (traits.rs PolySampler): device for a DeviceRng, else host -
-    def _tern_poly(self, rng, count=1) -> RnsPoly:
+    # count=None draws the reference's single polynomial, count=k a batch of k
+    def _tern_poly(self, rng, count=None) -> RnsPoly:
         if isinstance(rng, DeviceRng):
             return RnsPoly.sample_tribits(self.hamming_weight, self.basis, rng, count)
-        return RnsPoly.from_coeffs(self._ternary(rng, count), self.basis)
+        c = self._ternary(rng, count or 1)
+        return RnsPoly.from_coeffs(c if count else c[0], self.basis)
 
-    def _gauss_poly(self, rng, count=1) -> RnsPoly:
+    def _gauss_poly(self, rng, count=None) -> RnsPoly:
         if isinstance(rng, DeviceRng):
             return RnsPoly.sample_gaussian(self.error_std, self.basis, rng, count)
-        return RnsPoly.from_coeffs(self._gaussian(rng, count), self.basis)
+        c = self._gaussian(rng, count or 1)
+        return RnsPoly.from_coeffs(c if count else c[0], self.basis)
 
     def _ternary(self, rng, count=1):
         n = self.degree
@@ -81,13 +84,13 @@ class CkksEngine:
     def _gaussian(self, rng, count=1):
         return np.rint(rng.normal(0.0, self.error_std, size=(count, self.degree))).astype(np.int64)
 
-    def _uniform(self, rng, count=1, basis: Optional[RnsBasis] = None):
+    def _uniform(self, rng, count=None, basis: Optional[RnsBasis] = None):
         b = basis or self.basis
         if isinstance(rng, DeviceRng):
             return RnsPoly.sample_uniform(b, rng, count)
         q = np.array(b.moduli(), dtype=np.uint64)[None, :, None]
-        ch = rng.integers(0, 1 << 62, size=(count, len(b.moduli()), self.degree), dtype=np.uint64) % q
-        return RnsPoly.from_channels(ch, b)
+        ch = rng.integers(0, 1 << 62, size=(count or 1, len(b.moduli()), self.degree), dtype=np.uint64) % q
+        return RnsPoly.from_channels(ch if count else ch[0], b)
 
     # -- keys (engine.rs:288-399, keys/*.rs) ---------------------------------
     def generate_secret_key(self, rng) -> RnsPoly:

@@ -212,8 +212,7 @@ class GpuBackend:
         return RnsPoly.from_channels(channels, basis)
 
     def download(self, poly) -> np.ndarray:
-        ch = poly.channels()
-        return ch if ch.ndim == 3 else ch[None]
+        return poly.channels_batch()
 
     def key(self, basis, a_channels: np.ndarray, b_channels: np.ndarray):
         from . import RnsGadgetKey
