@@ -77,6 +77,11 @@ def parse():
     p.add_argument("--rot-offsets", choices=("pow2", "all"), default="pow2",
                    help="rotate: the log2(N/2) power-of-two offsets, or every offset 1..N/2-1 with "
                         "one resident key (SURVEY 8d sweep 2)")
+    p.add_argument("--graph", action="store_true",
+                   help="ctmul / rotate: the reference engine's call shape -- fused per-call C-ABI ops "
+                        "(rnt_ct_mul_relin + rnt_ct_rescale, rnt_ct_rotate) on each GPU's own ciphertexts, "
+                        "the step recorded once as a HIP graph and replayed (rnt_capture_begin / "
+                        "rnt_graph_launch); reports device-busy = kernel time / step time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-power", action="store_true", help="skip the rocm-smi power/clock samples")
     p.add_argument("--strong", action="store_true",
@@ -454,8 +459,122 @@ def run_polymul(args, comm, world, rank, local_rank):
     }
 
 
+def _graph_step_timing(basis, step, steps, warmup, comm, kernel_names):
+    """Warm `step` eagerly, time one eager step's kernels with HIP events
+    (kernel ms per step), record the step as a HIP graph and time `steps`
+    replays (barrier + sync on both sides).  Returns (graph, elapsed_max_s,
+    kernel_ms_per_step, kernels)."""
+    for _ in range(max(warmup, 1)):
+        step()
+    basis.sync()
+    basis.profile_enable(True)
+    step()
+    basis.sync()
+    kernels, kms = {}, 0.0
+    for k in kernel_names:
+        cnt, ms = basis.profile_read(k)
+        if cnt:
+            kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
+            kms += ms
+    basis.profile_enable(False)
+    with basis.capture() as g:
+        step()
+    for _ in range(max(warmup, 1)):
+        g.replay()
+    basis.sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.replay()
+    basis.sync()
+    t1 = time.perf_counter()
+    comm.barrier()
+    return g, comm.max(t1 - t0), kms, kernels
+
+
+def run_ctmul_graph(args, comm, world, rank, local_rank):
+    """The reference engine's own call shape for config 4's arithmetic:
+    mul_ciphertexts_gadget then rescale_ciphertext on `--ct-batch`
+    ciphertexts per call (1 = one ciphertext, as engine.rs:473-539 and
+    263-282 are called), through the fused C-ABI ops, the step replayed
+    from a recorded HIP graph; every GPU its own ciphertexts (replicas)."""
+    import numpy as np
+
+    import rns_ntt as rn
+
+    n = 1 << args.log_n
+    L = args.limbs
+    mod = rn.generate_primes(args.prime_bits, L, n)
+    wb = 4 if max(mod) < (1 << 31) else 8
+    Bs = rn.RnsBasis(mod, n, device=local_rank)
+    Bs1 = Bs.drop_last(1)
+    B = args.ct_batch
+    rng = np.random.default_rng(77 + rank)
+    cts = [uniform(rng, mod, B, n) for _ in range(4)]
+    key_a, key_b = uniform(rng, mod, L, n), uniform(rng, mod, L, n)
+    c = [rn.RnsPoly.from_channels(x, Bs) for x in cts]
+    key = rn.RnsGadgetKey.from_channels(key_a, key_b, Bs)
+    o0, o1, r0, r1 = rn.RnsPoly(Bs, B), rn.RnsPoly(Bs, B), rn.RnsPoly(Bs1, B), rn.RnsPoly(Bs1, B)
+    lib = rn.load()
+
+    def step():
+        rn.check(lib.rnt_ct_mul_relin(o0.handle, o1.handle, c[0].handle, c[1].handle, c[2].handle,
+                                      c[3].handle, key.a.handle, key.b.handle))
+        rn.check(lib.rnt_ct_rescale(r0.handle, r1.handle, o0.handle, o1.handle))
+
+    g, elapsed, kms, kernels = _graph_step_timing(
+        Bs, step, args.steps, args.warmup, comm,
+        ("col_fwd", "tensor_rows", "col_inv", "ks_decompose", "ks_rows", "rescale", "elementwise"))
+    ms_per_step = elapsed / args.steps * 1e3
+    value = B * args.steps * world / elapsed
+    parity_ok = None
+    if rank == 0:
+        orc = oracle()
+        ob = orc.Basis(mod, n)
+        parity_ok = True
+        for pi in sorted({0, B - 1}):
+            w0, w1 = orc.mul_ciphertexts_gadget(ob, cts[0][pi], cts[1][pi], cts[2][pi], cts[3][pi], key_a, key_b,
+                                                threads=usable_threads())
+            parity_ok &= bool(np.array_equal(r0.channels_of(pi)[0], orc.rescale(ob, w0))
+                              and np.array_equal(r1.channels_of(pi)[0], orc.rescale(ob, w1)))
+    log_c = args.log_n - max(args.log_n // 2, 4)
+    roof = {"bound": "valu", "kernel": "ks_rows", "unit": "butterflies/s", "peak": VALU_PEAK_BFLY,
+            "achieved": None, "frac": None, "traffic": None, "kernels": kernels}
+    if "ks_rows" in kernels:
+        bfly = B * (L * L + 2 * L) * (n // 2) * log_c
+        ach = bfly / (kernels["ks_rows"]["total_ms"] * 1e-3)
+        roof.update(achieved=ach, frac=ach / VALU_PEAK_BFLY, bfly_per_launch=bfly / kernels["ks_rows"]["launches"])
+    return {
+        "metric": CT_METRIC,
+        "value": value,
+        "unit": "ct-muls/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32" if wb == 4 else "u64",
+        "data": "synthetic (seeded uniform residues and key)",
+        "config": {
+            "workload": f"engine call shape: mul_ciphertexts_gadget + rescale_ciphertext of {B} ciphertext(s) per "
+                        f"call, N=2^{args.log_n}, L={L} x {args.prime_bits}-bit primes, replayed HIP graph",
+            "ct_pairs_per_gpu_per_step": B,
+            "parallelism": f"replicas x{world} (each GPU its own ciphertexts)",
+            "parity_spot_check": parity_ok,
+            "kernel_ms_per_step": kms,
+            "device_busy": kms / ms_per_step,
+        },
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+
+
 def run_ctmul(args, comm, world, rank, local_rank):
     """BASELINE config 4: ct x ct + gadget relin + rescale, limb-sharded."""
+    if args.graph:
+        return run_ctmul_graph(args, comm, world, rank, local_rank)
     import numpy as np
     import torch
 
@@ -464,7 +583,8 @@ def run_ctmul(args, comm, world, rank, local_rank):
 
     n = 1 << args.log_n
     L = args.limbs
-    mod = rn.generate_primes(31, L, n)
+    mod = rn.generate_primes(args.prime_bits, L, n)
+    wb = 4 if max(mod) < (1 << 31) else 8
     torch.cuda.set_device(local_rank)
     # --shard limb (default): the north star's limb shard with RCCL joins;
     # --shard batch: every rank runs the whole pipeline on its own
@@ -488,10 +608,12 @@ def run_ctmul(args, comm, world, rank, local_rank):
     c = [pipe.upload(x) for x in cts]
     key = pipe.upload_key(key_a, key_b)
     state0 = (pipe.basis, pipe.moduli, list(pipe.counts), pipe.limbs, pipe.owner_last)
-    # shared stream: measured at N=1 only (RCCL joins on an external stream
-    # are not yet run on a multi-GPU box), so it is the N=1 default;
-    # RNT_SHARED_STREAM=0/1 forces it off/on (A/B)
-    shared = os.environ.get("RNT_SHARED_STREAM", "1" if world == 1 else "0") != "0"
+    # shared stream (the default at every N): torch's ops and the RCCL joins
+    # are queued against the library's own HIP stream, so the pipeline runs
+    # without host syncs and each chunk's all-gather overlaps the compute of
+    # its neighbours (LimbShardedPipeline); RNT_SHARED_STREAM=0 restores
+    # torch's stream and the per-op host syncs (A/B)
+    shared = os.environ.get("RNT_SHARED_STREAM", "1") != "0"
     lib_stream = pipe.backend.shared_stream(pipe.basis) if shared else torch.cuda.current_stream()
 
     def step():
@@ -526,18 +648,28 @@ def run_ctmul(args, comm, world, rank, local_rank):
     parity_ok = None
     cpu = None
     Lr = state0[2][0 if batch_shard else rank]  # this rank's target limbs
-    if rank == 0 and (world == 1 or batch_shard):
+    # sampled parity of the timed output: the first pair, the first pair of
+    # the second pipeline chunk and the batch's last pair.  Limb-sharded:
+    # every rank sends its limbs of those pairs (after the rescale) to rank
+    # 0 over the gloo control plane, which assembles the full ciphertexts.
+    check_pairs = sorted({0, min(pipe.chunk, B - 1), B - 1})
+    mine = {pi: pipe.download(r[0], first=pi, count=1)[0] for pi in check_pairs}
+    if world > 1 and not batch_shard:
+        parts = comm.gather((rank, pipe.limbs.start, mine))
+    else:
+        parts = [(0, 0, mine)]
+    if rank == 0:
         orc = oracle()
         ob = orc.Basis(mod, n)
         threads = usable_threads()
-        got = pipe.download(r[0])
-        # pair 0 and the batch's last pair (the last key-switch chunk)
+        parts = sorted(parts, key=lambda t: t[1])  # by first limb
         parity_ok = True
-        for pi in sorted({0, B - 1}):
+        for pi in check_pairs:
+            got = np.concatenate([pr[2][pi] for pr in parts], axis=0)  # [L-1][N]
             u = pi % uniq
             o0, _ = orc.mul_ciphertexts_gadget(ob, cts[0][u], cts[1][u], cts[2][u], cts[3][u], key_a, key_b,
                                                threads=threads)
-            parity_ok &= bool(np.array_equal(got[pi], orc.rescale(ob, o0)))
+            parity_ok &= bool(np.array_equal(got, orc.rescale(ob, o0)))
         if not args.no_cpu_baseline and world == 1:
             def t_pair(th):
                 t = time.perf_counter()
@@ -580,16 +712,18 @@ def run_ctmul(args, comm, world, rank, local_rank):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32",
+        "dtype": "u32" if wb == 4 else "u64",
         "data": "synthetic (seeded uniform residues and key)",
         "config": {
-            "workload": f"ct x ct + gadget relin + rescale, N=2^{args.log_n}, L={L} x 31-bit primes",
+            "workload": f"ct x ct + gadget relin + rescale, N=2^{args.log_n}, L={L} x {args.prime_bits}-bit primes",
             "ct_pairs_per_gpu_per_step": args.ct_batch,
             "global_batch": B_global,
             "parallelism": (f"batch-sharded x{world}: no collective, full key per GPU" if batch_shard else
                             f"limb-sharded x{world}: RCCL all-gather of d2, broadcast of q_L limb"),
             "parity_spot_check": parity_ok,
-            "parity_pairs": sorted({0, B - 1}),
+            "parity_pairs": check_pairs,
+            "pipeline_chunk": pipe.chunk,
+            "shared_stream": shared,
         },
         "roofline": roof,
         "cpu_baseline": cpu,
@@ -618,7 +752,8 @@ def run_rotate(args, comm, world, rank, local_rank):
     log_n = 17 if args.log_n == 16 else args.log_n
     L = 32 if args.limbs == 16 else args.limbs
     n = 1 << log_n
-    mod = rn.generate_primes(31, L, n)
+    mod = rn.generate_primes(args.prime_bits, L, n)
+    wb = 4 if max(mod) < (1 << 31) else 8
     if world > 1 and args.shard == "limb":
         return run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod)
     Bs = rn.RnsBasis(mod, n, device=local_rank)
@@ -648,24 +783,37 @@ def run_rotate(args, comm, world, rank, local_rank):
             rn.check(lib.rnt_ct_rotate(out0.handle, out1.handle, c0.handle, c1.handle, k,
                                        key.a.handle, key.b.handle))
 
-    for _ in range(args.warmup):
-        step()
-    Bs.sync()
-    comm.barrier()
-    Bs.profile_enable(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    Bs.sync()
-    t1 = time.perf_counter()
-    comm.barrier()
-    elapsed = comm.max(t1 - t0)
-    kernels = {}
-    for k in ("ks_decompose", "ks_rows", "col_inv", "automorphism", "col_fwd", "row_fwd"):
-        cnt, ms = Bs.profile_read(k)
-        if cnt:
-            kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
-    Bs.profile_enable(False)
+    rot_kernels = ("ks_decompose", "ks_rows", "col_inv", "automorphism", "col_fwd", "row_fwd")
+    graph_info = None
+    if args.graph:
+        # the reference's call shape replayed: the whole sweep step recorded
+        # once as a HIP graph (rnt_capture_begin), kernels timed eagerly
+        g, elapsed, kms, kernels = _graph_step_timing(Bs, step, args.steps, args.warmup, comm, rot_kernels)
+        graph_info = {"kernel_ms_per_step": kms, "device_busy": kms / (elapsed / args.steps * 1e3)}
+        for kv in kernels.values():  # one eager step profiled: scale to the timed steps
+            kv["launches"] *= args.steps
+            kv["total_ms"] *= args.steps
+    else:
+        for _ in range(args.warmup):
+            step()
+        Bs.sync()
+        comm.barrier()
+        Bs.profile_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        Bs.sync()
+        t1 = time.perf_counter()
+        comm.barrier()
+        elapsed = comm.max(t1 - t0)
+        kernels = {}
+        for k in rot_kernels:
+            cnt, ms = Bs.profile_read(k)
+            if cnt:
+                kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
+        Bs.profile_enable(False)
+        kms = sum(kv["total_ms"] for kv in kernels.values()) / args.steps
+        graph_info = {"kernel_ms_per_step": kms, "device_busy": kms / (elapsed / args.steps * 1e3)}
     rots = B * len(offsets) * args.steps * world
     value = rots / elapsed
     log_c = log_n - max(log_n // 2, 4)
@@ -720,16 +868,18 @@ def run_rotate(args, comm, world, rank, local_rank):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32",
+        "dtype": "u32" if wb == 4 else "u64",
         "data": ("synthetic (seeded uniform residues; a distinct device-sampled gadget key per offset)"
                  if per_offset else "synthetic (seeded uniform residues; one device-sampled key reused for every offset)"),
         "config": {
             "workload": f"rotate_ciphertext sweep over {len(offsets)} "
                         f"{'power-of-two' if args.rot_offsets == 'pow2' else 'slot'} offsets, "
-                        f"N=2^{log_n}, L={L} x 31-bit primes, {B} ciphertexts",
+                        f"N=2^{log_n}, L={L} x {args.prime_bits}-bit primes, {B} ciphertexts",
             "keys": len(keys),
             "parallelism": f"replicas x{world} (each GPU its own ciphertexts)",
             "parity_spot_check": parity_ok,
+            "replayed_graph": bool(args.graph),
+            **graph_info,
         },
         "roofline": roof,
         "cpu_baseline": cpu,
@@ -992,7 +1142,9 @@ def run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod):
     """Config 5 limb-sharded: each rank owns L/world limbs of a
     global batch of rot_batch * world ciphertexts and a [L][L_r][N] slice of
     the rotation key; per offset: limb-local slot rotation, RCCL all-gather
-    of sigma(c1), key-switch of the local target limbs."""
+    of sigma(c1) per pipeline chunk, key-switch of the local target limbs,
+    all queued on the library's stream (shared stream; RNT_SHARED_STREAM=0:
+    torch's stream with per-op host syncs)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -1006,14 +1158,20 @@ def run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod):
     rng = np.random.default_rng(5)
     uniq = min(2, B)
     reps = (B + uniq - 1) // uniq
-    c0 = pipe.upload(np.tile(uniform(rng, mod, uniq, n), (reps, 1, 1))[:B])
-    c1 = pipe.upload(np.tile(uniform(rng, mod, uniq, n), (reps, 1, 1))[:B])
-    key = pipe.upload_key(uniform(rng, mod, L, n), uniform(rng, mod, L, n))
+    c0_u, c1_u = uniform(rng, mod, uniq, n), uniform(rng, mod, uniq, n)
+    c0 = pipe.upload(np.tile(c0_u, (reps, 1, 1))[:B])
+    c1 = pipe.upload(np.tile(c1_u, (reps, 1, 1))[:B])
+    ka, kb = uniform(rng, mod, L, n), uniform(rng, mod, L, n)
+    key = pipe.upload_key(ka, kb)
     offsets = [1 << e for e in range(log_n - 1)]
+    shared = os.environ.get("RNT_SHARED_STREAM", "1") != "0"
+    lib_stream = pipe.backend.shared_stream(pipe.basis) if shared else torch.cuda.current_stream()
 
     def step():
-        for k in offsets:
-            pipe.rotate(c0, c1, k, key)
+        with torch.cuda.stream(lib_stream):
+            for k in offsets:
+                out = pipe.rotate(c0, c1, k, key)
+        return out
 
     for _ in range(args.warmup):
         step()
@@ -1021,13 +1179,31 @@ def run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod):
     comm.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        out = step()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     comm.barrier()
     elapsed = comm.max(t1 - t0)
     value = B * len(offsets) * args.steps / elapsed
     bfly = (L * L + 2 * L) * (n // 2) * log_n
+    # sampled parity of the last offset's output: ciphertext 0 and the last
+    # one, every rank's limbs gathered to rank 0 over the gloo control plane
+    check = sorted({0, B - 1})
+    mine = {p: (pipe.download(out[0], first=p, count=1)[0], pipe.download(out[1], first=p, count=1)[0])
+            for p in check}
+    parts = comm.gather((pipe.limbs.start, mine))
+    parity_ok = None
+    if rank == 0:
+        orc = oracle()
+        ob = orc.Basis(mod, n)
+        parts = sorted(parts, key=lambda t: t[0])
+        parity_ok = True
+        for p in check:
+            g0 = np.concatenate([pr[1][p][0] for pr in parts], axis=0)
+            g1 = np.concatenate([pr[1][p][1] for pr in parts], axis=0)
+            w0, w1 = orc.rotate_ciphertext(ob, c0_u[p % uniq], c1_u[p % uniq], offsets[-1], ka, kb,
+                                           threads=usable_threads())
+            parity_ok &= bool(np.array_equal(g0, w0) and np.array_equal(g1, w1))
     return {
         "metric": ROT_METRIC,
         "value": value,
@@ -1039,12 +1215,15 @@ def run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32",
+        "dtype": "u32" if max(mod) < (1 << 31) else "u64",
         "data": "synthetic (seeded uniform residues and key; one key reused for every offset)",
         "config": {
             "workload": f"rotate_ciphertext sweep over {len(offsets)} power-of-two offsets, "
                         f"N=2^{log_n}, L={L} x 31-bit primes, {B} ciphertexts (global)",
-            "parallelism": f"limb-sharded x{world}: RCCL all-gather of sigma(c1) per offset",
+            "parallelism": f"limb-sharded x{world}: RCCL all-gather of sigma(c1) per offset and chunk",
+            "parity_spot_check": parity_ok,
+            "parity_ciphertexts": check,
+            "shared_stream": shared,
         },
         # whole key-switch butterflies per GPU (no per-kernel events on this path)
         "roofline": {"bound": "valu", "kernel": "whole key-switch", "unit": "butterflies/s",

@@ -136,6 +136,24 @@ int rnt_ctx_stream(const rnt_ctx* ctx, void** stream);
 int rnt_ctx_set_stream(const rnt_ctx* ctx, void* stream);
 int rnt_sync(const rnt_ctx* ctx);
 
+/* ---- captured op sequences (hipGraph) --------------------------------- */
+/* The reference engine calls one ciphertext at a time
+ * (mul_ciphertexts_gadget engine.rs:473-539, rotate_ciphertext :412-463), so
+ * a fixed per-ciphertext op sequence is launch-bound.  rnt_capture_begin
+ * starts recording every op the calling thread then queues on ctx's stream
+ * (any context sharing its tables) into a graph instead of running it;
+ * rnt_capture_end instantiates it; rnt_graph_launch replays it, with the
+ * same buffers, on the context's current stream.  Record only device ops
+ * (no upload, download, rnt_sync or allocation that misses the block cache)
+ * and run the sequence once un-recorded first, so its workspaces are cached;
+ * the graph keeps the workspace blocks its ops took until
+ * rnt_graph_destroy.  Buffers the graph reads and writes must outlive it. */
+typedef struct rnt_graph rnt_graph;
+int rnt_capture_begin(const rnt_ctx* ctx);
+int rnt_capture_end(const rnt_ctx* ctx, rnt_graph** out);
+int rnt_graph_launch(rnt_graph* graph);
+int rnt_graph_destroy(rnt_graph* graph);
+
 /* ---- buffers == batches of RnsPoly ------------------------------------ */
 /* Allocates device storage for n_polys polynomials over ctx's basis, all
  * zero, coefficient domain (RnsPoly::zero, poly.rs:36-43).  The zeroing is

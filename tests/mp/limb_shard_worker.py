@@ -23,6 +23,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--inputs", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--shared", action="store_true",
+                    help="queue torch's ops and the joins on the library's stream (GpuBackend.shared_stream)")
+    ap.add_argument("--chunk", type=int, default=None)
     args = ap.parse_args()
 
     import rns_ntt  # noqa: F401  (loads librnsntt before torch initialises HIP)
@@ -37,7 +40,12 @@ def main():
     z = np.load(args.inputs)
     mod = [int(q) for q in z["moduli"]]
     n = int(z["n"])
-    pipe = LimbShardedPipeline(mod, n, TorchDistComm(), GpuBackend(0))
+    import contextlib
+
+    be = GpuBackend(0)
+    pipe = LimbShardedPipeline(mod, n, TorchDistComm(), be, chunk=args.chunk)
+    scope = torch.cuda.stream(be.shared_stream(pipe.basis)) if args.shared else contextlib.nullcontext()
+    scope.__enter__()
     c = [pipe.upload(z[k]) for k in ("c0", "c1", "c0p", "c1p")]
     rlk = pipe.upload_key(z["ka"], z["kb"])
     rotk = pipe.upload_key(z["ra"], z["rb"])
@@ -51,6 +59,8 @@ def main():
     s0, s1 = pipe.rescale(m0, m1)
     res["res0"], res["res1"] = pipe.download(s0), pipe.download(s1)
     res["res_limbs"] = np.array([pipe.limbs.start, pipe.limbs.stop])
+    scope.__exit__(None, None, None)
+    torch.cuda.synchronize()
     np.savez(f"{args.out}.rank{rank}.npz", **res)
     dist.barrier()
     dist.destroy_process_group()

@@ -144,7 +144,7 @@ def test_error_detail_through_the_abi():
 
 _C_SCALARS = {"int": "c_int", "uint64_t": "u64", "int64_t": "i64", "uint32_t": "u32",
               "int32_t": "i32", "size_t": "usize", "double": "f64", "char": "c_char",
-              "void": "c_void", "rnt_ctx": "rnt_ctx", "rnt_buf": "rnt_buf"}
+              "void": "c_void", "rnt_ctx": "rnt_ctx", "rnt_buf": "rnt_buf", "rnt_graph": "rnt_graph"}
 
 
 def _c_type_to_rust(ctype: str) -> str:

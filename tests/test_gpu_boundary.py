@@ -220,3 +220,71 @@ def test_ops_follow_a_caller_stream(gpu):
     assert Bd.stream() == own
     # the own stream is ordered after the caller's: a download sees the product
     assert np.array_equal(out.channels(), want)
+
+
+def _reupload(rn, buf, channels):
+    """from_channels into an existing buffer (same device memory)."""
+    import ctypes
+
+    ch = np.ascontiguousarray(channels, dtype=np.uint64)
+    if ch.ndim == 2:
+        ch = ch[None]
+    rn.check(rn.load().rnt_upload(buf.handle, ch.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                  ch.shape[0], ch.shape[1], 0))
+
+
+def test_graph_capture_replays_the_engine_call_shape(gpu):
+    """rnt_capture_begin/end + rnt_graph_launch: one ciphertext's
+    mul_ciphertexts_gadget + rescale_ciphertext (engine.rs:473-539,
+    263-282) and a rotate_ciphertext (:412-463), recorded once and replayed
+    after the input buffers were overwritten in place: every replay
+    recomputes from the buffers' current contents, bit-exact against the
+    oracle; recording does not run the ops."""
+    rn = gpu
+    n, L = 1 << 12, 4
+    mods = rn.generate_primes(31, L, n)
+    Bd, Bo = rn.RnsBasis(mods, n), orc.Basis(mods, n)
+    rng = np.random.default_rng(77)
+    x = [_rand(rng, mods, n) for _ in range(4)]
+    ka, kb = _rand(rng, mods, n, L), _rand(rng, mods, n, L)
+    ra, rb = _rand(rng, mods, n, L), _rand(rng, mods, n, L)
+    key = rn.RnsGadgetKey.from_channels(ka, kb, Bd)
+    rkey = rn.RnsGadgetKey.from_channels(ra, rb, Bd)
+    c = [rn.RnsPoly.from_channels(v, Bd) for v in x]
+    lib = rn.load()
+    Bd1 = Bd.drop_last(1)
+    o0, o1, r0, r1 = rn.RnsPoly(Bd), rn.RnsPoly(Bd), rn.RnsPoly(Bd1), rn.RnsPoly(Bd1)
+    t0, t1 = rn.RnsPoly(Bd), rn.RnsPoly(Bd)
+    k = -3
+
+    def seq():
+        rn.check(lib.rnt_ct_mul_relin(o0.handle, o1.handle, c[0].handle, c[1].handle, c[2].handle,
+                                      c[3].handle, key.a.handle, key.b.handle))
+        rn.check(lib.rnt_ct_rescale(r0.handle, r1.handle, o0.handle, o1.handle))
+        rn.check(lib.rnt_ct_rotate(t0.handle, t1.handle, c[0].handle, c[1].handle, k, rkey.a.handle,
+                                   rkey.b.handle))
+
+    seq()  # warm: the workspaces are cached before recording
+    Bd.sync()
+    for p in (r0, r1, t0, t1):
+        _reupload(rn, p, np.zeros((p.basis.channel_count(), n), np.uint64))
+    with Bd.capture() as g:
+        seq()
+    Bd.sync()
+    assert not r0.channels().any() and not t1.channels().any()  # recorded, not run
+    for it in range(2):
+        x = [_rand(rng, mods, n) for _ in range(4)]
+        for buf, v in zip(c, x):
+            _reupload(rn, buf, v)
+        g.replay()
+        g.replay()
+        Bd.sync()
+        w0, w1 = orc.mul_ciphertexts_gadget(Bo, x[0], x[1], x[2], x[3], ka, kb)
+        assert np.array_equal(r0.channels(), orc.rescale(Bo, w0)), it
+        assert np.array_equal(r1.channels(), orc.rescale(Bo, w1)), it
+        v0, v1 = orc.rotate_ciphertext(Bo, x[0], x[1], k, ra, rb)
+        assert np.array_equal(t0.channels(), v0) and np.array_equal(t1.channels(), v1), it
+    del g  # returns the graph's workspace blocks to the cache
+    seq()
+    Bd.sync()
+    assert np.array_equal(t0.channels(), v0)

@@ -25,9 +25,13 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_two_process_limb_sharded_pipeline(gpu, tmp_path):
+@pytest.mark.parametrize("shared", [False, True], ids=["torch-stream", "shared-stream"])
+def test_two_process_limb_sharded_pipeline(gpu, tmp_path, shared):
+    """shared: each rank queues torch's ops and the (async, per-chunk) joins
+    on its library context's stream -- the bench's default at every N -- with
+    B = 3 in pipeline chunks of 2."""
     rn = gpu
-    n, L, B, k = 1 << 12, 5, 2, -3
+    n, L, B, k = 1 << 12, 5, 3, -3
     mod = rn.generate_primes(31, L, n)
     rng = np.random.default_rng(2024)
     u = lambda b=None: orc.uniform_poly(mod, n, rng, batch=b)  # noqa: E731
@@ -38,8 +42,9 @@ def test_two_process_limb_sharded_pipeline(gpu, tmp_path):
     out = str(tmp_path / "res")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", "29611",
-           os.path.join(REPO, "tests", "mp", "limb_shard_worker.py"), "--inputs", inp, "--out", out]
+           "--master-addr", "127.0.0.1", "--master-port", str(29611 + int(shared)),
+           os.path.join(REPO, "tests", "mp", "limb_shard_worker.py"), "--inputs", inp, "--out", out,
+           "--chunk", "2"] + (["--shared"] if shared else [])
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     ranks = [np.load(f"{out}.rank{r}.npz") for r in range(2)]

@@ -476,7 +476,7 @@ def test_crt_centered_large_q(gpu, log_n, L):
     B = rn.RnsBasis(mods, n)
     rng = np.random.default_rng(L)
     a = orc.uniform_poly(mods, n, rng, batch=1)
-    p = rn.RnsPoly.from_channels(a, B)
+    p = rn.RnsPoly.from_channels(a[0], B)  # the reference's single polynomial: [N] views
     exact = p.to_coeffs_exact()
     for i in rng.integers(0, n, size=64):
         assert exact[i] == _centered_crt(mods, a[0, :, i]), i

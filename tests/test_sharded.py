@@ -58,7 +58,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _gloo_worker(rank, world, port, mods, n, B, seed, q):
+def _gloo_worker(rank, world, port, mods, n, B, seed, q, chunk=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -68,7 +68,7 @@ def _gloo_worker(rank, world, port, mods, n, B, seed, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cts, key_a, key_b = _inputs(mods, n, B, seed)
-        pipe = LimbShardedPipeline(mods, n, TorchDistComm(), OracleBackend())
+        pipe = LimbShardedPipeline(mods, n, TorchDistComm(), OracleBackend(), chunk=chunk)
         limbs = (pipe.limbs.start, pipe.limbs.stop)
         relin, resc = _run_rank(pipe, cts, key_a, key_b)
         q.put((rank, limbs, relin, resc))
@@ -104,14 +104,18 @@ def _assemble(results):
     return relin0, relin1, resc0, resc1
 
 
-@pytest.mark.parametrize("world,L", [(2, 4), (3, 7)])
-def test_limb_sharded_gloo_matches_unsharded(world, L):
-    n, B, seed = 32, 2, 5
+@pytest.mark.parametrize("world,L,B,chunk", [(2, 4, 2, None), (3, 7, 3, 2), (2, 5, 3, 1)])
+def test_limb_sharded_gloo_matches_unsharded(world, L, B, chunk):
+    """chunk: ciphertexts per pipeline chunk (each chunk's joins start as
+    soon as its tensor product exists); 2 and 1 split B = 3 into uneven
+    chunks."""
+    n, seed = 32, 5
     mods = orc.generate_primes(31, L, n)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, mods, n, B, seed, q)) for r in range(world)]
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, mods, n, B, seed, q, chunk))
+             for r in range(world)]
     for p in procs:
         p.start()
     results = _collect(q, procs, world)
@@ -156,7 +160,7 @@ def _run_rank_rotate(pipe, c0, c1, key_a, key_b):
     return outs
 
 
-def _gloo_rot_worker(rank, world, port, mods, n, B, seed, q):
+def _gloo_rot_worker(rank, world, port, mods, n, B, seed, q, chunk=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -166,20 +170,20 @@ def _gloo_rot_worker(rank, world, port, mods, n, B, seed, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         c0, c1, key_a, key_b = _rot_inputs(mods, n, B, seed)
-        pipe = LimbShardedPipeline(mods, n, TorchDistComm(), OracleBackend())
+        pipe = LimbShardedPipeline(mods, n, TorchDistComm(), OracleBackend(), chunk=chunk)
         q.put((rank, _run_rank_rotate(pipe, c0, c1, key_a, key_b)))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,L", [(2, 4), (3, 5)])
-def test_limb_sharded_rotation_gloo_matches_unsharded(world, L):
-    n, B, seed = 32, 2, 21
+@pytest.mark.parametrize("world,L,B,chunk", [(2, 4, 2, None), (3, 5, 3, 2)])
+def test_limb_sharded_rotation_gloo_matches_unsharded(world, L, B, chunk):
+    n, seed = 32, 21
     mods = orc.generate_primes(31, L, n)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gloo_rot_worker, args=(r, world, port, mods, n, B, seed, q))
+    procs = [ctx.Process(target=_gloo_rot_worker, args=(r, world, port, mods, n, B, seed, q, chunk))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -69,6 +69,17 @@ int hip_fail(hipError_t e, const char* where) {
 
 inline size_t word_bytes(const rnt::Tables* t) { return t->wide ? 8 : 4; }
 
+// An op sequence being recorded into a hipGraph on this thread
+// (rnt_capture_begin .. rnt_capture_end): workspace blocks the captured ops
+// take stay with the graph, whose replays reuse those exact addresses, and
+// nothing that would synchronise the stream runs while recording.
+struct Capture {
+  std::vector<std::pair<void*, size_t>> owned;
+  hipStream_t stream = nullptr;
+  int device = 0;
+};
+thread_local Capture* g_capture = nullptr;
+
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
@@ -89,7 +100,7 @@ hipEvent_t prof_event(rnt::Prof* p) {
 template <class F>
 hipError_t prof_launch(const rnt::Tables* t, hipStream_t s, int id, F&& f) {
   rnt::Prof* p = t->prof;
-  if (p == nullptr || !p->on) return f();
+  if (p == nullptr || !p->on || g_capture != nullptr) return f();
   std::lock_guard<std::mutex> g(p->mu);
   hipEvent_t a = prof_event(p), b = prof_event(p);
   if (a) (void)hipEventRecord(a, s);
@@ -198,8 +209,11 @@ static void* pool_take(int device, size_t bytes, hipStream_t s, size_t* got) {
     g_pool.erase(g_pool.begin() + (long)best);
   }
   if (w.ev) {
-    // same stream: stream order already covers the last use
-    if (w.s != s && hipStreamWaitEvent(s, w.ev, 0) != hipSuccess) (void)hipEventSynchronize(w.ev);
+    // same stream: stream order already covers the last use; while a graph
+    // is being recorded the wait is a host wait (a recording stream cannot
+    // wait on an event from outside the recording)
+    if (w.s != s && (g_capture != nullptr || hipStreamWaitEvent(s, w.ev, 0) != hipSuccess))
+      (void)hipEventSynchronize(w.ev);
     std::lock_guard<std::mutex> lk(g_pool_mu);
     g_free_events.push_back(w.ev);
   }
@@ -211,6 +225,10 @@ static void* pool_take(int device, size_t bytes, hipStream_t s, size_t* got) {
 // oldest idle blocks of the device leave it while it is over its cap.
 static void pool_give(int device, void* p, size_t bytes, hipStream_t s) {
   if (!p) return;
+  if (g_capture != nullptr) {  // the recorded graph keeps using the block
+    g_capture->owned.push_back({p, bytes});
+    return;
+  }
   hipEvent_t ev = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
@@ -307,6 +325,32 @@ int ensure_ws(rnt_buf* b, size_t bytes) {
   b->ws_bytes = got;
   return RNT_OK;
 }
+
+// A call-scoped device workspace from the block cache: taken when an op
+// starts and handed back when the call returns, behind an event on the op's
+// stream (no host wait), so the next op -- on any buffer -- reuses the same
+// block.  Key-switch scratch (gigabytes per chunk) lives here rather than
+// with an output buffer: a caller that makes a fresh output per chunk (the
+// limb-sharded pipeline) would otherwise hold one scratch per live output.
+struct CallWs {
+  int dev;
+  hipStream_t s;
+  void* p = nullptr;
+  size_t bytes = 0;
+  explicit CallWs(const rnt_buf* b) : dev(b->ctx->t->device), s(b->ctx->t->stream) {}
+  CallWs(const CallWs&) = delete;
+  CallWs& operator=(const CallWs&) = delete;
+  int get(size_t need) {
+    size_t got = 0;
+    if (hipError_t e = pool_malloc(dev, need, s, &p, &got); e != hipSuccess)
+      return hip_fail(e, "hipMalloc(workspace)");
+    bytes = got;
+    return RNT_OK;
+  }
+  ~CallWs() {
+    if (p) pool_give(dev, p, bytes, s);
+  }
+};
 
 int ensure_stage(rnt_buf* b, size_t bytes) {
   if (b->stage_bytes >= bytes) return RNT_OK;
@@ -696,6 +740,96 @@ extern "C" int rnt_ctx_set_stream(const rnt_ctx* ctx, void* stream) {
   (void)hipEventDestroy(ev);  // released once it completes
   if (e != hipSuccess) return hip_fail(e, "rnt_ctx_set_stream");
   t->stream = next;
+  return RNT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// captured op sequences (hipGraph)
+// ---------------------------------------------------------------------------
+struct rnt_graph {
+  std::shared_ptr<rnt::Tables> t;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  std::vector<std::pair<void*, size_t>> owned;
+};
+
+extern "C" int rnt_capture_begin(const rnt_ctx* ctx) {
+  if (!ctx) return fail(RNT_ERR_BAD_ARGUMENT, "null ctx");
+  if (g_capture != nullptr) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_capture_begin: already recording on this thread");
+  if (int rc = set_device(ctx)) return rc;
+  Capture* c = nullptr;
+  try {
+    c = new Capture;
+  } catch (...) {
+    return fail(RNT_ERR_OUT_OF_MEMORY, "host allocation failed");
+  }
+  c->stream = ctx->t->stream;
+  c->device = ctx->t->device;
+  // relaxed: the ops' own host-side calls (none synchronising once warm)
+  // are not checked against the recording
+  if (hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed); e != hipSuccess) {
+    delete c;
+    return hip_fail(e, "hipStreamBeginCapture");
+  }
+  g_capture = c;
+  return RNT_OK;
+}
+
+extern "C" int rnt_capture_end(const rnt_ctx* ctx, rnt_graph** out) {
+  if (!ctx || !out) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  *out = nullptr;
+  Capture* c = g_capture;
+  if (c == nullptr || c->stream != ctx->t->stream)
+    return fail(RNT_ERR_BAD_ARGUMENT, "rnt_capture_end: no recording on this context's stream");
+  g_capture = nullptr;
+  hipGraph_t g = nullptr;
+  hipError_t e = hipStreamEndCapture(c->stream, &g);
+  rnt_graph* r = nullptr;
+  if (e == hipSuccess) {
+    try {
+      r = new rnt_graph;
+    } catch (...) {
+      e = hipErrorOutOfMemory;
+    }
+  }
+  if (r != nullptr) {
+    r->t = ctx->t;
+    r->graph = g;
+    r->owned = std::move(c->owned);
+    e = hipGraphInstantiate(&r->exec, g, nullptr, nullptr, 0);
+  }
+  if (e != hipSuccess) {
+    const int dev = c->device;
+    const hipStream_t st = c->stream;
+    std::vector<std::pair<void*, size_t>> owned = r ? std::move(r->owned) : std::move(c->owned);
+    if (g) (void)hipGraphDestroy(g);
+    delete r;
+    delete c;
+    for (auto& b : owned) pool_give(dev, b.first, b.second, st);
+    return hip_fail(e, "rnt_capture_end");
+  }
+  delete c;
+  *out = r;
+  return RNT_OK;
+}
+
+extern "C" int rnt_graph_launch(rnt_graph* g) {
+  if (!g) return fail(RNT_ERR_BAD_ARGUMENT, "null graph");
+  if (g_capture != nullptr) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_graph_launch while recording");
+  HIP_TRY(hipSetDevice(g->t->device), "hipSetDevice");
+  HIP_TRY(hipGraphLaunch(g->exec, g->t->stream), "hipGraphLaunch");
+  return RNT_OK;
+}
+
+extern "C" int rnt_graph_destroy(rnt_graph* g) {
+  if (!g) return RNT_OK;
+  (void)hipSetDevice(g->t->device);
+  // a replay may still be running: the blocks go back behind an event on
+  // the stream the replays were queued on
+  for (auto& b : g->owned) pool_give(g->t->device, b.first, b.second, g->t->stream);
+  if (g->exec) (void)hipGraphExecDestroy(g->exec);
+  if (g->graph) (void)hipGraphDestroy(g->graph);
+  delete g;
   return RNT_OK;
 }
 
@@ -1542,10 +1676,11 @@ extern "C" int rnt_keyswitch(rnt_buf* acc0, rnt_buf* acc1, const rnt_buf* d, con
   rnt::Launch k = launch_for(d);
   const size_t L = k.L, n = k.t->n, wb = word_bytes(k.t);
   const size_t bc = ks_chunk(k.t, L, d->n_polys);
-  if (int rc = ensure_ws(acc0, (L * L + 2 * L) * bc * n * wb)) return rc;
+  CallWs ws(acc0);
+  if (int rc = ws.get((L * L + 2 * L) * bc * n * wb)) return rc;
   for (size_t p0 = 0; p0 < d->n_polys; p0 += bc) {
     const size_t c = std::min(bc, d->n_polys - p0);
-    if (int rc = ks_chunk_run(k, acc0->ws, d, p0, c, key_a, key_b, acc0->data, acc1->data,
+    if (int rc = ks_chunk_run(k, ws.p, d, p0, c, key_a, key_b, acc0->data, acc1->data,
                               limb_stride(d), nullptr, nullptr, 0, nullptr, 0))
       return rc;
   }
@@ -1584,14 +1719,15 @@ extern "C" int rnt_keyswitch_ext(rnt_buf* acc0, rnt_buf* acc1, const void* src, 
   // polys per chunk: S is [Lt][Ls][Bc][N]
   size_t bc = std::max<size_t>(1, k.t->ks_ws_bytes / std::max<size_t>(1, Lt * Ls * n * wb));
   bc = std::min(bc, B);
-  if (int rc = ensure_ws(acc0, (Lt * Ls + 2 * Lt) * bc * n * wb)) return rc;
+  CallWs ws(acc0);
+  if (int rc = ws.get((Lt * Ls + 2 * Lt) * bc * n * wb)) return rc;
   const uint64_t src_ls = (uint64_t)B * n, full_ls = limb_stride(acc0);
   for (size_t p0 = 0; p0 < B; p0 += bc) {
     rnt::Launch kc = k;
     kc.B = std::min(bc, B - p0);
     kc.Ls = Ls;
     const uint64_t cls = (uint64_t)kc.B * n;
-    char* S = (char*)acc0->ws;
+    char* S = (char*)ws.p;
     char* U0 = S + Lt * Ls * kc.B * n * wb;
     char* U1 = U0 + Lt * kc.B * n * wb;
     const size_t off = p0 * n * wb;
@@ -1625,9 +1761,10 @@ extern "C" int rnt_ct_tensor(rnt_buf* d0, rnt_buf* d1, rnt_buf* d2, const rnt_bu
   if (int rc = set_device(c0->ctx)) return rc;
   rnt::Launch k = launch_for(c0);
   const size_t L = k.L, n = k.t->n, wb = word_bytes(k.t);
-  if (int rc = ensure_ws(d0, 4 * L * c0->n_polys * n * wb)) return rc;
+  CallWs ws(d0);
+  if (int rc = ws.get(4 * L * c0->n_polys * n * wb)) return rc;
   char* T[4];
-  for (int i = 0; i < 4; ++i) T[i] = (char*)d0->ws + i * L * c0->n_polys * n * wb;
+  for (int i = 0; i < 4; ++i) T[i] = (char*)ws.p + i * L * c0->n_polys * n * wb;
   const uint64_t ls = limb_stride(c0);
   LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, T[0], c0->data, T[1], c1->data, ls, ls), "tensor column");
   LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, T[2], c0p->data, T[3], c1p->data, ls, ls), "tensor column");
@@ -1658,8 +1795,9 @@ extern "C" int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
   // ws: T0..T3 (column outputs, chunk-local) | D0 | D1 | D2 | key-switch (S|U0|U1)
   const size_t chunk_words = L * bc * n;
   const size_t need = (7 * chunk_words + (L * L + 2 * L) * bc * n) * wb;
-  if (int rc = ensure_ws(out0, need)) return rc;
-  char* ws = (char*)out0->ws;
+  CallWs cws(out0);
+  if (int rc = cws.get(need)) return rc;
+  char* ws = (char*)cws.p;
   char* T[4];
   for (int i = 0; i < 4; ++i) T[i] = ws + i * chunk_words * wb;
   char* D0 = ws + 4 * chunk_words * wb;
@@ -1711,8 +1849,9 @@ extern "C" int rnt_ct_rotate(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, co
   const size_t bc = ks_chunk(k.t, L, B);
   const bool any_ntt = c0->in_ntt || c1->in_ntt;
   const size_t tmp_words = any_ntt ? words : 0;
-  if (int rc = ensure_ws(out0, (2 * words + tmp_words + (L * L + 2 * L) * bc * n) * wb)) return rc;
-  char* sig0 = (char*)out0->ws;
+  CallWs ws(out0);
+  if (int rc = ws.get((2 * words + tmp_words + (L * L + 2 * L) * bc * n) * wb)) return rc;
+  char* sig0 = (char*)ws.p;
   char* sig1 = sig0 + words * wb;
   char* tmp = sig1 + words * wb;
   char* KS = tmp + tmp_words * wb;

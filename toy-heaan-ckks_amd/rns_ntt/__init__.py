@@ -45,6 +45,7 @@ __all__ = [
     "CkksEncoder",
     "DeviceRng",
     "pool_trim",
+    "Graph",
 ]
 
 
@@ -203,6 +204,15 @@ class RnsBasis:
     def sync(self) -> None:
         check(load().rnt_sync(self._h))
 
+    def capture(self) -> "Graph":
+        """Record the device ops this thread queues on the basis' stream
+        inside ``with basis.capture() as g:`` into a HIP graph instead of
+        running them; ``g.replay()`` then re-runs the whole sequence (same
+        buffers) as one launch (rnt_capture_begin / rnt_graph_launch).  Run
+        the sequence once before recording it, so its workspaces are cached;
+        only device ops may be recorded (no from_channels / channels / sync)."""
+        return Graph(self)
+
     def profile_enable(self, enable: bool = True) -> None:
         """Bracket every kernel launched on this basis' stream with HIP events."""
         check(load().rnt_profile_enable(self._h, 1 if enable else 0))
@@ -232,6 +242,36 @@ class RnsBasis:
         h = getattr(self, "_h", None)
         if h is not None and h.value and _lib is not None and _lib._lib is not None:
             _lib._lib.rnt_ctx_destroy(h)
+            self._h = None
+
+
+class Graph:
+    """A recorded op sequence (see RnsBasis.capture)."""
+
+    def __init__(self, basis: "RnsBasis"):
+        self.basis = basis
+        self._h = None
+
+    def __enter__(self) -> "Graph":
+        check(load().rnt_capture_begin(self.basis.handle))
+        return self
+
+    def __exit__(self, exc_type, exc, tb) -> None:
+        h = ctypes.c_void_p()
+        rc = load().rnt_capture_end(self.basis.handle, ctypes.byref(h))
+        if exc_type is None:
+            check(rc)
+            self._h = h
+
+    def replay(self) -> None:
+        if self._h is None:
+            raise RuntimeError("graph was not recorded")
+        check(load().rnt_graph_launch(self._h))
+
+    def __del__(self, _lib=_lib):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None and _lib._lib is not None:
+            _lib._lib.rnt_graph_destroy(h)
             self._h = None
 
 

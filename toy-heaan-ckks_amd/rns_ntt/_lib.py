@@ -106,6 +106,10 @@ SIGNATURES = {
     "rnt_ctx_stream": (c_int, [_P, POINTER(_P)]),
     "rnt_ctx_set_stream": (c_int, [_P, c_void_p]),
     "rnt_sync": (c_int, [_P]),
+    "rnt_capture_begin": (c_int, [_P]),
+    "rnt_capture_end": (c_int, [_P, POINTER(_P)]),
+    "rnt_graph_launch": (c_int, [_P]),
+    "rnt_graph_destroy": (c_int, [_P]),
     "rnt_buf_alloc": (c_int, [_P, c_size_t, POINTER(_P)]),
     "rnt_buf_free": (c_int, [_P]),
     "rnt_buf_n_polys": (c_int, [_P, POINTER(c_size_t)]),

@@ -78,6 +78,16 @@ class Comm:
         self._dist.all_reduce(t, op=getattr(self._dist.ReduceOp, op))
         return float(t.item())
 
+    def gather(self, obj, dst: int = 0):
+        """Every rank's picklable `obj` as a list on rank `dst` (None
+        elsewhere); a single process gets [obj].  Control plane only (gloo):
+        used for the sampled parity checks of sharded outputs."""
+        if self._dist is None:
+            return [obj]
+        out = [None] * self.world if self.rank == dst else None
+        self._dist.gather_object(obj, out, dst=dst)
+        return out
+
     def close(self) -> None:
         if self._dist is not None and self._dist.is_initialized():
             self._dist.destroy_process_group()

@@ -40,6 +40,30 @@ from .dist import shard
 # ---------------------------------------------------------------------------
 
 
+class _Done:
+    """A join that has already completed (synchronous communicators)."""
+
+    def __init__(self, value):
+        self._v = value
+
+    def wait(self):
+        return self._v
+
+
+class _Pending:
+    """An in-flight torch.distributed collective; wait() returns its result.
+    On RCCL, wait() makes the CURRENT stream wait for the collective's stream
+    (no host wait), so the library work queued after it on that stream is
+    ordered behind the join while the host moves on."""
+
+    def __init__(self, work, finish):
+        self._work, self._finish = work, finish
+
+    def wait(self):
+        self._work.wait()
+        return self._finish()
+
+
 class TorchDistComm:
     """torch.distributed process group (nccl = RCCL on ROCm, or gloo)."""
 
@@ -53,24 +77,32 @@ class TorchDistComm:
         self._gloo = dist.get_backend(group) == "gloo"
 
     def all_gather_limbs(self, local, counts: Sequence[int]):
+        return self.all_gather_limbs_async(local, counts).wait()
+
+    def all_gather_limbs_async(self, local, counts: Sequence[int]):
+        """Start the limb all-gather of a [L_r][B][N] tensor into [L][B][N];
+        returns a handle whose wait() gives the gathered tensor."""
         import torch
 
         B, N = local.shape[1], local.shape[2]
         if not self._gloo and len(set(counts)) == 1:
             out = torch.empty((sum(counts), B, N), dtype=local.dtype, device=local.device)
-            self._dist.all_gather_into_tensor(out, local.contiguous(), group=self._group)
-            return out
-        # uneven limb counts: pad every shard to the largest, gather, trim
+            w = self._dist.all_gather_into_tensor(out, local.contiguous(), group=self._group, async_op=True)
+            return _Pending(w, lambda: out)
+        # uneven limb counts (or gloo): pad every shard to the largest, gather, trim
         m = max(counts)
         pad = torch.zeros((m, B, N), dtype=local.dtype, device=local.device)
         pad[: local.shape[0]].copy_(local)
         parts = [torch.empty((m, B, N), dtype=local.dtype, device=local.device) for _ in counts]
-        self._dist.all_gather(parts, pad, group=self._group)
-        return torch.cat([p[:c] for p, c in zip(parts, counts)], 0)
+        w = self._dist.all_gather(parts, pad, group=self._group, async_op=True)
+        return _Pending(w, lambda: torch.cat([p[:c] for p, c in zip(parts, counts)], 0))
 
     def broadcast(self, t, src: int):
-        self._dist.broadcast(t, src, group=self._group)
-        return t
+        return self.broadcast_async(t, src).wait()
+
+    def broadcast_async(self, t, src: int):
+        w = self._dist.broadcast(t, src, group=self._group, async_op=True)
+        return _Pending(w, lambda: t)
 
 
 class SingleComm:
@@ -82,8 +114,14 @@ class SingleComm:
     def all_gather_limbs(self, local, counts: Sequence[int]):
         return local
 
+    def all_gather_limbs_async(self, local, counts: Sequence[int]):
+        return _Done(local)
+
     def broadcast(self, t, src: int):
         return t
+
+    def broadcast_async(self, t, src: int):
+        return _Done(t)
 
 
 class ThreadComm:
@@ -116,6 +154,9 @@ class _ThreadRank:
         c._bar.wait()
         return out
 
+    def all_gather_limbs_async(self, local, counts: Sequence[int]):
+        return _Done(self.all_gather_limbs(local, counts))
+
     def broadcast(self, t, src: int):
         c = self._c
         if self.rank == src:
@@ -127,6 +168,9 @@ class _ThreadRank:
             _stream_done(t)
         c._bar.wait()
         return t
+
+    def broadcast_async(self, t, src: int):
+        return _Done(self.broadcast(t, src))
 
 
 def _stream_done(t):
@@ -285,18 +329,44 @@ class GpuBackend:
 # ---------------------------------------------------------------------------
 
 
+class Chunked:
+    """A limb-sharded batch held as consecutive chunks of ciphertexts (each a
+    backend poly over this rank's limbs), so every join can run per chunk
+    and overlap the compute of the chunks around it."""
+
+    def __init__(self, chunks: list):
+        self.chunks = list(chunks)
+
+    def __len__(self):
+        return len(self.chunks)
+
+    def __iter__(self):
+        return iter(self.chunks)
+
+    def __getitem__(self, i):
+        return self.chunks[i]
+
+
 class LimbShardedPipeline:
     """One rank's view of a limb-sharded batch of ciphertexts.
 
     ``moduli`` is the GLOBAL basis; this rank owns the contiguous limbs
     ``self.limbs``.  Inputs are given as full host channel arrays and sliced
-    here (a real deployment would load only its slice)."""
+    here (a real deployment would load only its slice).  A batch is held as
+    chunks of ``chunk`` ciphertexts (:class:`Chunked`); every join is
+    started per chunk as soon as that chunk's input exists and waited for
+    only by the compute that consumes it, so on RCCL (with the library's
+    stream as torch's current stream, GpuBackend.shared_stream) the
+    all-gather of chunk k runs beside the tensor product of chunk k+1 and the
+    key-switch of chunk k-1 (overlap the join with compute)."""
 
-    def __init__(self, moduli: Sequence[int], degree: int, comm, backend):
+    def __init__(self, moduli: Sequence[int], degree: int, comm, backend, chunk: Optional[int] = None):
         self.comm = comm
         self.backend = backend
         self.degree = degree
         self.moduli = list(moduli)
+        # default: the library's key-switch chunk at N = 2^16 (64 ciphertexts)
+        self.chunk = int(chunk) if chunk else 64
         if comm.world > len(self.moduli):
             raise ValueError(f"{comm.world} ranks for {len(self.moduli)} limbs")
         self._layout()
@@ -311,10 +381,13 @@ class LimbShardedPipeline:
         self.owner_last = max(r for r in range(W) if self.counts[r] > 0)
 
     # -- data in / out ------------------------------------------------------
-    def upload(self, channels_full: np.ndarray):
-        """[B][L][N] (global limbs) -> this rank's slice on its device."""
+    def upload(self, channels_full: np.ndarray) -> Chunked:
+        """[B][L][N] (global limbs) -> this rank's slice on its device, in
+        chunks of ``self.chunk`` ciphertexts."""
         ch = np.asarray(channels_full)
-        return self.backend.upload(self.basis, np.ascontiguousarray(ch[:, self.limbs.start:self.limbs.stop]))
+        loc = ch[:, self.limbs.start:self.limbs.stop]
+        return Chunked([self.backend.upload(self.basis, np.ascontiguousarray(loc[s:s + self.chunk]))
+                        for s in range(0, ch.shape[0], self.chunk)])
 
     def upload_key(self, a_full: np.ndarray, b_full: np.ndarray):
         """Gadget key [L][L][N] (source poly i, global limb j) -> the
@@ -323,43 +396,74 @@ class LimbShardedPipeline:
         return self.backend.key(self.basis, np.ascontiguousarray(a_full[:, s]),
                                 np.ascontiguousarray(b_full[:, s]))
 
-    def download(self, poly) -> np.ndarray:
-        return self.backend.download(poly)
+    def download(self, x: Chunked, first: int = 0, count: Optional[int] = None) -> np.ndarray:
+        """This rank's limbs of ciphertexts [first, first + count) as
+        [count][L_r][N] (all of them by default)."""
+        out, pos = [], 0
+        stop = None if count is None else first + count
+        for c in x:
+            b = self.backend.batch(c)
+            if (stop is None or pos < stop) and pos + b > first:
+                arr = self.backend.download(c)
+                lo, hi = max(first - pos, 0), b if stop is None else min(stop - pos, b)
+                out.append(arr[lo:hi])
+            pos += b
+        return np.concatenate(out, axis=0)
 
     # -- ct x ct + relin (engine.rs:473-539) ---------------------------------
-    def mul_relin(self, c0, c1, c0p, c1p, key):
-        d0, d1, d2 = self.backend.tensor(self.basis, c0, c1, c0p, c1p)
-        d2_full = self.comm.all_gather_limbs(d2, self.counts)  # the relin join
-        return self.backend.keyswitch(self.basis, d2_full, key, d0, d1)
+    def mul_relin(self, c0: Chunked, c1: Chunked, c0p: Chunked, c1p: Chunked, key):
+        """Tensor product per chunk, the relin join (all-gather of d2) started
+        per chunk right behind it, then per chunk: wait for its join, gadget
+        sum for the local target limbs seeded by d0/d1."""
+        pend = []
+        for x0, x1, y0, y1 in zip(c0, c1, c0p, c1p):
+            d0, d1, d2 = self.backend.tensor(self.basis, x0, x1, y0, y1)
+            pend.append((d0, d1, self.comm.all_gather_limbs_async(d2, self.counts)))  # the relin join
+        o0, o1 = [], []
+        for d0, d1, h in pend:
+            a0, a1 = self.backend.keyswitch(self.basis, h.wait(), key, d0, d1)
+            o0.append(a0)
+            o1.append(a1)
+        return Chunked(o0), Chunked(o1)
 
     # -- rotation (engine.rs:412-463) ---------------------------------------
-    def rotate(self, c0, c1, k: int, key):
+    def rotate(self, c0: Chunked, c1: Chunked, k: int, key):
         """rotate_ciphertext with slot offset k and this rank's slice of the
         rotation key (upload_key): sigma is limb-local, sigma(c1) is
-        all-gathered, the gadget sum runs on the local target limbs."""
-        r0 = self.backend.rotate(self.basis, c0, k)
-        r1 = self.backend.rotate_planes(self.basis, c1, k)
-        full = self.comm.all_gather_limbs(r1, self.counts)  # the rotation join
-        a0, a1 = self.backend.keyswitch(self.basis, full, key, None, None)
-        return self.backend.add(self.basis, a0, r0), a1
+        all-gathered per chunk, the gadget sum runs on the local target limbs."""
+        pend = []
+        for x0, x1 in zip(c0, c1):
+            r0 = self.backend.rotate(self.basis, x0, k)
+            r1 = self.backend.rotate_planes(self.basis, x1, k)
+            pend.append((r0, self.comm.all_gather_limbs_async(r1, self.counts)))  # the rotation join
+        o0, o1 = [], []
+        for r0, h in pend:
+            a0, a1 = self.backend.keyswitch(self.basis, h.wait(), key, None, None)
+            o0.append(self.backend.add(self.basis, a0, r0))
+            o1.append(a1)
+        return Chunked(o0), Chunked(o1)
 
     # -- rescale (engine.rs:263-282) -----------------------------------------
-    def rescale(self, c0, c1):
+    def rescale(self, c0: Chunked, c1: Chunked):
         q_last = self.moduli[-1]
-        B = self.backend.batch(c0)
         owner = self.rank == self.owner_last
         # every rank knows the owner's count: all raise together, before the
         # collective, instead of the others waiting in it
         if self.counts[self.owner_last] < 2:
             raise ValueError("rescale would leave the owner of the last limb with no limbs")
-        planes = self.backend.new_planes(self.basis, 2, B)
-        if owner:
-            planes[0].copy_(self.backend.last_limb(c0))
-            planes[1].copy_(self.backend.last_limb(c1))
-        self.comm.broadcast(planes, self.owner_last)  # the rescale join
+        pend = []
+        for x0, x1 in zip(c0, c1):
+            planes = self.backend.new_planes(self.basis, 2, self.backend.batch(x0))
+            if owner:
+                planes[0].copy_(self.backend.last_limb(x0))
+                planes[1].copy_(self.backend.last_limb(x1))
+            pend.append(self.comm.broadcast_async(planes, self.owner_last))  # the rescale join
         out_basis = self.backend.drop_last(self.basis) if owner else self.basis
-        r0 = self.backend.rescale(self.basis, out_basis, c0, planes[0], q_last)
-        r1 = self.backend.rescale(self.basis, out_basis, c1, planes[1], q_last)
+        r0, r1 = [], []
+        for x0, x1, h in zip(c0, c1, pend):
+            planes = h.wait()
+            r0.append(self.backend.rescale(self.basis, out_basis, x0, planes[0], q_last))
+            r1.append(self.backend.rescale(self.basis, out_basis, x1, planes[1], q_last))
         # the global basis lost its last limb, which only its owner held
         self.moduli = self.moduli[:-1]
         self.counts[self.owner_last] -= 1
@@ -367,7 +471,7 @@ class LimbShardedPipeline:
             self.limbs = range(self.limbs.start, self.limbs.stop - 1)
         self.owner_last = max(r for r in range(self.comm.world) if self.counts[r] > 0)
         self.basis = out_basis
-        return r0, r1
+        return Chunked(r0), Chunked(r1)
 
     @property
     def rank(self) -> int:
