@@ -58,7 +58,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=("polymul", "ctmul", "rotate", "encode", "ntt", "pointwise"), default="polymul")
+    p.add_argument("--workload", choices=("polymul", "ctmul", "rotate", "encode", "ntt", "pointwise", "copy"),
+                   default="polymul")
     p.add_argument("--shard", choices=("limb", "batch"), default="limb")
     p.add_argument("--batch", type=int, default=1024, help="poly-mul pairs per GPU per step")
     p.add_argument("--inputs", choices=("device", "host"), default="device",
@@ -644,6 +645,9 @@ def run_ctmul(args, comm, world, rank, local_rank):
         if cnt:
             kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
     prof_basis.profile_enable(False)
+    power = None
+    if rank == 0 and world == 1 and not args.no_power:
+        power = power_probe(step, torch.cuda.synchronize, local_rank)
 
     parity_ok = None
     cpu = None
@@ -727,6 +731,7 @@ def run_ctmul(args, comm, world, rank, local_rank):
         },
         "roofline": roof,
         "cpu_baseline": cpu,
+        "power": power,
     }
 
 
@@ -814,6 +819,9 @@ def run_rotate(args, comm, world, rank, local_rank):
         Bs.profile_enable(False)
         kms = sum(kv["total_ms"] for kv in kernels.values()) / args.steps
         graph_info = {"kernel_ms_per_step": kms, "device_busy": kms / (elapsed / args.steps * 1e3)}
+    power = None
+    if rank == 0 and not args.no_power:
+        power = power_probe(step, Bs.sync, local_rank)
     rots = B * len(offsets) * args.steps * world
     value = rots / elapsed
     log_c = log_n - max(log_n // 2, 4)
@@ -883,6 +891,7 @@ def run_rotate(args, comm, world, rank, local_rank):
         },
         "roofline": roof,
         "cpu_baseline": cpu,
+        "power": power,
     }
 
 
@@ -1100,6 +1109,9 @@ def run_pointwise(args, comm, world, rank, local_rank):
     elapsed = comm.max(t1 - t0)
     cnt, ms = B.profile_read("elementwise")
     B.profile_enable(False)
+    power = None
+    if rank == 0 and not args.no_power:
+        power = power_probe(lambda: rn.check(lib.rnt_mul(out.handle, a.handle, b.handle)), B.sync, local_rank)
     parity_ok = True
     if rank == 0:
         orc = oracle()
@@ -1135,6 +1147,66 @@ def run_pointwise(args, comm, world, rank, local_rank):
                      "kernels": {"elementwise": {"launches": cnt, "avg_ms": ms / cnt if cnt else None,
                                                  "total_ms": ms}}},
         "cpu_baseline": None,
+        "power": power,
+    }
+
+
+def run_copy(args, comm, world, rank, local_rank):
+    """A plain device copy of `--batch` polys (rnt_copy = k_copy16, 16 bytes
+    per lane): the measured streaming bandwidth the roofline fractions are
+    compared against, and a pure-HBM point of the energy model
+    (tools/energy_model.py)."""
+    import rns_ntt as rn
+
+    n = 1 << args.log_n
+    L = args.limbs
+    mod = rn.generate_primes(args.prime_bits, L, n)
+    B = rn.RnsBasis(mod, n, device=local_rank)
+    wb = 4 if max(mod) < (1 << 31) else 8
+    a = rn.RnsPoly.sample_uniform(B, rn.DeviceRng(55 + rank), args.batch)
+    dst = rn.RnsPoly(B, args.batch)
+    lib = rn.load()
+
+    def step():
+        rn.check(lib.rnt_copy(dst.handle, a.handle))
+
+    for _ in range(args.warmup):
+        step()
+    B.sync()
+    comm.barrier()
+    B.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    B.sync()
+    t1 = time.perf_counter()
+    comm.barrier()
+    elapsed = comm.max(t1 - t0)
+    cnt, ms = B.profile_read("copy")
+    B.profile_enable(False)
+    power = power_probe(step, B.sync, local_rank) if rank == 0 and not args.no_power else None
+    alg = 2 * L * args.batch * n * wb
+    achieved = alg / (ms / cnt * 1e-3) / 1e9
+    return {
+        "metric": "device copy GB/s (read + write)",
+        "value": alg * args.steps * world / elapsed / 1e9,
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32" if wb == 4 else "u64",
+        "data": "synthetic (seeded uniform residues drawn on the device)",
+        "config": {"workload": f"rnt_copy of {args.batch} polys, N=2^{args.log_n}, L={L}",
+                   "parallelism": f"replicas x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "copy", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "alg_bytes_per_launch": alg,
+                     "kernels": {"copy": {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}}},
+        "cpu_baseline": None,
+        "power": power,
     }
 
 
@@ -1259,7 +1331,7 @@ def main():
     comm = Comm.from_env()
     run = {"polymul": run_polymul, "ctmul": run_ctmul, "rotate": run_rotate,
            "encode": run_encode, "ntt": run_ntt,
-           "pointwise": run_pointwise}[args.workload]
+           "pointwise": run_pointwise, "copy": run_copy}[args.workload]
     line = run(args, comm, world, rank, local_rank)
     if rank == 0:
         result_out.write(json.dumps(line) + "\n")
