@@ -100,6 +100,14 @@ def relaunch_with_torchrun(args) -> int:
     return subprocess.call(cmd)
 
 
+def data_backend() -> str:
+    """The limb-sharded joins' process-group backend: "nccl" (RCCL over
+    xGMI, one GPU per rank).  BENCH_ONE_DEVICE=1 rehearsals put every rank
+    on device 0, where RCCL refuses to run, so they join over gloo (host
+    copies of the same tensors) to exercise the rest of the N-rank path."""
+    return "gloo" if os.environ.get("BENCH_ONE_DEVICE") == "1" else "nccl"
+
+
 def oracle():
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle as orc
@@ -595,7 +603,7 @@ def run_ctmul(args, comm, world, rank, local_rank):
     if world > 1 and not batch_shard:
         import torch.distributed as dist
 
-        data_comm = TorchDistComm(dist.new_group(backend="nccl"))  # RCCL over xGMI
+        data_comm = TorchDistComm(dist.new_group(backend=data_backend()))  # RCCL over xGMI
     else:
         data_comm = SingleComm()
     B_global = args.ct_batch * world  # weak scaling
@@ -1225,7 +1233,7 @@ def run_rotate_sharded(args, comm, world, rank, local_rank, log_n, L, mod):
 
     n = 1 << log_n
     torch.cuda.set_device(local_rank)
-    pipe = LimbShardedPipeline(mod, n, TorchDistComm(dist.new_group(backend="nccl")), GpuBackend(local_rank))
+    pipe = LimbShardedPipeline(mod, n, TorchDistComm(dist.new_group(backend=data_backend())), GpuBackend(local_rank))
     B = args.rot_batch * world
     rng = np.random.default_rng(5)
     uniq = min(2, B)

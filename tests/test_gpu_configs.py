@@ -123,6 +123,31 @@ def test_metric_path_edge_operands(gpu):
     assert np.array_equal(t.channels(), a.channels())
 
 
+def test_metric_batch_1024_sampled_pairs(gpu):
+    """The metric's own shape and batch (N = 2^16, L = 16 x 31-bit, 1024
+    pairs, operands drawn on the device as in bench.py): eight pairs --
+    the first, the last, both sides of the 512 midpoint and four random
+    ones -- bit-exact against the oracle's poly.rs:307-329 product, and the
+    same batch through the in-place form (a *= b, out aliasing a)."""
+    rn = gpu
+    n, L, B = 1 << 16, 16, 1024
+    mod = rn.generate_primes(31, L, n)
+    Bd, Bo = rn.RnsBasis(mod, n), orc.Basis(mod, n)
+    drng = rn.DeviceRng(2024)
+    a = rn.RnsPoly.sample_uniform(Bd, drng, B)
+    b = rn.RnsPoly.sample_uniform(Bd, drng, B)
+    c = a * b
+    rng = np.random.default_rng(1024)
+    picks = sorted({0, B - 1, 511, 512, *rng.integers(1, B - 1, size=4).tolist()})
+    a_h = {p: a.channels_of(p)[0] for p in picks}
+    b_h = {p: b.channels_of(p)[0] for p in picks}
+    for p in picks:
+        assert np.array_equal(c.channels_of(p)[0], orc.mul(Bo, a_h[p], b_h[p])), p
+    a *= b
+    for p in picks[:3]:
+        assert np.array_equal(a.channels_of(p)[0], c.channels_of(p)[0]), p
+
+
 @pytest.mark.parametrize("jg", [3, 16])
 def test_decomposition_groups(gpu, monkeypatch, jg):
     """RNT_DEC_JG fixes the key-switch decomposition's target limbs per

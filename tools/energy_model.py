@@ -1,24 +1,21 @@
 #!/usr/bin/env python3
-"""energy_model.py <dir> [--json out.json]: the poly-mul's power-cap model
-("the ceiling").
+"""energy_model.py: the poly-mul's power-cap model ("the
+ceiling"), fitted to measured workloads.
 
-Input: tools/gpu_energy.sh's output -- per workload a bench JSON line (its
-step time, per-kernel launches and the rocm-smi power probe: package watts
-and sclk while the step keeps running) and rocprofv3 --pmc passes of the
-same shape (SQ_INSTS_VALU, SQ_INSTS_LDS, FETCH_SIZE, WRITE_SIZE).
-
-Model (least squares over every workload):
-    P = a + b * f + e_v * VALU/s + e_l * LDS/s + e_m * HBM bytes/s
-f = sclk (GHz), VALU/LDS = wave instructions (SQ_INSTS_*), HBM bytes =
-2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md § HBM's gfx950 correction).
-a + b f is what the chip draws at clock f beyond the counted work (static,
-clock tree, fabric, everything not proportional to these counts).
-
-Prediction at the 1400 W cap for a variant of the poly-mul: with its
-counts per product (V, Ls, M) and its products per clock k (the measured
-rate / sclk, i.e. cycles per product held fixed), the clock solves
-a + b f + (e_v V + e_l Ls + e_m M) k f = cap, and the rate is k f (or the
-clock ceiling 2.4 GHz times k, whichever is lower).
+  energy_model.py collect <gpu_energy.sh dir>... <out.json>
+      per workload: the bench line's rate, step time, package power and
+      sclk (rocm-smi power probe while the step keeps running) and, from
+      the rocprofv3 --pmc passes of the same shape, the per-step VALU and
+      LDS wave instructions (SQ_INSTS_VALU / SQ_INSTS_LDS) and HBM bytes
+      (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md § HBM) of the
+      step's kernels (per-dispatch means x launches per step).
+  energy_model.py fit <data.json> [--json out.json]
+      least squares  P = P0 + e_v * VALU/s + e_m * HBM bytes/s  over every
+      workload, leave-one-out checks of power and of the rate each
+      workload would run at with the power it drew, and the poly-mul's
+      rate at the 1400 W cap for lower-traffic variants:
+      rate = (cap - P0) / (e_v * V + e_m * M) per product, bounded by the
+      VALU-only build's rate (no plane data moved, full clock).
 """
 from __future__ import annotations
 
@@ -40,7 +37,9 @@ KMAP = [(r"^k_colt_fwd|^k_col_fwd", "col_fwd"), (r"^k_colt_inv|^k_col_inv", "col
 
 
 def kid(name: str):
+    # "void rnt::k_row<unsigned int, 2, 8, false>(...)" -> "k_row<unsigned int, 2, ..."
     name = re.sub(r"^void ", "", name.strip())
+    name = re.sub(r"^(rnt::)?(\(anonymous namespace\)::)?", "", name)
     for pat, k in KMAP:
         if re.search(pat, name):
             return k
@@ -61,105 +60,137 @@ def pmc(d: str) -> dict:
     return out
 
 
-def load(d: str) -> list:
+def collect(dirs, out_path):
     rows = []
-    for j in sorted(glob.glob(os.path.join(d, "*.json"))):
-        tag = os.path.basename(j)[:-5]
-        try:
-            line = [x for x in open(j).read().splitlines() if x.startswith("{")][-1]
-        except IndexError:
-            continue
-        b = json.loads(line)
-        pw = b.get("power") or {}
-        if not pw.get("package_w_median") or not pw.get("sclk_mhz_median"):
-            continue
-        kern = (b.get("roofline") or {}).get("kernels") or {}
-        counts = {}
-        for part in ("sq", "fetch", "write"):
-            for k, cs in pmc(os.path.join(d, f"{tag}_{part}")).items():
-                for c, v in cs.items():
-                    counts.setdefault(k, {})[c] = v
-        steps = b["steps"]
-        per_step = collections.Counter()
-        for k, kv in kern.items():
-            lps = kv["launches"] / steps
-            for c, v in counts.get(k, {}).items():
-                per_step[c] += v * lps
-        hbm = 2 * per_step["FETCH_SIZE"] * 1024 + per_step["WRITE_SIZE"] * 1024  # rocprofv3 reports KiB
-        t = b["ms_per_step"] * 1e-3
-        rows.append({"tag": tag, "P": pw["package_w_median"], "f": pw["sclk_mhz_median"] / 1e3,
-                     "valu": per_step["SQ_INSTS_VALU"] / t / 1e9, "lds": per_step["SQ_INSTS_LDS"] / t / 1e9,
-                     "hbm": hbm / t / 1e12, "value": b["value"], "unit": b["unit"], "ms": b["ms_per_step"],
-                     "per_unit": {"valu": per_step["SQ_INSTS_VALU"], "lds": per_step["SQ_INSTS_LDS"], "hbm": hbm},
-                     "units_per_step": b["value"] * t})
-    return rows
+    for d in dirs:
+        for j in sorted(glob.glob(os.path.join(d, "*.json"))):
+            tag = os.path.basename(j)[:-5]
+            lines = [x for x in open(j).read().splitlines() if x.startswith("{")]
+            if not lines:
+                continue
+            b = json.loads(lines[-1])
+            pw = b.get("power") or {}
+            if not pw.get("package_w_median") or not pw.get("sclk_mhz_median"):
+                continue
+            kern = (b.get("roofline") or {}).get("kernels") or {}
+            counts = {}
+            for part in ("sq", "fetch", "write"):
+                for k, cs in pmc(os.path.join(d, f"{tag}_{part}")).items():
+                    counts.setdefault(k, {}).update(cs)
+            per_step = collections.Counter()
+            for k, kv in kern.items():
+                lps = kv["launches"] / b["steps"]
+                for c, v in counts.get(k, {}).items():
+                    per_step[c] += v * lps
+            t = b["ms_per_step"] * 1e-3
+            rows.append({
+                "tag": tag, "P_w": pw["package_w_median"], "sclk_ghz": pw["sclk_mhz_median"] / 1e3,
+                "rate": b["value"], "unit": b["unit"], "ms_per_step": b["ms_per_step"],
+                "units_per_step": b["value"] * t,
+                # per step, the step's kernels only
+                "valu_insts": per_step["SQ_INSTS_VALU"], "lds_insts": per_step["SQ_INSTS_LDS"],
+                # rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB
+                "hbm_bytes": (2 * per_step["FETCH_SIZE"] + per_step["WRITE_SIZE"]) * 1024,
+                "kernels": {k: round(kv["launches"] / b["steps"], 3) for k, kv in kern.items()},
+            })
+    json.dump({"source": "tools/gpu_energy.sh + tools/energy_model.py collect", "workloads": rows},
+              open(out_path, "w"), indent=1)
+    print(f"{len(rows)} workloads -> {out_path}")
 
 
-def fit(rows):
-    X = np.array([[1.0, r["f"], r["valu"], r["lds"], r["hbm"]] for r in rows])
-    y = np.array([r["P"] for r in rows])
-    coef, *_ = np.linalg.lstsq(X, y, rcond=None)
-    return coef, X @ coef
+def _rates(r):
+    t = r["ms_per_step"] * 1e-3
+    return r["valu_insts"] / t / 1e9, r["hbm_bytes"] / t / 1e12  # G wave-instr/s, TB/s
+
+
+def _lstsq(rows):
+    X = np.array([[1.0, *_rates(r)] for r in rows])
+    y = np.array([r["P_w"] for r in rows])
+    c, *_ = np.linalg.lstsq(X, y, rcond=None)
+    return c
+
+
+def _joules(c, r):
+    n = r["units_per_step"]
+    return c[1] * r["valu_insts"] / n / 1e9 + c[2] * r["hbm_bytes"] / n / 1e12  # J per unit
+
+
+def fit(path, out_json=None, cap=1400.0, holdout=("polymul_meas3", "polymul_meas4",
+                                                   "polymul_b256_meas3", "polymul_b256_meas4")):
+    allrows = json.load(open(path))["workloads"]
+    # the traffic-emulation builds (RNT_MEAS=3/4: every butterfly kept, the
+    # 5- or 7-plane traffic of a fused design) are held out of the fit: they
+    # test its what-if predictions
+    rows = [r for r in allrows if r["tag"] not in holdout]
+    held = [r for r in allrows if r["tag"] in holdout]
+    c = _lstsq(rows)
+    P0, ev, em = (float(x) for x in c)
+    print(f"P = {P0:.0f} W + {ev:.3f} nJ x VALU wave-instr/s + {em:.1f} pJ x HBM B/s   ({len(rows)} workloads)")
+    res = {"model": "P = P0 + e_v * VALU wave-instructions/s + e_m * HBM bytes/s",
+           "P0_w": P0, "e_valu_nj_per_wave_instr": ev, "e_hbm_pj_per_byte": em, "points": []}
+    print(f"{'workload':20s} {'P':>6s} {'fit':>6s} {'loo':>6s} {'GHz':>5s} {'VALU G/s':>8s} {'TB/s':>5s}"
+          f" {'rate':>10s} {'loo rate':>10s} {'err':>6s}")
+    for i, r in enumerate(rows):
+        ci = _lstsq(rows[:i] + rows[i + 1:])
+        v, m = _rates(r)
+        pf, pl = c @ [1, v, m], ci @ [1, v, m]
+        rate_loo = (r["P_w"] - ci[0]) / _joules(ci, r)  # the rate the drawn power buys
+        err = rate_loo / r["rate"] - 1
+        print(f"{r['tag']:20s} {r['P_w']:6.0f} {pf:6.0f} {pl:6.0f} {r['sclk_ghz']:5.2f} {v:8.1f} {m:5.2f}"
+              f" {r['rate']:10.4g} {rate_loo:10.4g} {err * 100:+5.1f}%")
+        res["points"].append({"tag": r["tag"], "P_w": r["P_w"], "fit_w": float(pf), "loo_w": float(pl),
+                              "rate": r["rate"], "unit": r["unit"], "loo_rate": float(rate_loo),
+                              "loo_rate_err": float(err), "valu_G_per_s": v, "hbm_TB_per_s": m,
+                              "sclk_ghz": r["sclk_ghz"]})
+    if held:
+        print("\nheld out (traffic emulation builds):")
+        res["held_out"] = []
+        for r in held:
+            v, m = _rates(r)
+            rate_pred = min((min(r["P_w"], cap) - c[0]) / _joules(c, r), float("inf"))
+            err = rate_pred / r["rate"] - 1
+            print(f"{r['tag']:20s} {r['P_w']:6.0f} {c @ [1, v, m]:6.0f} {r['sclk_ghz']:5.2f} {v:8.1f} {m:5.2f}"
+                  f" {r['rate']:10.4g} {rate_pred:10.4g} {err * 100:+5.1f}%  ({r['hbm_bytes'] / r['units_per_step'] / 1e6:.1f} MB/unit)")
+            res["held_out"].append({"tag": r["tag"], "P_w": r["P_w"], "rate": r["rate"], "pred_rate": rate_pred,
+                                    "err": err, "hbm_MB_per_unit": r["hbm_bytes"] / r["units_per_step"] / 1e6})
+    base = next((r for r in rows if r["tag"] == "polymul"), None)
+    valu_only = next((r for r in rows if r["tag"] == "polymul_meas1"), None)
+    if base:
+        n = base["units_per_step"]
+        V, M = base["valu_insts"] / n, base["hbm_bytes"] / n
+        ceiling = valu_only["rate"] * 2.4 / valu_only["sclk_ghz"] if valu_only else float("inf")
+        print(f"\npoly-mul (N=2^16, L=16): {V / 1e6:.2f} M VALU wave-instr and {M / 1e6:.1f} MB of HBM per product;"
+              f" energy {(ev * V / 1e9 + em * M / 1e12) * 1e3:.2f} mJ + P0 x time; VALU-only ceiling"
+              f" {ceiling / 1e3:.0f}k/s at 2.4 GHz")
+        res["polymul_per_product"] = {"valu_wave_instr": V, "hbm_bytes": M, "valu_only_ceiling": ceiling}
+        res["at_cap"] = {}
+        for name, planes, vf in (("as built: 9 planes of HBM per (poly, limb)", 9, 1.0),
+                                 ("7 planes (row pass + inverse column pass fused on one CU)", 7, 1.0),
+                                 ("5 planes (whole-plane fwd(a), then fwd(b) x a^ -> inverse)", 5, 1.0),
+                                 ("3 planes (read a, read b, write c only)", 3, 1.0),
+                                 ("9 planes, 10% fewer VALU instructions", 9, 0.9)):
+            e = ev * V * vf / 1e9 + em * M * planes / 9 / 1e12
+            rate = min((cap - P0) / e, ceiling)
+            res["at_cap"][name] = rate
+            print(f"  {name:62s} -> {rate / 1e3:6.1f}k poly-muls/s")
+    if out_json:
+        json.dump(res, open(out_json, "w"), indent=1)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("dir")
-    ap.add_argument("--json")
-    ap.add_argument("--cap", type=float, default=1400.0)
-    args = ap.parse_args()
-    rows = load(args.dir)
-    if len(rows) < 6:
-        raise SystemExit(f"need >= 6 workloads with power and PMC data, got {len(rows)}")
-    coef, pred = fit(rows)
-    names = ["a_W", "b_W_per_GHz", "e_valu_nJ_per_Ginstr(W per Ginstr/s)", "e_lds_W_per_Ginstr_s",
-             "e_hbm_W_per_TBs"]
-    print("fit:", {n: round(float(c), 3) for n, c in zip(names, coef)})
-    loo = []
-    for i in range(len(rows)):
-        c, _ = fit(rows[:i] + rows[i + 1:])
-        x = np.array([1.0, rows[i]["f"], rows[i]["valu"], rows[i]["lds"], rows[i]["hbm"]])
-        loo.append(float(x @ c))
-    out = {"coef": dict(zip(["a", "b", "e_valu", "e_lds", "e_hbm"], map(float, coef))), "points": []}
-    print(f"{'workload':16s} {'P':>7s} {'fit':>7s} {'loo':>7s} {'GHz':>5s} {'VALU G/s':>9s} {'LDS G/s':>8s} {'HBM TB/s':>8s}")
-    for r, p, l in zip(rows, pred, loo):
-        print(f"{r['tag']:16s} {r['P']:7.0f} {p:7.0f} {l:7.0f} {r['f']:5.2f} {r['valu']:9.1f} {r['lds']:8.1f} {r['hbm']:8.2f}")
-        out["points"].append({**{k: r[k] for k in ("tag", "P", "f", "valu", "lds", "hbm", "value", "unit", "ms")},
-                              "fit": float(p), "loo": float(l)})
-    # the poly-mul at the cap, and what-ifs
-    base = next((r for r in rows if r["tag"] == "polymul"), None)
-    if base:
-        a, b, ev, el, em = coef
-        n = base["units_per_step"]
-        V, Ls, M = (base["per_unit"][k] / n for k in ("valu", "lds", "hbm"))
-        k = base["value"] / base["f"]  # products per (GHz * s)
-
-        def rate(Vx, Lx, Mx, kx):
-            # joules per product: V, Ls in wave instructions, M in bytes
-            # (the coefficients are W per G instr/s and W per TB/s)
-            e = ev * Vx / 1e9 + el * Lx / 1e9 + em * Mx / 1e12
-            f = (args.cap - a) / (b + e * kx)
-            f = min(f, 2.4)
-            return kx * f, f
-
-        # k (products per GHz-second) is held fixed: the same cycles per
-        # product, only the energy changes -- an upper bound for a variant
-        # that moves fewer bytes, since it also assumes no new stalls
-        scen = {"as measured (9 planes of HBM per limb)": (V, Ls, M, k),
-                "5 planes (whole-plane fwd(a) + fused product)": (V, Ls, M * 5 / 9, k),
-                "3 planes (read a, b, write c only)": (V, Ls, M * 3 / 9, k),
-                "VALU instructions -10%": (V * 0.9, Ls, M, k),
-                "no HBM traffic at all": (V, Ls, 0.0, k)}
-        out["polymul_per_product"] = {"valu": V, "lds": Ls, "hbm_bytes": M, "products_per_GHz_s": k}
-        out["scenarios"] = {}
-        print(f"\npoly-mul per product: VALU {V:.3g}, LDS {Ls:.3g} wave-instr, HBM {M / 1e6:.1f} MB;"
-              f" measured {base['value']:.0f}/s at {base['P']:.0f} W, {base['f']:.2f} GHz")
-        for name, (Vx, Lx, Mx, kx) in scen.items():
-            r, f = rate(Vx, Lx, Mx, kx)
-            out["scenarios"][name] = {"rate": r, "GHz": f}
-            print(f"  {name:48s} -> {r / 1e3:7.1f}k/s at {f:.2f} GHz")
-    if args.json:
-        json.dump(out, open(args.json, "w"), indent=1)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    c = sub.add_parser("collect")
+    c.add_argument("paths", nargs="+")
+    f = sub.add_parser("fit")
+    f.add_argument("data")
+    f.add_argument("--json")
+    f.add_argument("--cap", type=float, default=1400.0)
+    a = ap.parse_args()
+    if a.cmd == "collect":
+        collect(a.paths[:-1], a.paths[-1])
+    else:
+        fit(a.data, a.json, a.cap)
 
 
 if __name__ == "__main__":

@@ -23,6 +23,11 @@ run() {  # run <tag> <lib|-> <bench args...>
     rc=$?; echo "pmc $tag $name rc=$rc" >&2; [ $rc -eq 0 ] || exit $rc
   done
 }
+if [ -n "$ONLY" ]; then  # ONLY="tag lib args...;tag lib args..." runs just those
+  IFS=';' read -ra items <<< "$ONLY"
+  for it in "${items[@]}"; do run $it; done
+  exit 0
+fi
 run polymul - --steps 20 --warmup 3
 run polymul_meas1 meas1 --steps 20 --warmup 3
 run polymul_meas2 meas2 --steps 20 --warmup 3

@@ -93,6 +93,18 @@ constexpr int kBufAux = 0;
 #define RNT_MEAS 0
 #endif
 constexpr int kMeas = RNT_MEAS;
+// 3 and 4 keep every butterfly and move the poly-mul's plane traffic of a
+// lower-traffic design: the intermediate planes named below are replaced
+// by synthetic values (loads) and never-true stores, so the three kernels
+// move 5 planes per (poly, limb) (3: a's column output and the row
+// output are not written, a's column output and the column-inverse input
+// not read) or 7 (4: only the row -> inverse-column plane is skipped) --
+// the energy model's what-ifs measured directly.
+// Sites: 0 k_colt_fwd operand-0 store, 1 k_row<2> load of operand 0,
+// 2 k_row<2> store, 3 k_colt_inv load.
+constexpr bool meas_virtual(int site) {
+  return (kMeas == 3 && site <= 3) || (kMeas == 4 && (site == 2 || site == 3));
+}
 template <class W>
 __device__ __forceinline__ W meas_val(uint32_t v, uint32_t s) {
   return (W)((v * 2654435761u + s) & 0x3fffffffu);
@@ -737,7 +749,12 @@ k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t
   }
   xf_fwd<G, W, 1>(x, cp.xp, lds, tw, m);
 #pragma unroll
-  for (int i = 0; i < E; ++i) dst.st(x[0][i], al.v, i * al.s);
+  for (int i = 0; i < E; ++i) {
+    if constexpr (meas_virtual(0)) {
+      if (x[0][i] != (W)0xffffffffu) continue;
+    }
+    dst.st(x[0][i], al.v, i * al.s);
+  }
 }
 
 template <class W, int LOG_R, int LOG_TC, bool LZ = false>
@@ -762,7 +779,8 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
   const BufView<W> src(in + ip, N), dst(out + op, N);
   W x[1][E];
 #pragma unroll
-  for (int i = 0; i < E; ++i) x[0][i] = src.ld(al.v, i * al.s);
+  for (int i = 0; i < E; ++i)
+    x[0][i] = meas_virtual(3) ? meas_val<W>(al.v, (uint32_t)i * al.s) : src.ld(al.v, i * al.s);
   xf_inv<G, W, 1, true>(x, cp.xp, lds, itw, mod_for<W, LZ>(lc), f);  // canonical out
   a0.refresh();
   if (addend != nullptr) {
@@ -910,7 +928,8 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
     W v[2][E];
 #pragma unroll
     for (int i = 0; i < E; ++i) {
-      v[0][i] = gload(xg, base + b0 + ((uint32_t)i << G::BB0));
+      v[0][i] = meas_virtual(1) ? meas_val<W>((uint32_t)(base + b0) + (uint32_t)i, 7u)
+                                : gload(xg, base + b0 + ((uint32_t)i << G::BB0));
       v[1][i] = gload(yg, base + b0 + ((uint32_t)i << G::BB0));
     }
     const auto mo = mod_for<W, LZ>(lc);
@@ -959,7 +978,12 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
     }
     if (rp.active) {
 #pragma unroll
-      for (int i = 0; i < E; ++i) gstore(xg, base + b0 + ((uint32_t)i << G::BB0), z[0][i]);
+      for (int i = 0; i < E; ++i) {
+        if constexpr (meas_virtual(2)) {
+          if (z[0][i] != (W)0xffffffffu) continue;
+        }
+        gstore(xg, base + b0 + ((uint32_t)i << G::BB0), z[0][i]);
+      }
     }
   } else if constexpr (MODE == 0) {
     W v[1][E];
