@@ -123,6 +123,39 @@ def test_metric_path_edge_operands(gpu):
     assert np.array_equal(t.channels(), a.channels())
 
 
+def test_plane_product_matches_oracle(gpu, monkeypatch):
+    """rnt_mul through the whole-plane kernels (RNT_PLANE=1: k_plane_fwd +
+    k_plane_mul, N = 2^16, u32 canonical bases), bit-exact against the
+    oracle's poly.rs:307-329 product on random, all-(q-1), zero and
+    negacyclic-monomial operands, and in both in-place forms."""
+    monkeypatch.setenv("RNT_PLANE", "1")
+    rn = gpu
+    n, L = 1 << 16, 3
+    mod = rn.generate_primes(31, L, n)
+    Bd, Bo = rn.RnsBasis(mod, n), orc.Basis(mod, n)
+    q = np.array(mod, dtype=np.uint64)[:, None]
+    rng = np.random.default_rng(65536)
+    full = np.broadcast_to(q - 1, (L, n)).copy()
+    mono = np.zeros((L, n), dtype=np.uint64)
+    mono[:, n - 1] = 1
+    r1, r2 = _rand(rng, mod, n, 1)[0], _rand(rng, mod, n, 1)[0]
+    pairs = [(r1, r2), (full, full), (full, r1), (np.zeros_like(r1), r2), (mono, mono), (mono, r2)]
+    a_h = np.stack([p[0] for p in pairs])
+    b_h = np.stack([p[1] for p in pairs])
+    a = rn.RnsPoly.from_channels(a_h, Bd)
+    b = rn.RnsPoly.from_channels(b_h, Bd)
+    got = (a * b).channels()
+    for i, (x, y) in enumerate(pairs):
+        assert np.array_equal(got[i], orc.mul(Bo, x, y)), i
+    a *= b  # out aliases a
+    assert np.array_equal(a.channels(), got)
+    b2 = rn.RnsPoly.from_channels(b_h, Bd)
+    a2 = rn.RnsPoly.from_channels(a_h, Bd)
+    from rns_ntt import _lib
+    rn.check(rn.load().rnt_mul(b2.handle, a2.handle, b2.handle))  # out aliases b
+    assert np.array_equal(b2.channels(), got)
+
+
 def test_metric_batch_1024_sampled_pairs(gpu):
     """The metric's own shape and batch (N = 2^16, L = 16 x 31-bit, 1024
     pairs, operands drawn on the device as in bench.py): eight pairs --

@@ -1006,6 +1006,285 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
   }
 }
 
+// ---- whole-plane product (rnt_mul at N = 2^16, u32 canonical bases) ------
+// Two launches per batch instead of three, 5 planes of HBM traffic per
+// (poly, limb) instead of 9 (the 5-plane traffic measured
+// 142k poly-muls/s against 122k for the shipped 9):
+//   k_plane_fwd: a -> a^ (the whole truncated forward transform of one
+//                plane in one workgroup's registers; a^ goes to a private
+//                layout), 2 planes;
+//   k_plane_mul: b -> b^ the same way, a^ (x) b^ (degree-3 block products),
+//                the whole truncated inverse, c, 3 planes.
+// A workgroup = 1024 threads holds one 2^16-word plane, 64 words a thread.
+// The 16-bit index i is split three ways (tA = t >> 5, tB = t & 31):
+//   L0  i = (r << 10) | t                  loads / stores, coalesced
+//   L1  i = (tA << 11) | (r << 5) | tB     register bits 10..5
+//   L2  i = (t << 6) | r                   register bits 5..0
+// and the network is the same merged negacyclic CT / GS heap as the
+// four-step kernels (node = (2^16 + i) >> (b + 1) at bit b), so a^ and the
+// product equal theirs word for word.  Pass A runs bits 15..10 in L0 (its
+// twiddles depend on register bits only: scalar loads), pass B bits 9..5
+// in L1, pass C bits 4..2 in L2 (bits 1..0 are the truncated stages).  The
+// exchanges go through 144 KiB of LDS in two rounds each, split on a bit
+// that is a register bit on both sides (bit 10 for L0 <-> L1, bit 5 for
+// L1 <-> L2), so a round reads exactly the registers it wrote and needs no
+// spare copy; the physical register of a logical one is a compile-time
+// permutation (slot1 / slot2).
+namespace plane {
+constexpr int T = 1024;
+constexpr int LDS_WORDS = (1 << 15) + (1 << 15) / 8;  // L1 <-> L2 rows of 32 words padded by 4
+__host__ __device__ constexpr int slot0(int r) { return r; }
+__host__ __device__ constexpr int slot1(int r) { return 2 * (r & 31) + (r >> 5); }
+__host__ __device__ constexpr int slot2(int r) { return 4 * ((r & 31) >> 1) + 2 * (r >> 5) + (r & 1); }
+template <int L>
+__host__ __device__ constexpr int slot(int r) {
+  return L == 0 ? slot0(r) : L == 1 ? slot1(r) : slot2(r);
+}
+__device__ __forceinline__ uint32_t pad2(uint32_t j) { return j + ((j >> 5) << 2); }
+}  // namespace plane
+
+// CT stages on logical register bits SLHI .. SLLO of layout LY (index bits
+// [BB, BB + 6)); node0 = 2^16 + the thread's index with register bits 0.
+// Twiddles in chunks of CH per stage (bounded registers beside the plane).
+// As in pass_ct, outputs the next stage of the pass only multiplies stay
+// in [0, 2q); the last stage leaves everything canonical.  Stages and
+// chunks are template recursions, so every register index is a
+// compile-time constant (a loop the unroller gave up on would put the
+// plane in scratch memory).
+template <int LY, int BB, int SL, int SLLO, int M0, int CH, class TS>
+__device__ __forceinline__ void plane_ct_chunks(uint32_t (&x)[64], uint32_t nb, const TS& tw,
+                                                const Mod<uint32_t>& mo) {
+  constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
+  Tw<uint32_t> t[n];
+#pragma unroll
+  for (int j = 0; j < n; ++j) t[j] = tw_get<uint32_t>(tw, nb, (uint32_t)(M0 + j));
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+#pragma unroll
+    for (int e = 0; e < d; ++e) {
+      const int i = ((M0 + j) << (SL + 1)) | e;
+      if (SL > SLLO && (i & (d >> 1)))
+        ct_bfly_lazy(x[plane::slot<LY>(i)], x[plane::slot<LY>(i | d)], t[j].w, t[j].p, mo);
+      else
+        ct_bfly(x[plane::slot<LY>(i)], x[plane::slot<LY>(i | d)], t[j].w, t[j].p, mo);
+    }
+  }
+  if constexpr (M0 + CH < cnt) plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH>(x, nb, tw, mo);
+}
+template <int LY, int BB, int SL, int SLLO, int CH, class TS>
+__device__ __forceinline__ void plane_ct(uint32_t (&x)[64], uint32_t node0, const TS& tw,
+                                         const Mod<uint32_t>& mo) {
+  plane_ct_chunks<LY, BB, SL, SLLO, 0, CH>(x, node0 >> (BB + SL + 1), tw, mo);
+  if constexpr (SL > SLLO) plane_ct<LY, BB, SL - 1, SLLO, CH>(x, node0, tw, mo);
+}
+
+// GS stages on logical register bits SLLO .. SLHI; FOLD: the stage at
+// index bit 15 applies the folded constants (4/N with the Montgomery
+// factor, LimbConst c1t/c2t) instead of its twiddle.
+template <int LY, int BB, int SL, int M0, int CH, class TS>
+__device__ __forceinline__ void plane_gs_chunks(uint32_t (&x)[64], uint32_t nb, const TS& itw,
+                                                const Mod<uint32_t>& mo) {
+  constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
+  Tw<uint32_t> t[n];
+#pragma unroll
+  for (int j = 0; j < n; ++j) t[j] = tw_get<uint32_t>(itw, nb, (uint32_t)(M0 + j));
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+#pragma unroll
+    for (int e = 0; e < d; ++e) {
+      const int i = ((M0 + j) << (SL + 1)) | e;
+      gs_bfly(x[plane::slot<LY>(i)], x[plane::slot<LY>(i | d)], t[j].w, t[j].p, mo);
+    }
+  }
+  if constexpr (M0 + CH < cnt) plane_gs_chunks<LY, BB, SL, M0 + CH, CH>(x, nb, itw, mo);
+}
+template <int LY, int BB, int SL, int SLHI, int CH, bool FOLD, class TS>
+__device__ __forceinline__ void plane_gs(uint32_t (&x)[64], uint32_t node0, const TS& itw,
+                                         const Mod<uint32_t>& mo, const Fold<uint32_t>& f) {
+  constexpr int d = 1 << SL;
+  if constexpr (FOLD && BB + SL + 1 == 16) {
+#pragma unroll
+    for (int e = 0; e < d; ++e) {  // the top stage: d = 32, one group
+      const uint32_t u = x[plane::slot<LY>(e)], v = x[plane::slot<LY>(e | d)];
+      x[plane::slot<LY>(e)] = shoup_mul(u + v, f.c1, f.c1p, mo);
+      x[plane::slot<LY>(e | d)] = shoup_mul(u - v + mo.q, f.c2, f.c2p, mo);
+    }
+  } else {
+    plane_gs_chunks<LY, BB, SL, 0, CH>(x, node0 >> (BB + SL + 1), itw, mo);
+  }
+  if constexpr (SL < SLHI) plane_gs<LY, BB, SL + 1, SLHI, CH, FOLD>(x, node0, itw, mo, f);
+}
+
+// L0 <-> L1 through LDS: round h carries the words with index bit 10 == h
+// (L0 registers 2k + h, L1 logical registers (h << 5) | k, both in the
+// physical registers 2k + h).  LDS index j = the 15 other bits.
+template <bool TO_L1>
+__device__ __forceinline__ void plane_xchg01(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
+  const uint32_t tA = t >> 5, tB = t & 31u;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const uint32_t j = TO_L1 ? (((uint32_t)k << 10) | t) : ((tA << 10) | ((uint32_t)k << 5) | tB);
+      lds[j] = x[2 * k + h];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const uint32_t j = TO_L1 ? ((tA << 10) | ((uint32_t)k << 5) | tB) : (((uint32_t)k << 10) | t);
+      x[2 * k + h] = lds[j];
+    }
+    __syncthreads();
+  }
+}
+
+// L1 <-> L2: round h carries index bit 5 == h.  LDS index j = the 15 other
+// bits, rows of 32 padded by 4 words (plane::pad2) so L2's 32 consecutive
+// words per thread come back as eight conflict-free 16-byte reads.
+template <bool TO_L2>
+__device__ __forceinline__ void plane_xchg12(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
+  const uint32_t tA = t >> 5, tB = t & 31u;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if constexpr (TO_L2) {
+      // L1 logical r1 = (hi << 5) | (2m + h): i >> 6 = (tA << 5) | (hi << 4) | m
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+          const uint32_t j = ((((tA << 5) | ((uint32_t)hi << 4) | (uint32_t)m)) << 5) | tB;
+          lds[plane::pad2(j)] = x[plane::slot1((hi << 5) | (2 * m + h))];
+        }
+      __syncthreads();
+      const uint4* row = (const uint4*)(lds + t * 36u);
+#pragma unroll
+      for (int q4 = 0; q4 < 8; ++q4) {
+        const uint4 v = row[q4];
+        x[plane::slot2((h << 5) | (4 * q4 + 0))] = v.x;
+        x[plane::slot2((h << 5) | (4 * q4 + 1))] = v.y;
+        x[plane::slot2((h << 5) | (4 * q4 + 2))] = v.z;
+        x[plane::slot2((h << 5) | (4 * q4 + 3))] = v.w;
+      }
+      __syncthreads();
+    } else {
+      uint4* row = (uint4*)(lds + t * 36u);
+#pragma unroll
+      for (int q4 = 0; q4 < 8; ++q4)
+        row[q4] = make_uint4(x[plane::slot2((h << 5) | (4 * q4 + 0))], x[plane::slot2((h << 5) | (4 * q4 + 1))],
+                             x[plane::slot2((h << 5) | (4 * q4 + 2))], x[plane::slot2((h << 5) | (4 * q4 + 3))]);
+      __syncthreads();
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+          const uint32_t j = ((((tA << 5) | ((uint32_t)hi << 4) | (uint32_t)m)) << 5) | tB;
+          x[plane::slot1((hi << 5) | (2 * m + h))] = lds[plane::pad2(j)];
+        }
+      __syncthreads();
+    }
+  }
+}
+
+// One workgroup per CU and equal work per workgroup keep every CU's load,
+// compute and store phases in step across the chip, so the loads of all
+// CUs meet at the HBM together while the VALUs idle, and then the other
+// way round.  Delaying the first workgroup of every other CU by `ticks`
+// of the 100 MHz real-time counter once shifts that CU's phase for the
+// rest of the launch (its next workgroups start when the previous one
+// ends), so half the CUs load while the other half compute.
+__device__ __forceinline__ void plane_stagger(uint32_t ticks) {
+  if (ticks == 0) return;
+  const uint32_t id = blockIdx.x + blockIdx.y * gridDim.x;
+  if (id >= 256u || !((id >> 3) & 1u)) return;  // first wave, every other CU of each XCD
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+// The truncated forward transform of the plane in x (L0 in, L2 out).
+__device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint32_t t,
+                                          const Tw<uint32_t>* tw, const Mod<uint32_t>& mo) {
+  const uint32_t N = 1u << 16;
+  // pass A's twiddle nodes ((2^16 + i) >> (b + 1), b >= 10) do not depend on
+  // the thread's bits 9..0: node0 = 2^16 keeps them wave-uniform (scalar loads)
+  plane_ct<0, 10, 5, 0, 32>(x, N, TwScalar<uint32_t>{(const RNT_CONST_AS Tw<uint32_t>*)tw}, mo);
+  plane_xchg01<true>(x, lds, t);
+  plane_ct<1, 5, 4, 0, 8>(x, N + (((t >> 5) << 11) | (t & 31u)), tw, mo);
+  plane_xchg12<true>(x, lds, t);
+  plane_ct<2, 0, 4, 2, 8>(x, N + (t << 6), tw, mo);
+}
+
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_fwd(uint32_t* __restrict__ ahat, const uint32_t* __restrict__ a, TabPtrs<uint32_t> tp,
+            uint64_t ls, uint32_t stagger) {
+  plane_stagger(stagger);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const uint32_t t = threadIdx.x, p = blockIdx.x, l = blockIdx.y;
+  const uint64_t N = 1ull << 16;
+  const uint64_t off = (uint64_t)l * ls + (uint64_t)p * N;
+  const BufView<uint32_t> src(a + off, (uint32_t)N);
+  uint32_t x[64];
+#pragma unroll
+  for (int r = 0; r < 64; ++r) x[r] = src.ld(t, (uint32_t)r << 10);
+  const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
+  plane_fwd(x, lds, t, tw, mod_of(tp.lc[l]));
+  // a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
+  uint4* dst = (uint4*)(ahat + off);
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk)
+    dst[kk * 1024 + t] = make_uint4(x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)],
+                                    x[plane::slot2(4 * kk + 2)], x[plane::slot2(4 * kk + 3)]);
+}
+
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_mul(uint32_t* __restrict__ c, const uint32_t* __restrict__ b, const uint32_t* __restrict__ ahat,
+            TabPtrs<uint32_t> tp, uint64_t ls, uint32_t stagger) {
+  plane_stagger(stagger);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const uint32_t t = threadIdx.x, p = blockIdx.x, l = blockIdx.y;
+  const uint64_t N = 1ull << 16;
+  const uint64_t off = (uint64_t)l * ls + (uint64_t)p * N;
+  const LimbConst<uint32_t> lc = tp.lc[l];
+  const Mod<uint32_t> mo = mod_of(lc);
+  const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
+  const Tw<uint32_t>* itw = tp.itw + (uint64_t)l * N;
+  uint32_t x[64];
+  {
+    const BufView<uint32_t> src(b + off, (uint32_t)N);
+#pragma unroll
+    for (int r = 0; r < 64; ++r) x[r] = src.ld(t, (uint32_t)r << 10);
+  }
+  plane_fwd(x, lds, t, tw, mo);
+  // degree-3 block products: block (t << 4) | kk, zeta = (-1)^kk psi_rev[N/8 + (t << 3) + kk/2]
+  const uint4* ah = (const uint4*)(ahat + off);
+  const uint32_t zb = (uint32_t)(N >> 3) + (t << 3);
+  const uint32_t n0 = (uint32_t)N;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const uint4 av = ah[kk * 1024 + t];
+    const uint32_t aa[4] = {av.x, av.y, av.z, av.w};
+    const uint32_t bb[4] = {x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
+                            x[plane::slot2(4 * kk + 3)]};
+    const Tw<uint32_t> w = tw[zb + (kk >> 1)];
+    const uint32_t zeta = (kk & 1) ? lc.q - w.w : w.w;
+    const uint32_t zeta_p = (kk & 1) ? ~w.p : w.p;
+    uint32_t cc[4];
+    mul_mod_x4(cc, aa, bb, zeta, zeta_p, lc.q, lc.qinv);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = cc[e];
+  }
+  plane_gs<2, 0, 2, 4, 8, false>(x, n0 + (t << 6), itw, mo, Fold<uint32_t>{});
+  plane_xchg12<false>(x, lds, t);
+  plane_gs<1, 5, 0, 4, 8, false>(x, n0 + (((t >> 5) << 11) | (t & 31u)), itw, mo, Fold<uint32_t>{});
+  plane_xchg01<false>(x, lds, t);
+  plane_gs<0, 10, 0, 5, 32, true>(x, n0, TwScalar<uint32_t>{(const RNT_CONST_AS Tw<uint32_t>*)itw}, mo,
+                                  Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p});
+  const BufView<uint32_t> dst(c + off, (uint32_t)N);
+#pragma unroll
+  for (int r = 0; r < 64; ++r) dst.st(x[r], t, (uint32_t)r << 10);
+}
+
 // Words per padded LDS key row: C + C/16 (ks_pad's 4 per 64), rounded up to
 // a whole 16-byte unit (the host sizes the LDS with the same formula).
 template <class W>
@@ -2049,6 +2328,32 @@ hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* ou
   RNT_WIDE((col_fwd_t<uint32_t, false>(k, out0, in0, out1, in1, in_ls, out_ls)),
            (col_fwd_t<uint64_t, false>(k, out0, in0, out1, in1, in_ls, out_ls)));
 }
+// The whole-plane product (k_plane_fwd + k_plane_mul) serves rnt_mul for
+// u32 canonical bases at N = 2^16 when Tables::plane is set (RNT_PLANE).
+bool plane_ok(const Tables* t) {
+  return t->plane && !t->wide && !lazy30_ok(t) && t->log_n == 16;
+}
+
+hipError_t launch_plane(const Launch& k, int which, void* out, const void* in, const void* ahat,
+                        uint64_t ls) {
+  if (k.B == 0 || k.L == 0) return hipSuccess;
+  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  const size_t lds = (size_t)plane::LDS_WORDS * 4;
+  const dim3 grid((unsigned)k.B, (unsigned)k.L);
+  if (which == 0) {
+    hipError_t e = allow_lds(k_plane_fwd, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_plane_fwd, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)in,
+                       tab_ptrs<uint32_t>(k.t), ls, k.t->plane_stagger);
+  } else {
+    hipError_t e = allow_lds(k_plane_mul, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_plane_mul, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)in,
+                       (const uint32_t*)ahat, tab_ptrs<uint32_t>(k.t), ls, k.t->plane_stagger);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls, bool lazy) {
   const bool lz = lazy && lazy30_ok(k.t);
   RNT_WIDE(row_t<uint32_t>(k, mode, x, y, ls, lz), row_t<uint64_t>(k, mode, x, y, ls, false));
