@@ -123,12 +123,14 @@ def test_metric_path_edge_operands(gpu):
     assert np.array_equal(t.channels(), a.channels())
 
 
-def test_plane_product_matches_oracle(gpu, monkeypatch):
-    """rnt_mul through the whole-plane kernels (RNT_PLANE=1: k_plane_fwd +
-    k_plane_mul, N = 2^16, u32 canonical bases), bit-exact against the
-    oracle's poly.rs:307-329 product on random, all-(q-1), zero and
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_plane_product_matches_oracle(gpu, monkeypatch, mode):
+    """rnt_mul through the whole-plane kernels (k_plane_fwd + k_plane_mul,
+    N = 2^16, u32 canonical bases; RNT_PLANE=1 one workgroup per plane,
+    RNT_PLANE=2 persistent workgroups with LDS prefetch), bit-exact against
+    the oracle's poly.rs:307-329 product on random, all-(q-1), zero and
     negacyclic-monomial operands, and in both in-place forms."""
-    monkeypatch.setenv("RNT_PLANE", "1")
+    monkeypatch.setenv("RNT_PLANE", mode)
     rn = gpu
     n, L = 1 << 16, 3
     mod = rn.generate_primes(31, L, n)

@@ -632,7 +632,7 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     // RNT_LAZY30=0 keeps the canonical product path for 30-bit bases (A/B)
     t->lazy30 = !wide && lazy30 && env_long("RNT_LAZY30", 1) != 0;
     // RNT_PLANE=1: rnt_mul through the whole-plane kernels (N = 2^16, u32)
-    t->plane = env_long("RNT_PLANE", 0) != 0;
+    t->plane = (int)env_long("RNT_PLANE", 0);
     t->plane_stagger = (uint32_t)env_long("RNT_PLANE_STAGGER", 0);
     {
       const long jg = env_long("RNT_DEC_JG", 0);  // A/B knob: 0 = auto, else 1..1024

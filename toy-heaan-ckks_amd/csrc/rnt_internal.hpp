@@ -81,7 +81,8 @@ struct Tables {
   int device = 0;
   int wide = 0;            // 0: W = u32, 1: W = u64
   bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path
-  bool plane = false;      // rnt_mul through the whole-plane kernels where plane_ok (RNT_PLANE)
+  int plane = 0;           // rnt_mul through the whole-plane kernels where plane_ok (RNT_PLANE:
+                           // 1 one workgroup per plane, 2 persistent with prefetch)
   uint32_t plane_stagger = 0;  // their first-wave phase shift, 100 MHz ticks (RNT_PLANE_STAGGER)
   uint32_t dec_jg = 0;     // key-switch decomposition: target limbs per workgroup (0 = auto)
   size_t ks_ws_bytes = (size_t)4096 << 20;  // key-switch scratch cap per chunk (RNT_KS_WS_MB)

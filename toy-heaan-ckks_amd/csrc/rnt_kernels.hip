@@ -1016,31 +1016,38 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
 //   k_plane_mul: b -> b^ the same way, a^ (x) b^ (degree-3 block products),
 //                the whole truncated inverse, c, 3 planes.
 // A workgroup = 1024 threads holds one 2^16-word plane, 64 words a thread.
-// The 16-bit index i is split three ways (tA = t >> 5, tB = t & 31):
-//   L0  i = (r << 10) | t                  loads / stores, coalesced
-//   L1  i = (tA << 11) | (r << 5) | tB     register bits 10..5
-//   L2  i = (t << 6) | r                   register bits 5..0
+// Thread t = (w << 6) | lam (wave w, lane lam); the 16-bit index i is split
+// three ways:
+//   L0  i = (r << 10) | (w << 6) | lam     registers: bits 15..10, coalesced
+//   L1  i = (w << 12) | (r << 6) | lam     registers: bits 11..6
+//   L2  i = (w << 12) | (lam << 6) | r     registers: bits 5..0
 // and the network is the same merged negacyclic CT / GS heap as the
 // four-step kernels (node = (2^16 + i) >> (b + 1) at bit b), so a^ and the
-// product equal theirs word for word.  Pass A runs bits 15..10 in L0 (its
-// twiddles depend on register bits only: scalar loads), pass B bits 9..5
-// in L1, pass C bits 4..2 in L2 (bits 1..0 are the truncated stages).  The
-// exchanges go through 144 KiB of LDS in two rounds each, split on a bit
-// that is a register bit on both sides (bit 10 for L0 <-> L1, bit 5 for
-// L1 <-> L2), so a round reads exactly the registers it wrote and needs no
-// spare copy; the physical register of a logical one is a compile-time
-// permutation (slot1 / slot2).
+// product equal theirs word for word.  Pass A runs bits 15..10 in L0, pass
+// B bits 9..6 in L1 (both with wave-uniform twiddle nodes: scalar loads),
+// pass C bits 5..2 in L2 (bits 1..0 are the truncated stages).
+//   X1 (L0 <-> L1) keeps the lanes and moves words between waves: 128 KiB
+//      of LDS in two rounds, split on index bit 10 (a register bit on both
+//      sides, so a round reads back exactly the registers it wrote).
+//   X2 (L1 <-> L2) stays inside each wave: lane bits 5, 4 trade places with
+//      register bits 5, 4 through v_permlane32_swap / v_permlane16_swap,
+//      and the remaining 16 x 16 transposes go through a wave-private LDS
+//      buffer in four rounds, with no workgroup barrier.
+// The physical register of a logical one is a compile-time permutation
+// (slot1, shared by L1 and L2).
 namespace plane {
 constexpr int T = 1024;
-constexpr int LDS_WORDS = (1 << 15) + (1 << 15) / 8;  // L1 <-> L2 rows of 32 words padded by 4
+constexpr int XS = 17;                  // X2 buffer row stride (words): conflict-free both ways
+constexpr int XW = 64 * XS;             // words of one X2 buffer
+constexpr int LDS_WORDS = 16 * 2 * XW;  // two X2 buffers per wave; >= 2^15 (an X1 round)
+static_assert(LDS_WORDS >= (1 << 15), "X1 round");
 __host__ __device__ constexpr int slot0(int r) { return r; }
-__host__ __device__ constexpr int slot1(int r) { return 2 * (r & 31) + (r >> 5); }
-__host__ __device__ constexpr int slot2(int r) { return 4 * ((r & 31) >> 1) + 2 * (r >> 5) + (r & 1); }
+__host__ __device__ constexpr int slot1(int r) { return 2 * (((r >> 5) << 4) | (r & 15)) + ((r >> 4) & 1); }
+__host__ __device__ constexpr int slot2(int r) { return slot1(r); }
 template <int L>
 __host__ __device__ constexpr int slot(int r) {
-  return L == 0 ? slot0(r) : L == 1 ? slot1(r) : slot2(r);
+  return L == 0 ? slot0(r) : slot1(r);
 }
-__device__ __forceinline__ uint32_t pad2(uint32_t j) { return j + ((j >> 5) << 2); }
 }  // namespace plane
 
 // CT stages on logical register bits SLHI .. SLLO of layout LY (index bits
@@ -1115,74 +1122,78 @@ __device__ __forceinline__ void plane_gs(uint32_t (&x)[64], uint32_t node0, cons
   if constexpr (SL < SLHI) plane_gs<LY, BB, SL + 1, SLHI, CH, FOLD>(x, node0, itw, mo, f);
 }
 
-// L0 <-> L1 through LDS: round h carries the words with index bit 10 == h
-// (L0 registers 2k + h, L1 logical registers (h << 5) | k, both in the
-// physical registers 2k + h).  LDS index j = the 15 other bits.
-template <bool TO_L1>
-__device__ __forceinline__ void plane_xchg01(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
-  const uint32_t tA = t >> 5, tB = t & 31u;
+// X1, L0 <-> L1 through LDS.  Round h carries the words with index bit
+// 10 == h: L0 registers 2k + h, L1 logical registers r1 = ((k >> 4) << 5) |
+// (h << 4) | (k & 15), both in physical register 2k + h.  LDS word = the 15
+// other index bits; every access is 64 consecutive words per wave.
+// SYNC_FIRST: other waves may still be reading their X2 buffers.
+template <bool TO_L1, bool SYNC_FIRST>
+__device__ __forceinline__ void plane_x1(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
+  const uint32_t w = t >> 6, lam = t & 63u;
+  if constexpr (SYNC_FIRST) __syncthreads();
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-      const uint32_t j = TO_L1 ? (((uint32_t)k << 10) | t) : ((tA << 10) | ((uint32_t)k << 5) | tB);
-      lds[j] = x[2 * k + h];
+      const uint32_t j0 = ((uint32_t)k << 10) | t;
+      const uint32_t j1 = ((((w << 1) | ((uint32_t)k >> 4))) << 10) | (((uint32_t)k & 15u) << 6) | lam;
+      lds[TO_L1 ? j0 : j1] = x[2 * k + h];
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-      const uint32_t j = TO_L1 ? ((tA << 10) | ((uint32_t)k << 5) | tB) : (((uint32_t)k << 10) | t);
-      x[2 * k + h] = lds[j];
+      const uint32_t j0 = ((uint32_t)k << 10) | t;
+      const uint32_t j1 = ((((w << 1) | ((uint32_t)k >> 4))) << 10) | (((uint32_t)k & 15u) << 6) | lam;
+      x[2 * k + h] = lds[TO_L1 ? j1 : j0];
     }
     __syncthreads();
   }
 }
 
-// L1 <-> L2: round h carries index bit 5 == h.  LDS index j = the 15 other
-// bits, rows of 32 padded by 4 words (plane::pad2) so L2's 32 consecutive
-// words per thread come back as eight conflict-free 16-byte reads.
-template <bool TO_L2>
-__device__ __forceinline__ void plane_xchg12(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
-  const uint32_t tA = t >> 5, tB = t & 31u;
+// Lane bit 5 <-> L1 register bit 5 and lane bit 4 <-> register bit 4
+// (self-inverse; the two commute).
+__device__ __forceinline__ void plane_swap54(uint32_t (&x)[64]) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    if constexpr (TO_L2) {
-      // L1 logical r1 = (hi << 5) | (2m + h): i >> 6 = (tA << 5) | (hi << 4) | m
-#pragma unroll
-      for (int hi = 0; hi < 2; ++hi)
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-          const uint32_t j = ((((tA << 5) | ((uint32_t)hi << 4) | (uint32_t)m)) << 5) | tB;
-          lds[plane::pad2(j)] = x[plane::slot1((hi << 5) | (2 * m + h))];
-        }
-      __syncthreads();
-      const uint4* row = (const uint4*)(lds + t * 36u);
-#pragma unroll
-      for (int q4 = 0; q4 < 8; ++q4) {
-        const uint4 v = row[q4];
-        x[plane::slot2((h << 5) | (4 * q4 + 0))] = v.x;
-        x[plane::slot2((h << 5) | (4 * q4 + 1))] = v.y;
-        x[plane::slot2((h << 5) | (4 * q4 + 2))] = v.z;
-        x[plane::slot2((h << 5) | (4 * q4 + 3))] = v.w;
-      }
-      __syncthreads();
-    } else {
-      uint4* row = (uint4*)(lds + t * 36u);
-#pragma unroll
-      for (int q4 = 0; q4 < 8; ++q4)
-        row[q4] = make_uint4(x[plane::slot2((h << 5) | (4 * q4 + 0))], x[plane::slot2((h << 5) | (4 * q4 + 1))],
-                             x[plane::slot2((h << 5) | (4 * q4 + 2))], x[plane::slot2((h << 5) | (4 * q4 + 3))]);
-      __syncthreads();
-#pragma unroll
-      for (int hi = 0; hi < 2; ++hi)
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-          const uint32_t j = ((((tA << 5) | ((uint32_t)hi << 4) | (uint32_t)m)) << 5) | tB;
-          x[plane::slot1((hi << 5) | (2 * m + h))] = lds[plane::pad2(j)];
-        }
-      __syncthreads();
-    }
+  for (int m = 0; m < 64; ++m) {
+    if (m & 32) continue;
+    const auto r = __builtin_amdgcn_permlane32_swap(x[plane::slot1(m)], x[plane::slot1(m | 32)], false, false);
+    x[plane::slot1(m)] = r[0];
+    x[plane::slot1(m | 32)] = r[1];
   }
+#pragma unroll
+  for (int m = 0; m < 64; ++m) {
+    if (m & 16) continue;
+    const auto r = __builtin_amdgcn_permlane16_swap(x[plane::slot1(m)], x[plane::slot1(m | 16)], false, false);
+    x[plane::slot1(m)] = r[0];
+    x[plane::slot1(m | 16)] = r[1];
+  }
+}
+
+// X2, L1 <-> L2 inside each wave.  After plane_swap54 a lane holds index
+// bits 11, 10 (lane bits 5, 4) and 3..0, a register m holds bits 5, 4
+// (m >> 4) and 9..6 (m & 15); per group g = m >> 4 the 16 x 16 blocks of
+// (m & 15) x (lane & 15) transpose through the wave's LDS buffer: word
+// (lane, m & 15) at lane * 17 + (m & 15), read back by lane' as register
+// (g << 4) | c from lane (lane' & 48) | c, column lane' & 15 (both
+// directions 64 distinct banks).  LDS instructions of one wave execute in
+// order, so the reads see the same wave's writes; two buffers alternate.
+template <bool TO_L2>
+__device__ __forceinline__ void plane_x2(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
+  const uint32_t w = t >> 6, lam = t & 63u;
+  if constexpr (TO_L2) plane_swap54(x);
+  const uint32_t a15 = lam * plane::XS;                          // + (m & 15)
+  const uint32_t a2 = (lam & 48u) * plane::XS + (lam & 15u);     // + c * XS
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint32_t* buf = lds + (w * 2u + (uint32_t)(g & 1)) * plane::XW;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) buf[TO_L2 ? a15 + j : a2 + j * plane::XS] = x[plane::slot1((g << 4) | j)];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[plane::slot1((g << 4) | c)] = buf[TO_L2 ? a2 + c * plane::XS : a15 + c];
+    __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (!TO_L2) plane_swap54(x);
 }
 
 // One workgroup per CU and equal work per workgroup keep every CU's load,
@@ -1200,90 +1211,245 @@ __device__ __forceinline__ void plane_stagger(uint32_t ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
-// The truncated forward transform of the plane in x (L0 in, L2 out).
-__device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint32_t t,
-                                          const Tw<uint32_t>* tw, const Mod<uint32_t>& mo) {
-  const uint32_t N = 1u << 16;
-  // pass A's twiddle nodes ((2^16 + i) >> (b + 1), b >= 10) do not depend on
-  // the thread's bits 9..0: node0 = 2^16 keeps them wave-uniform (scalar loads)
-  plane_ct<0, 10, 5, 0, 32>(x, N, TwScalar<uint32_t>{(const RNT_CONST_AS Tw<uint32_t>*)tw}, mo);
-  plane_xchg01<true>(x, lds, t);
-  plane_ct<1, 5, 4, 0, 8>(x, N + (((t >> 5) << 11) | (t & 31u)), tw, mo);
-  plane_xchg12<true>(x, lds, t);
-  plane_ct<2, 0, 4, 2, 8>(x, N + (t << 6), tw, mo);
+// Phase timeline of the plane kernels (measurement build only:
+// tools/build_variant.sh trace -DRNT_PLANE_TRACE; tools/plane_trace.py).
+// Lane 0 of every wave of the first 4096 workgroups waits for the wave's
+// own memory operations and stamps the 100 MHz real-time counter at each
+// phase boundary.
+#ifdef RNT_PLANE_TRACE
+constexpr int kTraceWg = 4096, kTraceStamps = 16;
+__device__ uint64_t g_plane_trace[2 * kTraceWg * 16 * kTraceStamps];
+#define PLANE_STAMP(K, S)                                                                       \
+  do {                                                                                          \
+    const uint32_t wg_ = trace_id;                                                              \
+    if ((threadIdx.x & 63u) == 0 && wg_ < (uint32_t)kTraceWg) {                                 \
+      __builtin_amdgcn_s_waitcnt(0);                                                            \
+      g_plane_trace[(((K) * kTraceWg + wg_) * 16 + (threadIdx.x >> 6)) * kTraceStamps + (S)] =  \
+          __builtin_amdgcn_s_memrealtime();                                                     \
+    }                                                                                           \
+  } while (0)
+#else
+#define PLANE_STAMP(K, S) \
+  do {                    \
+  } while (0)
+#endif
+
+// Measurement builds (tools/build_variant.sh, wrong results by design):
+// RNT_PLANE_EXP bit 0: pass C / inverse pass C twiddles wave-uniform;
+// bit 1: no plane loads (synthetic words); bit 2: no plane stores.
+#ifndef RNT_PLANE_EXP
+#define RNT_PLANE_EXP 0
+#endif
+
+// Plane prefetch (persistent launches): while a workgroup finishes one
+// plane, the first half of its next input plane (L0 registers 0..31, the
+// plane's first 2^15 words) goes global -> LDS by DMA (no registers),
+// 1 KiB per wave instruction.  A CU pulls only about 10 B/clk from HBM, so
+// a plane load that starts cold takes ~11 us; with half of it already in
+// LDS the exposed part halves.  The caller has made the LDS free (barrier).
+__device__ __forceinline__ void plane_prefetch(uint32_t* lds, const uint32_t* src, uint32_t words, uint32_t t) {
+  const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), lam = t & 63u;
+  const uint32_t chunks = words >> 8;  // 256 words per wave instruction
+  for (uint32_t ch = w; ch < chunks; ch += 16u)
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + (ch << 8) + lam * 4u),
+                                     (__attribute__((address_space(3))) void*)(lds + (ch << 8)), 16, 0, 0);
 }
 
+// Load the L0 plane at src; with `have` the first half is waiting in LDS
+// (plane_prefetch).  Every wave waits for its own DMA, then the barrier
+// publishes all of it.
+__device__ __forceinline__ void plane_load(uint32_t (&x)[64], const uint32_t* src, const uint32_t* lds,
+                                           uint32_t t, bool have) {
+  const BufView<uint32_t> g(src, 1u << 16);
+  if constexpr ((RNT_PLANE_EXP & 2) != 0) {
+#pragma unroll
+    for (int r = 0; r < 64; ++r) x[r] = (t * 2654435761u + (uint32_t)r * 40503u) >> 2;
+    return;
+  }
+  if (have) {
+#pragma unroll
+    for (int r = 32; r < 64; ++r) x[r] = g.ld(t, (uint32_t)r << 10);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 32; ++r) x[r] = lds[((uint32_t)r << 10) | t];
+  } else {
+#pragma unroll
+    for (int r = 0; r < 64; ++r) x[r] = g.ld(t, (uint32_t)r << 10);
+  }
+}
+
+// The truncated forward transform of the plane in x (L0 in, L2 out).
+// pf_src (persistent launches): the plane to prefetch into LDS once X2 is
+// done, with pf_words of it, or null; PF: the LDS may hold a prefetched
+// plane that other waves are still reading when X1 starts.
+template <int K, bool PF>
+__device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint32_t t,
+                                          const Tw<uint32_t>* tw, const Mod<uint32_t>& mo,
+                                          const uint32_t* pf_src, uint32_t pf_words, uint32_t trace_id) {
+  (void)trace_id;
+  const uint32_t N = 1u << 16;
+  const TwScalar<uint32_t> tws{(const RNT_CONST_AS Tw<uint32_t>*)tw};
+  // pass A's twiddle nodes ((2^16 + i) >> (b + 1), b >= 10) depend on
+  // register bits only, pass B's (b >= 6) on register and wave bits: both
+  // wave-uniform (scalar loads)
+  plane_ct<0, 10, 5, 0, 32>(x, N, tws, mo);
+  PLANE_STAMP(K, 2);
+  plane_x1<true, PF>(x, lds, t);
+  PLANE_STAMP(K, 3);
+  const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
+  plane_ct<1, 6, 3, 0, 16>(x, N + (wu << 12), tws, mo);
+  PLANE_STAMP(K, 4);
+  plane_x2<true>(x, lds, t);
+  PLANE_STAMP(K, 5);
+  if (PF && pf_src != nullptr) {
+    __syncthreads();  // every wave is done with its X2 buffers
+    plane_prefetch(lds, pf_src, pf_words, t);
+  }
+  if constexpr ((RNT_PLANE_EXP & 1) != 0)
+    plane_ct<2, 0, 5, 2, 8>(x, N, tws, mo);
+  else
+    plane_ct<2, 0, 5, 2, 8>(x, N + (t << 6), tw, mo);
+  PLANE_STAMP(K, 6);
+}
+
+// Planes are numbered p = l * B + poly (limb-major, so concurrent
+// workgroups share one limb's twiddles in L2).  PF = false: one workgroup
+// per plane, grid (B, L).  PF = true: a persistent grid of one workgroup
+// per CU walks p = blockIdx.x, + gridDim.x, ... and prefetches each next
+// input plane's first half into LDS behind the current one.
+template <bool PF>
 __global__ void __launch_bounds__(plane::T, 1)
 k_plane_fwd(uint32_t* __restrict__ ahat, const uint32_t* __restrict__ a, TabPtrs<uint32_t> tp,
-            uint64_t ls, uint32_t stagger) {
+            uint64_t ls, uint32_t stagger, uint32_t B, uint32_t nplanes) {
   plane_stagger(stagger);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   uint32_t* lds = (uint32_t*)smem_raw;
-  const uint32_t t = threadIdx.x, p = blockIdx.x, l = blockIdx.y;
+  const uint32_t t = threadIdx.x;
   const uint64_t N = 1ull << 16;
-  const uint64_t off = (uint64_t)l * ls + (uint64_t)p * N;
-  const BufView<uint32_t> src(a + off, (uint32_t)N);
-  uint32_t x[64];
+  uint32_t p = PF ? blockIdx.x : blockIdx.x + blockIdx.y * B;
+  bool have = false;
+  for (;;) {
+    const uint32_t trace_id = p;
+    PLANE_STAMP(0, 0);
+    const uint32_t l = p / B, poly = p - l * B;
+    const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
+    const uint32_t pn = p + gridDim.x;
+    const uint32_t* pf = nullptr;
+    if (PF && pn < nplanes) {
+      const uint32_t ln = pn / B;
+      pf = a + (uint64_t)ln * ls + (uint64_t)(pn - ln * B) * N;
+    }
+    uint32_t x[64];
+    plane_load(x, a + off, lds, t, PF && have);
+    PLANE_STAMP(0, 1);
+    plane_fwd<0, PF>(x, lds, t, tp.tw + (uint64_t)l * N, mod_of(tp.lc[l]), pf, 1u << 15, trace_id);
+    // a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
+    uint4* dst = (uint4*)(ahat + off);
+    if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) break;
 #pragma unroll
-  for (int r = 0; r < 64; ++r) x[r] = src.ld(t, (uint32_t)r << 10);
-  const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
-  plane_fwd(x, lds, t, tw, mod_of(tp.lc[l]));
-  // a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
-  uint4* dst = (uint4*)(ahat + off);
-#pragma unroll
-  for (int kk = 0; kk < 16; ++kk)
-    dst[kk * 1024 + t] = make_uint4(x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)],
-                                    x[plane::slot2(4 * kk + 2)], x[plane::slot2(4 * kk + 3)]);
+    for (int kk = 0; kk < 16; ++kk)
+      dst[kk * 1024 + t] = make_uint4(x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)],
+                                      x[plane::slot2(4 * kk + 2)], x[plane::slot2(4 * kk + 3)]);
+    PLANE_STAMP(0, 7);
+    if (!PF || pf == nullptr) break;
+    p = pn;
+    have = true;
+  }
 }
 
+template <bool PF>
 __global__ void __launch_bounds__(plane::T, 1)
 k_plane_mul(uint32_t* __restrict__ c, const uint32_t* __restrict__ b, const uint32_t* __restrict__ ahat,
-            TabPtrs<uint32_t> tp, uint64_t ls, uint32_t stagger) {
+            TabPtrs<uint32_t> tp, uint64_t ls, uint32_t stagger, uint32_t B, uint32_t nplanes) {
   plane_stagger(stagger);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   uint32_t* lds = (uint32_t*)smem_raw;
-  const uint32_t t = threadIdx.x, p = blockIdx.x, l = blockIdx.y;
+  const uint32_t t = threadIdx.x;
   const uint64_t N = 1ull << 16;
-  const uint64_t off = (uint64_t)l * ls + (uint64_t)p * N;
-  const LimbConst<uint32_t> lc = tp.lc[l];
-  const Mod<uint32_t> mo = mod_of(lc);
-  const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
-  const Tw<uint32_t>* itw = tp.itw + (uint64_t)l * N;
-  uint32_t x[64];
-  {
-    const BufView<uint32_t> src(b + off, (uint32_t)N);
-#pragma unroll
-    for (int r = 0; r < 64; ++r) x[r] = src.ld(t, (uint32_t)r << 10);
-  }
-  plane_fwd(x, lds, t, tw, mo);
-  // degree-3 block products: block (t << 4) | kk, zeta = (-1)^kk psi_rev[N/8 + (t << 3) + kk/2]
-  const uint4* ah = (const uint4*)(ahat + off);
-  const uint32_t zb = (uint32_t)(N >> 3) + (t << 3);
   const uint32_t n0 = (uint32_t)N;
+  uint32_t p = PF ? blockIdx.x : blockIdx.x + blockIdx.y * B;
+  bool have = false;
+  for (;;) {
+    const uint32_t trace_id = p;
+    PLANE_STAMP(1, 0);
+    const uint32_t l = p / B, poly = p - l * B;
+    const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
+    const uint32_t pn = p + gridDim.x;
+    const uint32_t* pf = nullptr;
+    if (PF && pn < nplanes) {
+      const uint32_t ln = pn / B;
+      pf = b + (uint64_t)ln * ls + (uint64_t)(pn - ln * B) * N;
+    }
+    const LimbConst<uint32_t> lc = tp.lc[l];
+    const Mod<uint32_t> mo = mod_of(lc);
+    const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
+    const Tw<uint32_t>* itw = tp.itw + (uint64_t)l * N;
+    uint32_t x[64];
+    plane_load(x, b + off, lds, t, PF && have);
+    PLANE_STAMP(1, 1);
+    // PF: the first half of a^ (blocks kk < 8: its first 2^15 words) comes
+    // to LDS behind pass C
+    plane_fwd<1, PF>(x, lds, t, tw, mo, PF ? ahat + off : nullptr, 1u << 15, trace_id);
+    // degree-3 block products: block (t << 4) | kk, zeta = (-1)^kk psi_rev[N/8 + (t << 3) + kk/2]
+    const uint4* ah = (const uint4*)(ahat + off);
+    const uint32_t zb = (uint32_t)(N >> 3) + (t << 3);
+    if constexpr (PF) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk) {
-    const uint4 av = ah[kk * 1024 + t];
-    const uint32_t aa[4] = {av.x, av.y, av.z, av.w};
-    const uint32_t bb[4] = {x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
-                            x[plane::slot2(4 * kk + 3)]};
-    const Tw<uint32_t> w = tw[zb + (kk >> 1)];
-    const uint32_t zeta = (kk & 1) ? lc.q - w.w : w.w;
-    const uint32_t zeta_p = (kk & 1) ? ~w.p : w.p;
-    uint32_t cc[4];
-    mul_mod_x4(cc, aa, bb, zeta, zeta_p, lc.q, lc.qinv);
+    for (int kk = 0; kk < 16; ++kk) {
+      const uint4 av = (RNT_PLANE_EXP & 2) != 0 ? make_uint4(t * 7u + kk, t * 11u, t + 3u * kk, t ^ 0x55u)
+                       : (PF && kk < 8)           ? ((const uint4*)lds)[kk * 1024 + t]
+                                                  : ah[kk * 1024 + t];
+      const uint32_t aa[4] = {av.x, av.y, av.z, av.w};
+      const uint32_t bb[4] = {x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
+                              x[plane::slot2(4 * kk + 3)]};
+      const Tw<uint32_t> w = tw[zb + (kk >> 1)];
+      const uint32_t zeta = (kk & 1) ? lc.q - w.w : w.w;
+      const uint32_t zeta_p = (kk & 1) ? ~w.p : w.p;
+      uint32_t cc[4];
+      mul_mod_x4(cc, aa, bb, zeta, zeta_p, lc.q, lc.qinv);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = cc[e];
+      for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = cc[e];
+    }
+    PLANE_STAMP(1, 7);
+    if constexpr ((RNT_PLANE_EXP & 1) != 0)
+      plane_gs<2, 0, 2, 5, 8, false>(x, n0, TwScalar<uint32_t>{(const RNT_CONST_AS Tw<uint32_t>*)itw}, mo,
+                                     Fold<uint32_t>{});
+    else
+      plane_gs<2, 0, 2, 5, 8, false>(x, n0 + (t << 6), itw, mo, Fold<uint32_t>{});
+    PLANE_STAMP(1, 8);
+    if constexpr (PF) __syncthreads();  // every wave is done reading a^ from LDS
+    plane_x2<false>(x, lds, t);
+    PLANE_STAMP(1, 9);
+    const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
+    plane_gs<1, 6, 0, 3, 16, false>(x, n0 + (wu << 12), TwScalar<uint32_t>{(const RNT_CONST_AS Tw<uint32_t>*)itw},
+                                    mo, Fold<uint32_t>{});
+    PLANE_STAMP(1, 10);
+    plane_x1<false, true>(x, lds, t);  // ends with a barrier: the LDS is free
+    PLANE_STAMP(1, 11);
+    if (PF && pf != nullptr) plane_prefetch(lds, pf, 1u << 15, t);
+    plane_gs<0, 10, 0, 5, 32, true>(x, n0, TwScalar<uint32_t>{(const RNT_CONST_AS Tw<uint32_t>*)itw}, mo,
+                                    Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p});
+    PLANE_STAMP(1, 12);
+    const BufView<uint32_t> dst(c + off, (uint32_t)N);
+    if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) break;
+#pragma unroll
+    for (int r = 0; r < 64; ++r) dst.st(x[r], t, (uint32_t)r << 10);
+    PLANE_STAMP(1, 13);
+    if (!PF || pf == nullptr) break;
+    p = pn;
+    have = true;
   }
-  plane_gs<2, 0, 2, 4, 8, false>(x, n0 + (t << 6), itw, mo, Fold<uint32_t>{});
-  plane_xchg12<false>(x, lds, t);
-  plane_gs<1, 5, 0, 4, 8, false>(x, n0 + (((t >> 5) << 11) | (t & 31u)), itw, mo, Fold<uint32_t>{});
-  plane_xchg01<false>(x, lds, t);
-  plane_gs<0, 10, 0, 5, 32, true>(x, n0, TwScalar<uint32_t>{(const RNT_CONST_AS Tw<uint32_t>*)itw}, mo,
-                                  Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p});
-  const BufView<uint32_t> dst(c + off, (uint32_t)N);
-#pragma unroll
-  for (int r = 0; r < 64; ++r) dst.st(x[r], t, (uint32_t)r << 10);
 }
+
+#ifdef RNT_PLANE_TRACE
+extern "C" __attribute__((visibility("default"))) int rnt_debug_plane_trace(uint64_t* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_plane_trace), sizeof(g_plane_trace));
+}
+#endif
 
 // Words per padded LDS key row: C + C/16 (ks_pad's 4 per 64), rounded up to
 // a whole 16-byte unit (the host sizes the LDS with the same formula).
@@ -2334,22 +2500,41 @@ bool plane_ok(const Tables* t) {
   return t->plane && !t->wide && !lazy30_ok(t) && t->log_n == 16;
 }
 
+static int device_cus() {
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    return n;
+  }();
+  return cus;
+}
+
 hipError_t launch_plane(const Launch& k, int which, void* out, const void* in, const void* ahat,
                         uint64_t ls) {
   if (k.B == 0 || k.L == 0) return hipSuccess;
-  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  if (k.B > 0x7fffffffull || k.L > 65535 || k.B * k.L > 0xffffffffull) return hipErrorInvalidConfiguration;
   const size_t lds = (size_t)plane::LDS_WORDS * 4;
-  const dim3 grid((unsigned)k.B, (unsigned)k.L);
+  const uint32_t B = (uint32_t)k.B, np = (uint32_t)(k.B * k.L);
+  // persistent launches (RNT_PLANE=2): one workgroup per CU, never more
+  // workgroups than planes
+  const bool pf = k.t->plane >= 2;
+  const dim3 grid = pf ? dim3((unsigned)std::min<uint64_t>(np, (uint64_t)device_cus())) : dim3(B, (unsigned)k.L);
+  const uint32_t st = k.t->plane_stagger;
+  const uint32_t* src = (const uint32_t*)in;
   if (which == 0) {
-    hipError_t e = allow_lds(k_plane_fwd, lds);
+    auto fn = pf ? k_plane_fwd<true> : k_plane_fwd<false>;
+    hipError_t e = allow_lds(fn, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_plane_fwd, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)in,
-                       tab_ptrs<uint32_t>(k.t), ls, k.t->plane_stagger);
+    hipLaunchKernelGGL(fn, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, src, tab_ptrs<uint32_t>(k.t), ls, st, B,
+                       np);
   } else {
-    hipError_t e = allow_lds(k_plane_mul, lds);
+    auto fn = pf ? k_plane_mul<true> : k_plane_mul<false>;
+    hipError_t e = allow_lds(fn, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_plane_mul, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)in,
-                       (const uint32_t*)ahat, tab_ptrs<uint32_t>(k.t), ls, k.t->plane_stagger);
+    hipLaunchKernelGGL(fn, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, src, (const uint32_t*)ahat,
+                       tab_ptrs<uint32_t>(k.t), ls, st, B, np);
   }
   return hipGetLastError();
 }
