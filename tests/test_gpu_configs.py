@@ -93,9 +93,13 @@ def test_config5_rotation_full_32_limbs(gpu, k):
     assert np.array_equal(r.c1.channels(), w1)
 
 
-def test_metric_path_edge_operands(gpu):
+@pytest.mark.parametrize("plane", [None, "0"])
+def test_metric_path_edge_operands(gpu, monkeypatch, plane):
     """All-(q-1), zero and monomial operands through the default 31-bit
-    poly-mul (the metric's path), against the oracle."""
+    poly-mul (the metric's path: the fused whole-plane kernel), and through
+    the four-step kernels (RNT_PLANE=0), against the oracle."""
+    if plane is not None:
+        monkeypatch.setenv("RNT_PLANE", plane)
     rn = gpu
     n, L = 1 << 16, 16
     mod = rn.generate_primes(31, L, n)
@@ -123,11 +127,11 @@ def test_metric_path_edge_operands(gpu):
     assert np.array_equal(t.channels(), a.channels())
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["1", "3"])
 def test_plane_product_matches_oracle(gpu, monkeypatch, mode):
     """rnt_mul through the whole-plane kernels (k_plane_fwd + k_plane_mul,
-    N = 2^16, u32 canonical bases; RNT_PLANE=1 one workgroup per plane,
-    RNT_PLANE=2 persistent workgroups with LDS prefetch), bit-exact against
+    N = 2^16, u32 canonical bases; RNT_PLANE=1 two launches, RNT_PLANE=3
+    both halves in one workgroup), bit-exact against
     the oracle's poly.rs:307-329 product on random, all-(q-1), zero and
     negacyclic-monomial operands, and in both in-place forms."""
     monkeypatch.setenv("RNT_PLANE", mode)
@@ -158,12 +162,16 @@ def test_plane_product_matches_oracle(gpu, monkeypatch, mode):
     assert np.array_equal(b2.channels(), got)
 
 
-def test_metric_batch_1024_sampled_pairs(gpu):
+@pytest.mark.parametrize("plane", [None, "0"])
+def test_metric_batch_1024_sampled_pairs(gpu, monkeypatch, plane):
     """The metric's own shape and batch (N = 2^16, L = 16 x 31-bit, 1024
     pairs, operands drawn on the device as in bench.py): eight pairs --
     the first, the last, both sides of the 512 midpoint and four random
     ones -- bit-exact against the oracle's poly.rs:307-329 product, and the
-    same batch through the in-place form (a *= b, out aliasing a)."""
+    same batch through the in-place form (a *= b, out aliasing a); default
+    path and the four-step kernels (RNT_PLANE=0)."""
+    if plane is not None:
+        monkeypatch.setenv("RNT_PLANE", plane)
     rn = gpu
     n, L, B = 1 << 16, 16, 1024
     mod = rn.generate_primes(31, L, n)

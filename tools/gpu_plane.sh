@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 200 --timeout-method thread -k "plane or metric_path" > gpurun_out/plane_test.out 2>&1 || { tail -40 gpurun_out/plane_test.out; exit 1; }
 tail -3 gpurun_out/plane_test.out
 for i in 1 2; do
-  for v in 0 1 2; do
+  for v in ${MODES:-0 1 2}; do
     RNT_PLANE=$v timeout -k 10 200 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/ab_plane${v}_$i.json 2> gpurun_out/ab_plane${v}_$i.err || exit 1
     python3 -c "import json;d=json.loads(open('gpurun_out/ab_plane${v}_$i.json').read().splitlines()[-1]);print('plane=$v', round(d['value']), d['config']['parity_spot_check'], {k:round(v['avg_ms'],3) for k,v in d['roofline']['kernels'].items()}, d['power'])"
   done

@@ -83,7 +83,7 @@ thread_local Capture* g_capture = nullptr;
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
-    "sfft", "sample", "copy", "plane_fwd", "plane_mul"};
+    "sfft", "sample", "copy", "plane_fwd", "plane_mul", "plane_fused"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -632,7 +632,9 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     // RNT_LAZY30=0 keeps the canonical product path for 30-bit bases (A/B)
     t->lazy30 = !wide && lazy30 && env_long("RNT_LAZY30", 1) != 0;
     // RNT_PLANE=1: rnt_mul through the whole-plane kernels (N = 2^16, u32)
-    t->plane = (int)env_long("RNT_PLANE", 0);
+    // the whole-plane product is the default where it applies (plane_ok);
+    // RNT_PLANE=0 keeps the four-step kernels, 1 the two-launch plane path
+    t->plane = (int)env_long("RNT_PLANE", 3);
     t->plane_stagger = (uint32_t)env_long("RNT_PLANE_STAGGER", 0);
     {
       const long jg = env_long("RNT_DEC_JG", 0);  // A/B knob: 0 = auto, else 1..1024
@@ -1104,6 +1106,12 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   // pointwise product, inverse rows), the inverse column pass.
   const uint64_t ls = limb_stride(out);
   if (int rc = ensure_ws(out, poly_words(out) * word_bytes(k.t))) return rc;
+  if (rnt::plane_ok(k.t) && k.t->plane == 3) {
+    LAUNCH(k.t, rnt::K_PLANE_FUSED, rnt::launch_plane_fused(k, out->data, a->data, b->data, out->ws, ls),
+           "plane fused product");
+    out->in_ntt = 0;
+    return RNT_OK;
+  }
   if (rnt::plane_ok(k.t)) {
     // whole-plane product: a^ into the workspace, then b^ (x) a^ -> c
     LAUNCH(k.t, rnt::K_PLANE_FWD, rnt::launch_plane(k, 0, out->ws, a->data, nullptr, ls), "plane forward");

@@ -82,7 +82,7 @@ struct Tables {
   int wide = 0;            // 0: W = u32, 1: W = u64
   bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path
   int plane = 0;           // rnt_mul through the whole-plane kernels where plane_ok (RNT_PLANE:
-                           // 1 one workgroup per plane, 2 persistent with prefetch)
+                           // 1 two launches, 3 both halves in one workgroup)
   uint32_t plane_stagger = 0;  // their first-wave phase shift, 100 MHz ticks (RNT_PLANE_STAGGER)
   uint32_t dec_jg = 0;     // key-switch decomposition: target limbs per workgroup (0 = auto)
   size_t ks_ws_bytes = (size_t)4096 << 20;  // key-switch scratch cap per chunk (RNT_KS_WS_MB)
@@ -116,7 +116,7 @@ struct Tables {
 enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
-  K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FWD, K_PLANE_MUL, K_COUNT
+  K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FWD, K_PLANE_MUL, K_PLANE_FUSED, K_COUNT
 };
 
 struct Prof {
@@ -198,6 +198,7 @@ hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_
 bool plane_ok(const Tables* t);
 hipError_t launch_plane(const Launch& k, int which, void* out, const void* in, const void* ahat,
                         uint64_t ls);
+hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls);
 // Whether rnt_mul's row kernel stops its transforms two stages early and
 // multiplies degree-3 residues (u32 canonical bases, row length 2^(4k));
 // its inverse column pass then takes rfold = 2.

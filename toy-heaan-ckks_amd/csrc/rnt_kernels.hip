@@ -1035,6 +1035,9 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
 //      buffer in four rounds, with no workgroup barrier.
 // The physical register of a logical one is a compile-time permutation
 // (slot1, shared by L1 and L2).
+#ifndef RNT_PLANE_EXP
+#define RNT_PLANE_EXP 0
+#endif
 namespace plane {
 constexpr int T = 1024;
 constexpr int XS = 17;                  // X2 buffer row stride (words): conflict-free both ways
@@ -1064,7 +1067,8 @@ __device__ __forceinline__ void plane_ct_chunks(uint32_t (&x)[64], uint32_t nb, 
   constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
   Tw<uint32_t> t[n];
 #pragma unroll
-  for (int j = 0; j < n; ++j) t[j] = tw_get<uint32_t>(tw, nb, (uint32_t)(M0 + j));
+  for (int j = 0; j < n; ++j)
+    t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_get<uint32_t>(tw, nb, (uint32_t)(M0 + j));
 #pragma unroll
   for (int j = 0; j < n; ++j) {
 #pragma unroll
@@ -1094,7 +1098,8 @@ __device__ __forceinline__ void plane_gs_chunks(uint32_t (&x)[64], uint32_t nb, 
   constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
   Tw<uint32_t> t[n];
 #pragma unroll
-  for (int j = 0; j < n; ++j) t[j] = tw_get<uint32_t>(itw, nb, (uint32_t)(M0 + j));
+  for (int j = 0; j < n; ++j)
+    t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_get<uint32_t>(itw, nb, (uint32_t)(M0 + j));
 #pragma unroll
   for (int j = 0; j < n; ++j) {
 #pragma unroll
@@ -1130,6 +1135,7 @@ __device__ __forceinline__ void plane_gs(uint32_t (&x)[64], uint32_t node0, cons
 template <bool TO_L1, bool SYNC_FIRST>
 __device__ __forceinline__ void plane_x1(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
   const uint32_t w = t >> 6, lam = t & 63u;
+  if constexpr ((RNT_PLANE_EXP & 16) != 0) return;
   if constexpr (SYNC_FIRST) __syncthreads();
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -1180,6 +1186,7 @@ __device__ __forceinline__ void plane_swap54(uint32_t (&x)[64]) {
 template <bool TO_L2>
 __device__ __forceinline__ void plane_x2(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
   const uint32_t w = t >> 6, lam = t & 63u;
+  if constexpr ((RNT_PLANE_EXP & 16) != 0) return;
   if constexpr (TO_L2) plane_swap54(x);
   const uint32_t a15 = lam * plane::XS;                          // + (m & 15)
   const uint32_t a2 = (lam & 48u) * plane::XS + (lam & 15u);     // + c * XS
@@ -1236,57 +1243,27 @@ __device__ uint64_t g_plane_trace[2 * kTraceWg * 16 * kTraceStamps];
 
 // Measurement builds (tools/build_variant.sh, wrong results by design):
 // RNT_PLANE_EXP bit 0: pass C / inverse pass C twiddles wave-uniform;
-// bit 1: no plane loads (synthetic words); bit 2: no plane stores.
-#ifndef RNT_PLANE_EXP
-#define RNT_PLANE_EXP 0
-#endif
+// bit 1: no plane loads (synthetic words); bit 2: no plane stores;
+// bit 3: no twiddle loads in the passes (one constant); bit 4: no X1 / X2.
 
-// Plane prefetch (persistent launches): while a workgroup finishes one
-// plane, the first half of its next input plane (L0 registers 0..31, the
-// plane's first 2^15 words) goes global -> LDS by DMA (no registers),
-// 1 KiB per wave instruction.  A CU pulls only about 10 B/clk from HBM, so
-// a plane load that starts cold takes ~11 us; with half of it already in
-// LDS the exposed part halves.  The caller has made the LDS free (barrier).
-__device__ __forceinline__ void plane_prefetch(uint32_t* lds, const uint32_t* src, uint32_t words, uint32_t t) {
-  const uint32_t w = __builtin_amdgcn_readfirstlane(t >> 6), lam = t & 63u;
-  const uint32_t chunks = words >> 8;  // 256 words per wave instruction
-  for (uint32_t ch = w; ch < chunks; ch += 16u)
-    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + (ch << 8) + lam * 4u),
-                                     (__attribute__((address_space(3))) void*)(lds + (ch << 8)), 16, 0, 0);
-}
-
-// Load the L0 plane at src; with `have` the first half is waiting in LDS
-// (plane_prefetch).  Every wave waits for its own DMA, then the barrier
-// publishes all of it.
-__device__ __forceinline__ void plane_load(uint32_t (&x)[64], const uint32_t* src, const uint32_t* lds,
-                                           uint32_t t, bool have) {
-  const BufView<uint32_t> g(src, 1u << 16);
+// Load the L0 plane at src (64 coalesced dword loads a thread).
+__device__ __forceinline__ void plane_load(uint32_t (&x)[64], const uint32_t* src, uint32_t t) {
   if constexpr ((RNT_PLANE_EXP & 2) != 0) {
 #pragma unroll
     for (int r = 0; r < 64; ++r) x[r] = (t * 2654435761u + (uint32_t)r * 40503u) >> 2;
     return;
   }
-  if (have) {
+  const BufView<uint32_t> g(src, 1u << 16);
 #pragma unroll
-    for (int r = 32; r < 64; ++r) x[r] = g.ld(t, (uint32_t)r << 10);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 32; ++r) x[r] = lds[((uint32_t)r << 10) | t];
-  } else {
-#pragma unroll
-    for (int r = 0; r < 64; ++r) x[r] = g.ld(t, (uint32_t)r << 10);
-  }
+  for (int r = 0; r < 64; ++r) x[r] = g.ld(t, (uint32_t)r << 10);
 }
 
 // The truncated forward transform of the plane in x (L0 in, L2 out).
-// pf_src (persistent launches): the plane to prefetch into LDS once X2 is
-// done, with pf_words of it, or null; PF: the LDS may hold a prefetched
-// plane that other waves are still reading when X1 starts.
-template <int K, bool PF>
+// SYNC1: other waves may still be using the LDS (their X2 buffers of an
+// earlier transform) when X1 starts.
+template <int K, bool SYNC1>
 __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint32_t t,
-                                          const Tw<uint32_t>* tw, const Mod<uint32_t>& mo,
-                                          const uint32_t* pf_src, uint32_t pf_words, uint32_t trace_id) {
+                                          const Tw<uint32_t>* tw, const Mod<uint32_t>& mo, uint32_t trace_id) {
   (void)trace_id;
   const uint32_t N = 1u << 16;
   const TwScalar<uint32_t> tws{(const RNT_CONST_AS Tw<uint32_t>*)tw};
@@ -1295,17 +1272,13 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   // wave-uniform (scalar loads)
   plane_ct<0, 10, 5, 0, 32>(x, N, tws, mo);
   PLANE_STAMP(K, 2);
-  plane_x1<true, PF>(x, lds, t);
+  plane_x1<true, SYNC1>(x, lds, t);
   PLANE_STAMP(K, 3);
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
   plane_ct<1, 6, 3, 0, 16>(x, N + (wu << 12), tws, mo);
   PLANE_STAMP(K, 4);
   plane_x2<true>(x, lds, t);
   PLANE_STAMP(K, 5);
-  if (PF && pf_src != nullptr) {
-    __syncthreads();  // every wave is done with its X2 buffers
-    plane_prefetch(lds, pf_src, pf_words, t);
-  }
   if constexpr ((RNT_PLANE_EXP & 1) != 0)
     plane_ct<2, 0, 5, 2, 8>(x, N, tws, mo);
   else
@@ -1313,136 +1286,132 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   PLANE_STAMP(K, 6);
 }
 
-// Planes are numbered p = l * B + poly (limb-major, so concurrent
-// workgroups share one limb's twiddles in L2).  PF = false: one workgroup
-// per plane, grid (B, L).  PF = true: a persistent grid of one workgroup
-// per CU walks p = blockIdx.x, + gridDim.x, ... and prefetches each next
-// input plane's first half into LDS behind the current one.
-template <bool PF>
-__global__ void __launch_bounds__(plane::T, 1)
-k_plane_fwd(uint32_t* __restrict__ ahat, const uint32_t* __restrict__ a, TabPtrs<uint32_t> tp,
-            uint64_t ls, uint32_t stagger, uint32_t B, uint32_t nplanes) {
-  plane_stagger(stagger);
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  uint32_t* lds = (uint32_t*)smem_raw;
-  const uint32_t t = threadIdx.x;
-  const uint64_t N = 1ull << 16;
-  uint32_t p = PF ? blockIdx.x : blockIdx.x + blockIdx.y * B;
-  bool have = false;
-  for (;;) {
-    const uint32_t trace_id = p;
-    PLANE_STAMP(0, 0);
-    const uint32_t l = p / B, poly = p - l * B;
-    const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
-    const uint32_t pn = p + gridDim.x;
-    const uint32_t* pf = nullptr;
-    if (PF && pn < nplanes) {
-      const uint32_t ln = pn / B;
-      pf = a + (uint64_t)ln * ls + (uint64_t)(pn - ln * B) * N;
-    }
-    uint32_t x[64];
-    plane_load(x, a + off, lds, t, PF && have);
-    PLANE_STAMP(0, 1);
-    plane_fwd<0, PF>(x, lds, t, tp.tw + (uint64_t)l * N, mod_of(tp.lc[l]), pf, 1u << 15, trace_id);
-    // a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
-    uint4* dst = (uint4*)(ahat + off);
-    if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) break;
+// The rest of the product once b^ is in x (L2): the degree-3 block
+// products with a^ (ah: the private layout, block kk of thread t at
+// ah[kk * 1024 + t]), the whole truncated inverse, c stored in L0.
+template <int K>
+__device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds, uint32_t t, const uint4* ah,
+                                               uint32_t* c, const Tw<uint32_t>* tw, const Tw<uint32_t>* itw,
+                                               const LimbConst<uint32_t>& lc, const Mod<uint32_t>& mo,
+                                               uint32_t trace_id) {
+  (void)trace_id;
+  const uint32_t n0 = 1u << 16;
+  // degree-3 block products: block (t << 4) | kk, zeta = (-1)^kk psi_rev[N/8 + (t << 3) + kk/2]
+  const uint32_t zb = (n0 >> 3) + (t << 3);
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk)
-      dst[kk * 1024 + t] = make_uint4(x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)],
-                                      x[plane::slot2(4 * kk + 2)], x[plane::slot2(4 * kk + 3)]);
-    PLANE_STAMP(0, 7);
-    if (!PF || pf == nullptr) break;
-    p = pn;
-    have = true;
+  for (int kk = 0; kk < 16; ++kk) {
+    const uint4 av = (RNT_PLANE_EXP & 2) != 0 ? make_uint4(t * 7u + kk, t * 11u, t + 3u * kk, t ^ 0x55u)
+                                              : ah[kk * 1024 + t];
+    const uint32_t aa[4] = {av.x, av.y, av.z, av.w};
+    const uint32_t bb[4] = {x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
+                            x[plane::slot2(4 * kk + 3)]};
+    const Tw<uint32_t> w = tw[zb + (kk >> 1)];
+    const uint32_t zeta = (kk & 1) ? lc.q - w.w : w.w;
+    const uint32_t zeta_p = (kk & 1) ? ~w.p : w.p;
+    uint32_t cc[4];
+    mul_mod_x4(cc, aa, bb, zeta, zeta_p, lc.q, lc.qinv);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = cc[e];
   }
+  PLANE_STAMP(K, 7);
+  const TwScalar<uint32_t> itws{(const RNT_CONST_AS Tw<uint32_t>*)itw};
+  if constexpr ((RNT_PLANE_EXP & 1) != 0)
+    plane_gs<2, 0, 2, 5, 8, false>(x, n0, itws, mo, Fold<uint32_t>{});
+  else
+    plane_gs<2, 0, 2, 5, 8, false>(x, n0 + (t << 6), itw, mo, Fold<uint32_t>{});
+  PLANE_STAMP(K, 8);
+  plane_x2<false>(x, lds, t);
+  PLANE_STAMP(K, 9);
+  const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
+  plane_gs<1, 6, 0, 3, 16, false>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+  PLANE_STAMP(K, 10);
+  plane_x1<false, true>(x, lds, t);  // other waves may still be in their X2
+  PLANE_STAMP(K, 11);
+  plane_gs<0, 10, 0, 5, 32, true>(x, n0, itws, mo, Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p});
+  PLANE_STAMP(K, 12);
+  if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) return;
+  const BufView<uint32_t> dst(c, n0);
+#pragma unroll
+  for (int r = 0; r < 64; ++r) dst.st(x[r], t, (uint32_t)r << 10);
+  PLANE_STAMP(K, 13);
 }
 
-template <bool PF>
+// a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
+__device__ __forceinline__ void plane_store_hat(uint4* dst, const uint32_t (&x)[64], uint32_t t) {
+  if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) return;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk)
+    dst[kk * 1024 + t] = make_uint4(x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)],
+                                    x[plane::slot2(4 * kk + 2)], x[plane::slot2(4 * kk + 3)]);
+}
+
+// One workgroup per plane, grid (B, L).
 __global__ void __launch_bounds__(plane::T, 1)
-k_plane_mul(uint32_t* __restrict__ c, const uint32_t* __restrict__ b, const uint32_t* __restrict__ ahat,
-            TabPtrs<uint32_t> tp, uint64_t ls, uint32_t stagger, uint32_t B, uint32_t nplanes) {
+k_plane_fwd(uint32_t* __restrict__ ahat, const uint32_t* __restrict__ a, TabPtrs<uint32_t> tp, uint64_t ls,
+            uint32_t stagger) {
   plane_stagger(stagger);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   uint32_t* lds = (uint32_t*)smem_raw;
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
+  const uint32_t trace_id = poly + l * gridDim.x;
+  PLANE_STAMP(0, 0);
   const uint64_t N = 1ull << 16;
-  const uint32_t n0 = (uint32_t)N;
-  uint32_t p = PF ? blockIdx.x : blockIdx.x + blockIdx.y * B;
-  bool have = false;
-  for (;;) {
-    const uint32_t trace_id = p;
-    PLANE_STAMP(1, 0);
-    const uint32_t l = p / B, poly = p - l * B;
-    const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
-    const uint32_t pn = p + gridDim.x;
-    const uint32_t* pf = nullptr;
-    if (PF && pn < nplanes) {
-      const uint32_t ln = pn / B;
-      pf = b + (uint64_t)ln * ls + (uint64_t)(pn - ln * B) * N;
-    }
-    const LimbConst<uint32_t> lc = tp.lc[l];
-    const Mod<uint32_t> mo = mod_of(lc);
-    const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
-    const Tw<uint32_t>* itw = tp.itw + (uint64_t)l * N;
-    uint32_t x[64];
-    plane_load(x, b + off, lds, t, PF && have);
-    PLANE_STAMP(1, 1);
-    // PF: the first half of a^ (blocks kk < 8: its first 2^15 words) comes
-    // to LDS behind pass C
-    plane_fwd<1, PF>(x, lds, t, tw, mo, PF ? ahat + off : nullptr, 1u << 15, trace_id);
-    // degree-3 block products: block (t << 4) | kk, zeta = (-1)^kk psi_rev[N/8 + (t << 3) + kk/2]
-    const uint4* ah = (const uint4*)(ahat + off);
-    const uint32_t zb = (uint32_t)(N >> 3) + (t << 3);
-    if constexpr (PF) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      const uint4 av = (RNT_PLANE_EXP & 2) != 0 ? make_uint4(t * 7u + kk, t * 11u, t + 3u * kk, t ^ 0x55u)
-                       : (PF && kk < 8)           ? ((const uint4*)lds)[kk * 1024 + t]
-                                                  : ah[kk * 1024 + t];
-      const uint32_t aa[4] = {av.x, av.y, av.z, av.w};
-      const uint32_t bb[4] = {x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
-                              x[plane::slot2(4 * kk + 3)]};
-      const Tw<uint32_t> w = tw[zb + (kk >> 1)];
-      const uint32_t zeta = (kk & 1) ? lc.q - w.w : w.w;
-      const uint32_t zeta_p = (kk & 1) ? ~w.p : w.p;
-      uint32_t cc[4];
-      mul_mod_x4(cc, aa, bb, zeta, zeta_p, lc.q, lc.qinv);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = cc[e];
-    }
-    PLANE_STAMP(1, 7);
-    if constexpr ((RNT_PLANE_EXP & 1) != 0)
-      plane_gs<2, 0, 2, 5, 8, false>(x, n0, TwScalar<uint32_t>{(const RNT_CONST_AS Tw<uint32_t>*)itw}, mo,
-                                     Fold<uint32_t>{});
-    else
-      plane_gs<2, 0, 2, 5, 8, false>(x, n0 + (t << 6), itw, mo, Fold<uint32_t>{});
-    PLANE_STAMP(1, 8);
-    if constexpr (PF) __syncthreads();  // every wave is done reading a^ from LDS
-    plane_x2<false>(x, lds, t);
-    PLANE_STAMP(1, 9);
-    const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
-    plane_gs<1, 6, 0, 3, 16, false>(x, n0 + (wu << 12), TwScalar<uint32_t>{(const RNT_CONST_AS Tw<uint32_t>*)itw},
-                                    mo, Fold<uint32_t>{});
-    PLANE_STAMP(1, 10);
-    plane_x1<false, true>(x, lds, t);  // ends with a barrier: the LDS is free
-    PLANE_STAMP(1, 11);
-    if (PF && pf != nullptr) plane_prefetch(lds, pf, 1u << 15, t);
-    plane_gs<0, 10, 0, 5, 32, true>(x, n0, TwScalar<uint32_t>{(const RNT_CONST_AS Tw<uint32_t>*)itw}, mo,
-                                    Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p});
-    PLANE_STAMP(1, 12);
-    const BufView<uint32_t> dst(c + off, (uint32_t)N);
-    if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) break;
-#pragma unroll
-    for (int r = 0; r < 64; ++r) dst.st(x[r], t, (uint32_t)r << 10);
-    PLANE_STAMP(1, 13);
-    if (!PF || pf == nullptr) break;
-    p = pn;
-    have = true;
-  }
+  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
+  uint32_t x[64];
+  plane_load(x, a + off, t);
+  PLANE_STAMP(0, 1);
+  plane_fwd<0, false>(x, lds, t, tp.tw + (uint64_t)l * N, mod_of(tp.lc[l]), trace_id);
+  plane_store_hat((uint4*)(ahat + off), x, t);
+  PLANE_STAMP(0, 7);
+}
+
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_mul(uint32_t* __restrict__ c, const uint32_t* __restrict__ b, const uint32_t* __restrict__ ahat,
+            TabPtrs<uint32_t> tp, uint64_t ls, uint32_t stagger) {
+  plane_stagger(stagger);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
+  const uint32_t trace_id = poly + l * gridDim.x;
+  PLANE_STAMP(1, 0);
+  const uint64_t N = 1ull << 16;
+  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
+  const LimbConst<uint32_t> lc = tp.lc[l];
+  const Mod<uint32_t> mo = mod_of(lc);
+  const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
+  uint32_t x[64];
+  plane_load(x, b + off, t);
+  PLANE_STAMP(1, 1);
+  plane_fwd<1, false>(x, lds, t, tw, mo, trace_id);
+  plane_mul_tail<1>(x, lds, t, (const uint4*)(ahat + off), c + off, tw, tp.itw + (uint64_t)l * N, lc, mo, trace_id);
+}
+
+// Both halves in one workgroup (RNT_PLANE=3): a -> a^ through the scratch
+// plane, which the same threads read back ~40 us later (so the read is
+// served by the Infinity Cache or L2 rather than HBM), then b -> c as
+// k_plane_mul.  One launch per batch; the store of a^ and the load of b
+// are back to back and overlap.
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_fused(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
+              TabPtrs<uint32_t> tp, uint64_t ls) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
+  const uint32_t trace_id = poly + l * gridDim.x;
+  const uint64_t N = 1ull << 16;
+  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
+  const LimbConst<uint32_t> lc = tp.lc[l];
+  const Mod<uint32_t> mo = mod_of(lc);
+  const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
+  uint4* ah = (uint4*)(scratch + off);
+  uint32_t x[64];
+  plane_load(x, a + off, t);
+  plane_fwd<0, false>(x, lds, t, tw, mo, trace_id);
+  plane_store_hat(ah, x, t);
+  plane_load(x, b + off, t);
+  plane_fwd<1, true>(x, lds, t, tw, mo, trace_id);
+  // a^ comes back from this thread's own stores above
+  plane_mul_tail<1>(x, lds, t, ah, c + off, tw, tp.itw + (uint64_t)l * N, lc, mo, trace_id);
 }
 
 #ifdef RNT_PLANE_TRACE
@@ -2496,46 +2465,42 @@ hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* ou
 }
 // The whole-plane product (k_plane_fwd + k_plane_mul) serves rnt_mul for
 // u32 canonical bases at N = 2^16 when Tables::plane is set (RNT_PLANE).
+// The whole-plane kernels take every u32 basis at N = 2^16 (their
+// canonical arithmetic holds for any q < 2^31, so 30-bit bases too: 131k
+// against the lazy four-step kernels' 114k products/s).
 bool plane_ok(const Tables* t) {
-  return t->plane && !t->wide && !lazy30_ok(t) && t->log_n == 16;
-}
-
-static int device_cus() {
-  static int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-    return n;
-  }();
-  return cus;
+  return t->plane != 0 && !t->wide && t->log_n == 16;
 }
 
 hipError_t launch_plane(const Launch& k, int which, void* out, const void* in, const void* ahat,
                         uint64_t ls) {
   if (k.B == 0 || k.L == 0) return hipSuccess;
-  if (k.B > 0x7fffffffull || k.L > 65535 || k.B * k.L > 0xffffffffull) return hipErrorInvalidConfiguration;
+  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
   const size_t lds = (size_t)plane::LDS_WORDS * 4;
-  const uint32_t B = (uint32_t)k.B, np = (uint32_t)(k.B * k.L);
-  // persistent launches (RNT_PLANE=2): one workgroup per CU, never more
-  // workgroups than planes
-  const bool pf = k.t->plane >= 2;
-  const dim3 grid = pf ? dim3((unsigned)std::min<uint64_t>(np, (uint64_t)device_cus())) : dim3(B, (unsigned)k.L);
+  const dim3 grid((unsigned)k.B, (unsigned)k.L);
   const uint32_t st = k.t->plane_stagger;
-  const uint32_t* src = (const uint32_t*)in;
   if (which == 0) {
-    auto fn = pf ? k_plane_fwd<true> : k_plane_fwd<false>;
-    hipError_t e = allow_lds(fn, lds);
+    hipError_t e = allow_lds(k_plane_fwd, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(fn, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, src, tab_ptrs<uint32_t>(k.t), ls, st, B,
-                       np);
+    hipLaunchKernelGGL(k_plane_fwd, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)in,
+                       tab_ptrs<uint32_t>(k.t), ls, st);
   } else {
-    auto fn = pf ? k_plane_mul<true> : k_plane_mul<false>;
-    hipError_t e = allow_lds(fn, lds);
+    hipError_t e = allow_lds(k_plane_mul, lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(fn, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, src, (const uint32_t*)ahat,
-                       tab_ptrs<uint32_t>(k.t), ls, st, B, np);
+    hipLaunchKernelGGL(k_plane_mul, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)in,
+                       (const uint32_t*)ahat, tab_ptrs<uint32_t>(k.t), ls, st);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls) {
+  if (k.B == 0 || k.L == 0) return hipSuccess;
+  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  const size_t lds = (size_t)plane::LDS_WORDS * 4;
+  hipError_t e = allow_lds(k_plane_fused, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_plane_fused, dim3((unsigned)k.B, (unsigned)k.L), dim3(plane::T), lds, k.s, (uint32_t*)out,
+                     (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)scratch, tab_ptrs<uint32_t>(k.t), ls);
   return hipGetLastError();
 }
 
