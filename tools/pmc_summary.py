@@ -23,7 +23,13 @@ FN = {"k_colt_fwd": "col_fwd", "k_colt_inv": "col_inv", "k_ks_rows": "ks_rows",
 ROW_MODES = {"0": "row_fwd", "1": "row_inv", "2": "row_mul"}
 
 
+PLANE = {"k_plane_fwd": "plane_fwd", "k_plane_mul": "plane_mul", "k_plane_fused": "plane_fused"}
+
+
 def short(kname):
+    m = re.search(r"\b(k_plane_\w+)\(", kname)
+    if m:
+        return PLANE.get(m.group(1))
     m = re.search(r"(k_\w+)<([^>]*)>", kname)
     if not m or not m.group(2).startswith("unsigned int"):
         return None

@@ -1410,8 +1410,12 @@ k_plane_fused(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, ui
   plane_store_hat(ah, x, t);
   plane_load(x, b + off, t);
   plane_fwd<1, true>(x, lds, t, tw, mo, trace_id);
-  // a^ comes back from this thread's own stores above
-  plane_mul_tail<1>(x, lds, t, ah, c + off, tw, tp.itw + (uint64_t)l * N, lc, mo, trace_id);
+  // a^ comes back from this thread's own stores above; an opaque copy of
+  // the base keeps the compiler from holding the 16 store addresses live
+  // (in scratch) across b's transform
+  const uint4* ah2 = ah;
+  asm volatile("" : "+s"(ah2));
+  plane_mul_tail<1>(x, lds, t, ah2, c + off, tw, tp.itw + (uint64_t)l * N, lc, mo, trace_id);
 }
 
 #ifdef RNT_PLANE_TRACE
