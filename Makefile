@@ -11,7 +11,11 @@ CFLAGS   := -O2 -fPIC -std=c11 -Wall -pthread
 
 all: $(LIBDIR)/librnsntt.so oracle/liboracle.so
 
-$(LIBDIR)/rnt_kernels.o: $(CSRC)/rnt_kernels.hip $(CSRC)/rnt_internal.hpp $(CSRC)/rnt_modarith.hpp
+$(LIBDIR)/rnt_kernels.o: $(CSRC)/rnt_kernels.hip $(CSRC)/rnt_internal.hpp $(CSRC)/rnt_modarith.hpp $(CSRC)/rnt_device.hpp
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/rnt_plane.o: $(CSRC)/rnt_plane.hip $(CSRC)/rnt_internal.hpp $(CSRC)/rnt_modarith.hpp $(CSRC)/rnt_device.hpp
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -27,7 +31,7 @@ $(LIBDIR)/rnt_api.o: $(CSRC)/rnt_api.cpp $(CSRC)/rnt_internal.hpp $(CSRC)/rnt_ho
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBDIR)/librnsntt.so: $(LIBDIR)/rnt_kernels.o $(LIBDIR)/rnt_encode.o $(LIBDIR)/rnt_sample.o $(LIBDIR)/rnt_api.o
+$(LIBDIR)/librnsntt.so: $(LIBDIR)/rnt_kernels.o $(LIBDIR)/rnt_plane.o $(LIBDIR)/rnt_encode.o $(LIBDIR)/rnt_sample.o $(LIBDIR)/rnt_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 oracle/liboracle.so: oracle/oracle.c oracle/oracle.h

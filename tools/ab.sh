@@ -8,13 +8,16 @@ set -o pipefail
 mkdir -p gpurun_out
 REPS=$1; shift
 VARS=${@:-base}
+# AB_POWER=1 keeps the bench's power probe (3 s more per run)
+POWER_ARG=--no-power
+[ "${AB_POWER:-0}" = "1" ] && POWER_ARG=
 for i in $(seq 1 $REPS); do
   for v in $VARS; do
     IFS='+' read -ra parts <<< "$v"
     libname=${parts[0]}
     if [ "$libname" = base ]; then lib=toy-heaan-ckks_amd/lib/librnsntt.so; else lib=toy-heaan-ckks_amd/lib/variants/librnsntt_$libname.so; fi
     tag=$(echo "${AB_TAG:-}$v" | tr '+=' '__')
-    env RNSNTT_LIB=$lib "${parts[@]:1}" timeout -k 10 300 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-power $BENCH_ARGS > gpurun_out/ab_${tag}_$i.json 2> gpurun_out/ab_${tag}_$i.err || exit $?
+    env RNSNTT_LIB=$lib "${parts[@]:1}" timeout -k 10 300 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline $POWER_ARG $BENCH_ARGS > gpurun_out/ab_${tag}_$i.json 2> gpurun_out/ab_${tag}_$i.err || exit $?
   done
 done
 for v in $VARS; do tag=$(echo "${AB_TAG:-}$v" | tr '+=' '__'); echo "== $v" >&2; python3 tools/ab_summary.py gpurun_out/ab_${tag}_[0-9]*.json >&2; done

@@ -1,0 +1,679 @@
+// rnt_plane.hip -- the whole-plane poly-mul (rnt_mul at N = 2^16, u32 bases).
+//
+// Reference unit: one coefficient-domain `a *= &b`
+// (src/rings/backends/rns_ntt/poly.rs:307-329: to_ntt_domain of both
+// operands, the pointwise mul_mod, to_coeff_domain), computed for a batch of
+// (poly, limb) planes with the same merged negacyclic CT / GS network as the
+// four-step kernels in rnt_kernels.hip, so the result is word-for-word the
+// same (and the reference's).
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "rnt_internal.hpp"
+#include "rnt_modarith.hpp"
+#include "rnt_device.hpp"
+#include "rnt_bfly4.hpp"
+
+namespace rnt {
+
+// ---- whole-plane product (rnt_mul at N = 2^16, u32 canonical bases) ------
+// Two launches per batch instead of three, 5 planes of HBM traffic per
+// (poly, limb) instead of 9 (the 5-plane traffic measured
+// 142k poly-muls/s against 122k for the shipped 9):
+//   k_plane_fwd: a -> a^ (the whole truncated forward transform of one
+//                plane in one workgroup's registers; a^ goes to a private
+//                layout), 2 planes;
+//   k_plane_mul: b -> b^ the same way, a^ (x) b^ (degree-3 block products),
+//                the whole truncated inverse, c, 3 planes.
+// A workgroup = 1024 threads holds one 2^16-word plane, 64 words a thread.
+// Thread t = (w << 6) | lam (wave w, lane lam); the 16-bit index i is split
+// three ways:
+//   L0  i = (r << 10) | (w << 6) | lam     registers: bits 15..10, coalesced
+//   L1  i = (w << 12) | (r << 6) | lam     registers: bits 11..6
+//   L2  i = (w << 12) | (lam << 6) | r     registers: bits 5..0
+// and the network is the same merged negacyclic CT / GS heap as the
+// four-step kernels (node = (2^16 + i) >> (b + 1) at bit b), so a^ and the
+// product equal theirs word for word.  Pass A runs bits 15..10 in L0, pass
+// B bits 9..6 in L1 (both with wave-uniform twiddle nodes: scalar loads),
+// pass C bits 5..2 in L2 (bits 1..0 are the truncated stages).
+//   X1 (L0 <-> L1) keeps the lanes and moves words between waves: 128 KiB
+//      of LDS in two rounds, split on index bit 10 (a register bit on both
+//      sides, so a round reads back exactly the registers it wrote).
+//   X2 (L1 <-> L2) stays inside each wave: lane bits 5, 4 trade places with
+//      register bits 5, 4 through v_permlane32_swap / v_permlane16_swap,
+//      and the remaining 16 x 16 transposes go through a wave-private LDS
+//      buffer in four rounds, with no workgroup barrier.
+// The physical register of a logical one is a compile-time permutation
+// (slot1, shared by L1 and L2).
+#ifndef RNT_PLANE_EXP
+#define RNT_PLANE_EXP 0
+#endif
+namespace plane {
+constexpr int T = 1024;
+constexpr int XS = 17;                  // X2 buffer row stride (words): conflict-free both ways
+constexpr int XW = 64 * XS;             // words of one X2 buffer
+constexpr int LDS_WORDS = 16 * 2 * XW;  // two X2 buffers per wave; >= 2^15 (an X1 round)
+static_assert(LDS_WORDS >= (1 << 15), "X1 round");
+__host__ __device__ constexpr int slot0(int r) { return r; }
+__host__ __device__ constexpr int slot1(int r) { return 2 * (((r >> 5) << 4) | (r & 15)) + ((r >> 4) & 1); }
+__host__ __device__ constexpr int slot2(int r) { return slot1(r); }
+template <int L>
+__host__ __device__ constexpr int slot(int r) {
+  return L == 0 ? slot0(r) : slot1(r);
+}
+}  // namespace plane
+
+// CT stages on logical register bits SLHI .. SLLO of layout LY (index bits
+// [BB, BB + 6)); node0 = 2^16 + the thread's index with register bits 0.
+// Twiddles in chunks of CH per stage (bounded registers beside the plane).
+// As in pass_ct, outputs the next stage of the pass only multiplies stay
+// in [0, 2q); the last stage leaves everything canonical.  Stages and
+// chunks are template recursions, so every register index is a
+// compile-time constant (a loop the unroller gave up on would put the
+// plane in scratch memory).
+// Butterflies as interleaved groups of four in inline asm (rnt_bfly4.hpp):
+// 1 (default) or 0 (the C++ butterflies of rnt_modarith.hpp, A/B).
+#ifndef RNT_PLANE_ASM
+#define RNT_PLANE_ASM 1
+#endif
+template <class TS>
+constexpr bool tw_uniform() {
+  return std::is_same<TS, TwScalar<uint32_t>>::value;
+}
+
+// The n * 2^SL butterflies of a CT stage chunk in groups of four.  With
+// SPLIT (a stage inside the pass) the butterflies whose upper half of e is
+// set (i & (d >> 1)) are the lazy ones (both outputs only multiplied next);
+// each class is grouped on its own.  Butterfly m of class CLS: twiddle j =
+// m / HALF, e = CLS * HALF + m % HALF.
+template <int LY, int SL, int M0, int HALF, bool LAZY, bool SW, int n>
+__device__ __forceinline__ void plane_ct_groups(uint32_t (&x)[64], const Tw<uint32_t> (&t)[n], const Mod<uint32_t>& mo) {
+  constexpr int d = 1 << SL, per = n * HALF, e0 = LAZY ? HALF : 0;
+  static_assert(per % 4 == 0, "butterfly groups of four");
+#pragma unroll
+  for (int g = 0; g < per / 4; ++g) {
+    int il[4], jj[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int m = 4 * g + k;
+      jj[k] = m / HALF;
+      il[k] = ((M0 + jj[k]) << (SL + 1)) | (e0 + m % HALF);
+    }
+    const uint32_t w[4] = {t[jj[0]].w, t[jj[1]].w, t[jj[2]].w, t[jj[3]].w};
+    const uint32_t wp[4] = {t[jj[0]].p, t[jj[1]].p, t[jj[2]].p, t[jj[3]].p};
+    uint64_t P[4];
+    b4::shoup_prod4<SW>(P, x[plane::slot<LY>(il[0] | d)], x[plane::slot<LY>(il[1] | d)],
+                        x[plane::slot<LY>(il[2] | d)], x[plane::slot<LY>(il[3] | d)], w, wp, mo.nq);
+    uint32_t pl[4] = {(uint32_t)P[0], (uint32_t)P[1], (uint32_t)P[2], (uint32_t)P[3]};
+    if constexpr (LAZY)
+      b4::ct_reduce4_lazy(x[plane::slot<LY>(il[0])], x[plane::slot<LY>(il[1])], x[plane::slot<LY>(il[2])],
+                          x[plane::slot<LY>(il[3])], x[plane::slot<LY>(il[0] | d)], x[plane::slot<LY>(il[1] | d)],
+                          x[plane::slot<LY>(il[2] | d)], x[plane::slot<LY>(il[3] | d)], pl, mo.q);
+    else
+      b4::ct_reduce4(x[plane::slot<LY>(il[0])], x[plane::slot<LY>(il[1])], x[plane::slot<LY>(il[2])],
+                     x[plane::slot<LY>(il[3])], x[plane::slot<LY>(il[0] | d)], x[plane::slot<LY>(il[1] | d)],
+                     x[plane::slot<LY>(il[2] | d)], x[plane::slot<LY>(il[3] | d)], pl, mo.q);
+  }
+}
+
+// GS butterflies of a stage chunk in groups of four: (u, v) <- (u + v,
+// (u - v) w), every output canonical.
+template <int LY, int SL, int M0, bool SW, int n>
+__device__ __forceinline__ void plane_gs_groups(uint32_t (&x)[64], const Tw<uint32_t> (&t)[n], const Mod<uint32_t>& mo) {
+  constexpr int d = 1 << SL, per = n * d;
+  static_assert(per % 4 == 0, "butterfly groups of four");
+#pragma unroll
+  for (int g = 0; g < per / 4; ++g) {
+    int il[4], jj[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int m = 4 * g + k;
+      jj[k] = m / d;
+      il[k] = ((M0 + jj[k]) << (SL + 1)) | (m % d);
+    }
+    const uint32_t w[4] = {t[jj[0]].w, t[jj[1]].w, t[jj[2]].w, t[jj[3]].w};
+    const uint32_t wp[4] = {t[jj[0]].p, t[jj[1]].p, t[jj[2]].p, t[jj[3]].p};
+    uint32_t dd[4];
+    b4::gs_pre4(x[plane::slot<LY>(il[0])], x[plane::slot<LY>(il[1])], x[plane::slot<LY>(il[2])],
+                x[plane::slot<LY>(il[3])], x[plane::slot<LY>(il[0] | d)], x[plane::slot<LY>(il[1] | d)],
+                x[plane::slot<LY>(il[2] | d)], x[plane::slot<LY>(il[3] | d)], dd, mo.q);
+    uint64_t P[4];
+    b4::shoup_prod4<SW>(P, dd[0], dd[1], dd[2], dd[3], w, wp, mo.nq);
+    const uint32_t pl[4] = {(uint32_t)P[0], (uint32_t)P[1], (uint32_t)P[2], (uint32_t)P[3]};
+    b4::csub4(x[plane::slot<LY>(il[0] | d)], x[plane::slot<LY>(il[1] | d)], x[plane::slot<LY>(il[2] | d)],
+              x[plane::slot<LY>(il[3] | d)], pl, mo.q);
+  }
+}
+
+template <int LY, int BB, int SL, int SLLO, int M0, int CH, class TS>
+__device__ __forceinline__ void plane_ct_chunks(uint32_t (&x)[64], uint32_t nb, const TS& tw,
+                                                const Mod<uint32_t>& mo) {
+  constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
+  Tw<uint32_t> t[n];
+#pragma unroll
+  for (int j = 0; j < n; ++j)
+    t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_get<uint32_t>(tw, nb, (uint32_t)(M0 + j));
+  if constexpr (RNT_PLANE_ASM != 0) {
+    constexpr bool SW = tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0;
+    if constexpr (SL > SLLO) {
+      plane_ct_groups<LY, SL, M0, d / 2, false, SW>(x, t, mo);
+      plane_ct_groups<LY, SL, M0, d / 2, true, SW>(x, t, mo);
+    } else {
+      plane_ct_groups<LY, SL, M0, d, false, SW>(x, t, mo);
+    }
+    if constexpr (M0 + CH < cnt) plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH>(x, nb, tw, mo);
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+#pragma unroll
+    for (int e = 0; e < d; ++e) {
+      const int i = ((M0 + j) << (SL + 1)) | e;
+      if (SL > SLLO && (i & (d >> 1)))
+        ct_bfly_lazy(x[plane::slot<LY>(i)], x[plane::slot<LY>(i | d)], t[j].w, t[j].p, mo);
+      else
+        ct_bfly(x[plane::slot<LY>(i)], x[plane::slot<LY>(i | d)], t[j].w, t[j].p, mo);
+    }
+  }
+  if constexpr (M0 + CH < cnt) plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH>(x, nb, tw, mo);
+}
+template <int LY, int BB, int SL, int SLLO, int CH, class TS>
+__device__ __forceinline__ void plane_ct(uint32_t (&x)[64], uint32_t node0, const TS& tw,
+                                         const Mod<uint32_t>& mo) {
+  plane_ct_chunks<LY, BB, SL, SLLO, 0, CH>(x, node0 >> (BB + SL + 1), tw, mo);
+  if constexpr (SL > SLLO) plane_ct<LY, BB, SL - 1, SLLO, CH>(x, node0, tw, mo);
+}
+
+// GS stages on logical register bits SLLO .. SLHI; FOLD: the stage at
+// index bit 15 applies the folded constants (4/N with the Montgomery
+// factor, LimbConst c1t/c2t) instead of its twiddle.
+template <int LY, int BB, int SL, int M0, int CH, class TS>
+__device__ __forceinline__ void plane_gs_chunks(uint32_t (&x)[64], uint32_t nb, const TS& itw,
+                                                const Mod<uint32_t>& mo) {
+  constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
+  Tw<uint32_t> t[n];
+#pragma unroll
+  for (int j = 0; j < n; ++j)
+    t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_get<uint32_t>(itw, nb, (uint32_t)(M0 + j));
+  if constexpr (RNT_PLANE_ASM != 0) {
+    plane_gs_groups<LY, SL, M0, tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0>(x, t, mo);
+    if constexpr (M0 + CH < cnt) plane_gs_chunks<LY, BB, SL, M0 + CH, CH>(x, nb, itw, mo);
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+#pragma unroll
+    for (int e = 0; e < d; ++e) {
+      const int i = ((M0 + j) << (SL + 1)) | e;
+      gs_bfly(x[plane::slot<LY>(i)], x[plane::slot<LY>(i | d)], t[j].w, t[j].p, mo);
+    }
+  }
+  if constexpr (M0 + CH < cnt) plane_gs_chunks<LY, BB, SL, M0 + CH, CH>(x, nb, itw, mo);
+}
+template <int LY, int BB, int SL, int SLHI, int CH, bool FOLD, class TS>
+__device__ __forceinline__ void plane_gs(uint32_t (&x)[64], uint32_t node0, const TS& itw,
+                                         const Mod<uint32_t>& mo, const Fold<uint32_t>& f) {
+  constexpr int d = 1 << SL;
+  if constexpr (FOLD && BB + SL + 1 == 16) {
+#pragma unroll
+    for (int e = 0; e < d; ++e) {  // the top stage: d = 32, one group
+      const uint32_t u = x[plane::slot<LY>(e)], v = x[plane::slot<LY>(e | d)];
+      x[plane::slot<LY>(e)] = shoup_mul(u + v, f.c1, f.c1p, mo);
+      x[plane::slot<LY>(e | d)] = shoup_mul(u - v + mo.q, f.c2, f.c2p, mo);
+    }
+  } else {
+    plane_gs_chunks<LY, BB, SL, 0, CH>(x, node0 >> (BB + SL + 1), itw, mo);
+  }
+  if constexpr (SL < SLHI) plane_gs<LY, BB, SL + 1, SLHI, CH, FOLD>(x, node0, itw, mo, f);
+}
+
+// X1, L0 <-> L1 through LDS.  Round h carries the words with index bit
+// 10 == h: L0 registers 2k + h, L1 logical registers r1 = ((k >> 4) << 5) |
+// (h << 4) | (k & 15), both in physical register 2k + h.  LDS word = the 15
+// other index bits; every access is 64 consecutive words per wave.
+// SYNC_FIRST: other waves may still be reading their X2 buffers.
+template <bool TO_L1, bool SYNC_FIRST>
+__device__ __forceinline__ void plane_x1(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
+  const uint32_t w = t >> 6, lam = t & 63u;
+  if constexpr ((RNT_PLANE_EXP & 16) != 0) return;
+  if constexpr (SYNC_FIRST) __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const uint32_t j0 = ((uint32_t)k << 10) | t;
+      const uint32_t j1 = ((((w << 1) | ((uint32_t)k >> 4))) << 10) | (((uint32_t)k & 15u) << 6) | lam;
+      lds[TO_L1 ? j0 : j1] = x[2 * k + h];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const uint32_t j0 = ((uint32_t)k << 10) | t;
+      const uint32_t j1 = ((((w << 1) | ((uint32_t)k >> 4))) << 10) | (((uint32_t)k & 15u) << 6) | lam;
+      x[2 * k + h] = lds[TO_L1 ? j1 : j0];
+    }
+    __syncthreads();
+  }
+}
+
+// Lane bit 5 <-> L1 register bit 5 and lane bit 4 <-> register bit 4
+// (self-inverse; the two commute).
+__device__ __forceinline__ void plane_swap54(uint32_t (&x)[64]) {
+#pragma unroll
+  for (int m = 0; m < 64; ++m) {
+    if (m & 32) continue;
+    const auto r = __builtin_amdgcn_permlane32_swap(x[plane::slot1(m)], x[plane::slot1(m | 32)], false, false);
+    x[plane::slot1(m)] = r[0];
+    x[plane::slot1(m | 32)] = r[1];
+  }
+#pragma unroll
+  for (int m = 0; m < 64; ++m) {
+    if (m & 16) continue;
+    const auto r = __builtin_amdgcn_permlane16_swap(x[plane::slot1(m)], x[plane::slot1(m | 16)], false, false);
+    x[plane::slot1(m)] = r[0];
+    x[plane::slot1(m | 16)] = r[1];
+  }
+}
+
+// X2, L1 <-> L2 inside each wave.  After plane_swap54 a lane holds index
+// bits 11, 10 (lane bits 5, 4) and 3..0, a register m holds bits 5, 4
+// (m >> 4) and 9..6 (m & 15); per group g = m >> 4 the 16 x 16 blocks of
+// (m & 15) x (lane & 15) transpose through the wave's LDS buffer: word
+// (lane, m & 15) at lane * 17 + (m & 15), read back by lane' as register
+// (g << 4) | c from lane (lane' & 48) | c, column lane' & 15 (both
+// directions 64 distinct banks).  LDS instructions of one wave execute in
+// order, so the reads see the same wave's writes; two buffers alternate.
+template <bool TO_L2>
+__device__ __forceinline__ void plane_x2(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
+  const uint32_t w = t >> 6, lam = t & 63u;
+  if constexpr ((RNT_PLANE_EXP & 16) != 0) return;
+  if constexpr (TO_L2) plane_swap54(x);
+  const uint32_t a15 = lam * plane::XS;                          // + (m & 15)
+  const uint32_t a2 = (lam & 48u) * plane::XS + (lam & 15u);     // + c * XS
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    uint32_t* buf = lds + (w * 2u + (uint32_t)(g & 1)) * plane::XW;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) buf[TO_L2 ? a15 + j : a2 + j * plane::XS] = x[plane::slot1((g << 4) | j)];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < 16; ++c) x[plane::slot1((g << 4) | c)] = buf[TO_L2 ? a2 + c * plane::XS : a15 + c];
+    __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (!TO_L2) plane_swap54(x);
+}
+
+// One workgroup per CU and equal work per workgroup keep every CU's load,
+// compute and store phases in step across the chip, so the loads of all
+// CUs meet at the HBM together while the VALUs idle, and then the other
+// way round.  Delaying the first workgroup of every other CU by `ticks`
+// of the 100 MHz real-time counter once shifts that CU's phase for the
+// rest of the launch (its next workgroups start when the previous one
+// ends), so half the CUs load while the other half compute.
+__device__ __forceinline__ void plane_stagger(uint32_t ticks) {
+  if (ticks == 0) return;
+  const uint32_t id = blockIdx.x + blockIdx.y * gridDim.x;
+  if (id >= 256u || !((id >> 3) & 1u)) return;  // first wave, every other CU of each XCD
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+// Phase timeline of the plane kernels (measurement build only:
+// tools/build_variant.sh trace -DRNT_PLANE_TRACE; tools/plane_trace.py).
+// Lane 0 of every wave of the first 4096 workgroups waits for the wave's
+// own memory operations and stamps the 100 MHz real-time counter at each
+// phase boundary.
+#ifdef RNT_PLANE_TRACE
+constexpr int kTraceWg = 4096, kTraceStamps = 16;
+__device__ uint64_t g_plane_trace[2 * kTraceWg * 16 * kTraceStamps];
+#define PLANE_STAMP(K, S)                                                                       \
+  do {                                                                                          \
+    const uint32_t wg_ = trace_id;                                                              \
+    if ((threadIdx.x & 63u) == 0 && wg_ < (uint32_t)kTraceWg) {                                 \
+      __builtin_amdgcn_s_waitcnt(0);                                                            \
+      g_plane_trace[(((K) * kTraceWg + wg_) * 16 + (threadIdx.x >> 6)) * kTraceStamps + (S)] =  \
+          __builtin_amdgcn_s_memrealtime();                                                     \
+    }                                                                                           \
+  } while (0)
+#else
+#define PLANE_STAMP(K, S) \
+  do {                    \
+  } while (0)
+#endif
+
+// Measurement builds (tools/build_variant.sh, wrong results by design):
+// RNT_PLANE_EXP bit 0: pass C / inverse pass C twiddles wave-uniform;
+// bit 1: no plane loads (synthetic words); bit 2: no plane stores;
+// bit 3: no twiddle loads in the passes (one constant); bit 4: no X1 / X2.
+
+// Cache policy (buffer aux bits) of the streamed operand loads and the
+// product store: 0 default, 2 non-temporal (A/B knob, -DRNT_PLANE_AUX=2).
+#ifndef RNT_PLANE_AUX
+#define RNT_PLANE_AUX 0
+#endif
+constexpr int kPlaneAux = RNT_PLANE_AUX;
+// Register prefetch depths of the fused kernel (k_plane_fused): b's words
+// during a's transform, a^ blocks during b's (A/B knobs).
+#ifndef RNT_PLANE_PFB
+#define RNT_PLANE_PFB 0
+#endif
+#ifndef RNT_PLANE_PFA
+#define RNT_PLANE_PFA 0
+#endif
+constexpr int kPlanePfB = RNT_PLANE_PFB, kPlanePfA = RNT_PLANE_PFA;
+// Twiddles per scalar-load chunk in pass A (64 SGPRs at 32)
+#ifndef RNT_PLANE_CHA
+#define RNT_PLANE_CHA 32
+#endif
+constexpr int kPlaneChA = RNT_PLANE_CHA;
+
+// Load the L0 plane at src (64 coalesced dword loads a thread).
+__device__ __forceinline__ void plane_load(uint32_t (&x)[64], const uint32_t* src, uint32_t t) {
+  if constexpr ((RNT_PLANE_EXP & 2) != 0) {
+#pragma unroll
+    for (int r = 0; r < 64; ++r) x[r] = (t * 2654435761u + (uint32_t)r * 40503u) >> 2;
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t g = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)(4u << 16), 0x00020000);
+#pragma unroll
+  for (int r = 0; r < 64; ++r) x[r] = __builtin_amdgcn_raw_buffer_load_b32(g, t * 4u, (uint32_t)r << 12, kPlaneAux);
+}
+
+// The CU this workgroup runs on, as a dense id below kPlaneSlots: XCC_ID
+// (hwreg 20, bits 3:0) and HW_ID's SE_ID (15:13), SH_ID (12), CU_ID (11:8).
+// The plane kernels use 139 KiB of LDS and the whole register file, so a CU
+// runs one of their workgroups at a time: while it runs, the id names a
+// scratch slot no other workgroup of the launch uses.
+constexpr uint32_t kPlaneSlots = 1u << 12;
+__device__ __forceinline__ uint32_t plane_cu_slot() {
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+  return ((xcc & 15u) << 8) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 15u);
+}
+
+// The truncated forward transform of the plane in x (L0 in, L2 out).
+// SYNC1: other waves may still be using the LDS (their X2 buffers of an
+// earlier transform) when X1 starts.
+struct NoHook {
+  __device__ void operator()() const {}
+};
+// AFTER_X1 / AFTER_X2 run right after the exchanges (prefetches of the next
+// operand: issued there, they are in flight during the passes that follow).
+template <int K, bool SYNC1, class H1 = NoHook, class H2 = NoHook>
+__device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint32_t t,
+                                          const Tw<uint32_t>* tw, const Mod<uint32_t>& mo, uint32_t trace_id,
+                                          const H1& after_x1 = H1{}, const H2& after_x2 = H2{}) {
+  (void)trace_id;
+  const uint32_t N = 1u << 16;
+  const TwScalar<uint32_t> tws{(const RNT_CONST_AS Tw<uint32_t>*)tw};
+  // pass A's twiddle nodes ((2^16 + i) >> (b + 1), b >= 10) depend on
+  // register bits only, pass B's (b >= 6) on register and wave bits: both
+  // wave-uniform (scalar loads)
+  plane_ct<0, 10, 5, 0, kPlaneChA>(x, N, tws, mo);
+  PLANE_STAMP(K, 2);
+  plane_x1<true, SYNC1>(x, lds, t);
+  PLANE_STAMP(K, 3);
+  after_x1();
+  const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
+  plane_ct<1, 6, 3, 0, 16>(x, N + (wu << 12), tws, mo);
+  PLANE_STAMP(K, 4);
+  plane_x2<true>(x, lds, t);
+  PLANE_STAMP(K, 5);
+  after_x2();
+  if constexpr ((RNT_PLANE_EXP & 1) != 0)
+    plane_ct<2, 0, 5, 2, 8>(x, N, tws, mo);
+  else
+    plane_ct<2, 0, 5, 2, 8>(x, N + (t << 6), tw, mo);
+  PLANE_STAMP(K, 6);
+}
+
+// The rest of the product once b^ is in x (L2): the degree-3 block
+// products with a^ (ah: the private layout, block kk of thread t at
+// ah[kk * 1024 + t]), the whole truncated inverse, c stored in L0.
+// AH(kk) gives block kk of a^ (from memory, or a register prefetch).
+template <int K, class AH>
+__device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds, uint32_t t, const AH& ah,
+                                               uint32_t* c, const Tw<uint32_t>* tw, const Tw<uint32_t>* itw,
+                                               const LimbConst<uint32_t>& lc, const Mod<uint32_t>& mo,
+                                               uint32_t trace_id) {
+  (void)trace_id;
+  const uint32_t n0 = 1u << 16;
+  // degree-3 block products: block (t << 4) | kk, zeta = (-1)^kk psi_rev[N/8 + (t << 3) + kk/2]
+  const uint32_t zb = (n0 >> 3) + (t << 3);
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const uint4 av = (RNT_PLANE_EXP & 2) != 0 ? make_uint4(t * 7u + kk, t * 11u, t + 3u * kk, t ^ 0x55u)
+                                              : ah(kk);
+    const uint32_t aa[4] = {av.x, av.y, av.z, av.w};
+    const uint32_t bb[4] = {x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
+                            x[plane::slot2(4 * kk + 3)]};
+    const Tw<uint32_t> w = tw[zb + (kk >> 1)];
+    const uint32_t zeta = (kk & 1) ? lc.q - w.w : w.w;
+    const uint32_t zeta_p = (kk & 1) ? ~w.p : w.p;
+    uint32_t cc[4];
+    mul_mod_x4(cc, aa, bb, zeta, zeta_p, lc.q, lc.qinv);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = cc[e];
+  }
+  PLANE_STAMP(K, 7);
+  const TwScalar<uint32_t> itws{(const RNT_CONST_AS Tw<uint32_t>*)itw};
+  if constexpr ((RNT_PLANE_EXP & 1) != 0)
+    plane_gs<2, 0, 2, 5, 8, false>(x, n0, itws, mo, Fold<uint32_t>{});
+  else
+    plane_gs<2, 0, 2, 5, 8, false>(x, n0 + (t << 6), itw, mo, Fold<uint32_t>{});
+  PLANE_STAMP(K, 8);
+  plane_x2<false>(x, lds, t);
+  PLANE_STAMP(K, 9);
+  const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
+  plane_gs<1, 6, 0, 3, 16, false>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+  PLANE_STAMP(K, 10);
+  plane_x1<false, true>(x, lds, t);  // other waves may still be in their X2
+  PLANE_STAMP(K, 11);
+  plane_gs<0, 10, 0, 5, kPlaneChA, true>(x, n0, itws, mo, Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p});
+  PLANE_STAMP(K, 12);
+  if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) return;
+  const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc((void*)c, 0, (int)(4u << 16), 0x00020000);
+#pragma unroll
+  for (int r = 0; r < 64; ++r) __builtin_amdgcn_raw_buffer_store_b32(x[r], dst, t * 4u, (uint32_t)r << 12, kPlaneAux);
+  PLANE_STAMP(K, 13);
+}
+
+// a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
+__device__ __forceinline__ void plane_store_hat(uint4* dst, const uint32_t (&x)[64], uint32_t t) {
+  if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) return;
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk)
+    dst[kk * 1024 + t] = make_uint4(x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)],
+                                    x[plane::slot2(4 * kk + 2)], x[plane::slot2(4 * kk + 3)]);
+}
+
+// One workgroup per plane, grid (B, L).
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_fwd(uint32_t* __restrict__ ahat, const uint32_t* __restrict__ a, TabPtrs<uint32_t> tp, uint64_t ls,
+            uint32_t stagger) {
+  plane_stagger(stagger);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
+  const uint32_t trace_id = poly + l * gridDim.x;
+  PLANE_STAMP(0, 0);
+  const uint64_t N = 1ull << 16;
+  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
+  uint32_t x[64];
+  plane_load(x, a + off, t);
+  PLANE_STAMP(0, 1);
+  plane_fwd<0, false>(x, lds, t, tp.tw + (uint64_t)l * N, mod_of(tp.lc[l]), trace_id);
+  plane_store_hat((uint4*)(ahat + off), x, t);
+  PLANE_STAMP(0, 7);
+}
+
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_mul(uint32_t* __restrict__ c, const uint32_t* __restrict__ b, const uint32_t* __restrict__ ahat,
+            TabPtrs<uint32_t> tp, uint64_t ls, uint32_t stagger) {
+  plane_stagger(stagger);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
+  const uint32_t trace_id = poly + l * gridDim.x;
+  PLANE_STAMP(1, 0);
+  const uint64_t N = 1ull << 16;
+  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
+  const LimbConst<uint32_t> lc = tp.lc[l];
+  const Mod<uint32_t> mo = mod_of(lc);
+  const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
+  uint32_t x[64];
+  plane_load(x, b + off, t);
+  PLANE_STAMP(1, 1);
+  plane_fwd<1, false>(x, lds, t, tw, mo, trace_id);
+  const uint4* ah = (const uint4*)(ahat + off);
+  plane_mul_tail<1>(x, lds, t, [ah, t](int kk) { return ah[kk * 1024 + t]; }, c + off, tw, tp.itw + (uint64_t)l * N,
+                    lc, mo, trace_id);
+}
+
+// Both halves in one workgroup (RNT_PLANE=3): a -> a^ through the scratch
+// plane, which the same threads read back ~40 us later (so the read is
+// served by the Infinity Cache or L2 rather than HBM), then b -> c as
+// k_plane_mul.  One launch per batch; the store of a^ and the load of b
+// are back to back and overlap.
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_fused(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
+              TabPtrs<uint32_t> tp, uint64_t ls, uint32_t cu_slots) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
+  const uint32_t trace_id = poly + l * gridDim.x;
+  const uint64_t N = 1ull << 16;
+  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
+  const LimbConst<uint32_t> lc = tp.lc[l];
+  const Mod<uint32_t> mo = mod_of(lc);
+  const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
+  // a^ goes to a scratch plane: per (poly, limb), or (cu_slots) per CU, so
+  // the launch's scratch footprint is 256 KiB per CU (64 MiB on 256 CUs),
+  // rewritten by the CU's next workgroup while it may still sit in the
+  // Infinity Cache
+  uint4* ah = (uint4*)(scratch + (cu_slots ? (uint64_t)plane_cu_slot() * N : off));
+  uint32_t x[64];
+  PLANE_STAMP(0, 0);
+  plane_load(x, a + off, t);
+  PLANE_STAMP(0, 1);
+#if RNT_PLANE_PFB > 0 || RNT_PLANE_PFA > 0
+  // b's first PFB registers are loaded during a's passes B and C, the first
+  // PFA blocks of a^ during b's pass C: in flight while the VALU works
+  // (a CU runs one of these workgroups, so nothing else hides a load)
+  constexpr int PFB = kPlanePfB, PFA = kPlanePfA;
+  uint32_t y[PFB > 0 ? PFB : 1];
+  plane_fwd<0, false>(x, lds, t, tw, mo, trace_id, [&]() {
+    if constexpr (PFB > 0) {
+      const uint32_t* bp = b + off;
+      asm volatile("" : "+s"(bp));
+      const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc((void*)bp, 0, (int)(4u << 16), 0x00020000);
+#pragma unroll
+      for (int r = 0; r < PFB; ++r) y[r] = __builtin_amdgcn_raw_buffer_load_b32(gb, t * 4u, (uint32_t)r << 12, kPlaneAux);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+  plane_store_hat(ah, x, t);
+  PLANE_STAMP(0, 7);
+  PLANE_STAMP(1, 0);
+  {
+    const uint32_t* bp = b + off;
+    asm volatile("" : "+s"(bp));
+    const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc((void*)bp, 0, (int)(4u << 16), 0x00020000);
+#pragma unroll
+    for (int r = 0; r < 64; ++r)
+      x[r] = r < PFB ? y[r < PFB ? r : 0] : __builtin_amdgcn_raw_buffer_load_b32(gb, t * 4u, (uint32_t)r << 12, kPlaneAux);
+  }
+  PLANE_STAMP(1, 1);
+  // a^ comes back from this thread's own stores above; an opaque copy of
+  // the base keeps the compiler from holding the 16 store addresses live
+  // (in scratch) across b's transform
+  const uint4* ah2 = ah;
+  asm volatile("" : "+s"(ah2));
+  uint4 ap[PFA > 0 ? PFA : 1];
+  plane_fwd<1, true>(x, lds, t, tw, mo, trace_id, NoHook{}, [&ap, ah2, t]() {
+#pragma unroll
+    for (int kk = 0; kk < PFA; ++kk) ap[kk] = ah2[kk * 1024 + t];
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  // (the block source captures the base by value: a by-reference capture
+  // undoes the opaque copy, and the store addresses go to scratch again)
+  plane_mul_tail<1>(x, lds, t, [&ap, ah2, t](int kk) { return kk < PFA ? ap[kk < PFA ? kk : 0] : ah2[kk * 1024 + t]; }, c + off,
+                    tw, tp.itw + (uint64_t)l * N, lc, mo, trace_id);
+#else
+  plane_fwd<0, false>(x, lds, t, tw, mo, trace_id);
+  plane_store_hat(ah, x, t);
+  PLANE_STAMP(0, 7);
+  PLANE_STAMP(1, 0);
+  plane_load(x, b + off, t);
+  PLANE_STAMP(1, 1);
+  plane_fwd<1, true>(x, lds, t, tw, mo, trace_id);
+  // a^ comes back from this thread's own stores above; an opaque copy of
+  // the base keeps the compiler from holding the 16 store addresses live
+  // (in scratch) across b's transform (the block source captures it by
+  // value: a by-reference capture undoes the copy)
+  const uint4* ah2 = ah;
+  asm volatile("" : "+s"(ah2));
+  plane_mul_tail<1>(x, lds, t, [ah2, t](int kk) { return ah2[kk * 1024 + t]; }, c + off, tw,
+                    tp.itw + (uint64_t)l * N, lc, mo, trace_id);
+#endif
+}
+
+#ifdef RNT_PLANE_TRACE
+extern "C" __attribute__((visibility("default"))) int rnt_debug_plane_trace(uint64_t* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_plane_trace), sizeof(g_plane_trace));
+}
+#endif
+
+// The whole-plane product (k_plane_fwd + k_plane_mul) serves rnt_mul for
+// u32 canonical bases at N = 2^16 when Tables::plane is set (RNT_PLANE).
+// The whole-plane kernels take every u32 basis at N = 2^16 (their
+// canonical arithmetic holds for any q < 2^31, so 30-bit bases too: 131k
+// against the lazy four-step kernels' 114k products/s).
+bool plane_ok(const Tables* t) {
+  return t->plane != 0 && !t->wide && t->log_n == 16;
+}
+
+hipError_t launch_plane(const Launch& k, int which, void* out, const void* in, const void* ahat,
+                        uint64_t ls) {
+  if (k.B == 0 || k.L == 0) return hipSuccess;
+  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  const size_t lds = (size_t)plane::LDS_WORDS * 4;
+  const dim3 grid((unsigned)k.B, (unsigned)k.L);
+  const uint32_t st = k.t->plane_stagger;
+  if (which == 0) {
+    hipError_t e = allow_lds(k_plane_fwd, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_plane_fwd, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)in,
+                       tab_ptrs<uint32_t>(k.t), ls, st);
+  } else {
+    hipError_t e = allow_lds(k_plane_mul, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_plane_mul, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)in,
+                       (const uint32_t*)ahat, tab_ptrs<uint32_t>(k.t), ls, st);
+  }
+  return hipGetLastError();
+}
+
+#ifndef RNT_PLANE_SLOTS
+#define RNT_PLANE_SLOTS 0
+#endif
+// Per-CU scratch slots once the batch has at least as many planes as slots
+// (the workspace, one plane per (poly, limb), then holds every slot).
+bool plane_fused_slots(const Launch& k) {
+  return RNT_PLANE_SLOTS && (uint64_t)k.B * k.L >= kPlaneSlots;
+}
+
+hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls) {
+  if (k.B == 0 || k.L == 0) return hipSuccess;
+  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  const size_t lds = (size_t)plane::LDS_WORDS * 4;
+  hipError_t e = allow_lds(k_plane_fused, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_plane_fused, dim3((unsigned)k.B, (unsigned)k.L), dim3(plane::T), lds, k.s, (uint32_t*)out,
+                     (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)scratch, tab_ptrs<uint32_t>(k.t), ls,
+                     plane_fused_slots(k) ? 1u : 0u);
+  return hipGetLastError();
+}
+
+}  // namespace rnt
