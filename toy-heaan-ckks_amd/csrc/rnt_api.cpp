@@ -633,7 +633,8 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     t->lazy30 = !wide && lazy30 && env_long("RNT_LAZY30", 1) != 0;
     // RNT_PLANE=1: rnt_mul through the whole-plane kernels (N = 2^16, u32)
     // the whole-plane product is the default where it applies (plane_ok);
-    // RNT_PLANE=0 keeps the four-step kernels, 1 the two-launch plane path
+    // RNT_PLANE=0 keeps the four-step kernels, 1 the two-launch plane path,
+    // 3 the fused kernel (one workgroup per plane), 4 its persistent form
     t->plane = (int)env_long("RNT_PLANE", 3);
     t->plane_stagger = (uint32_t)env_long("RNT_PLANE_STAGGER", 0);
     {
@@ -1106,7 +1107,7 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   // pointwise product, inverse rows), the inverse column pass.
   const uint64_t ls = limb_stride(out);
   if (int rc = ensure_ws(out, poly_words(out) * word_bytes(k.t))) return rc;
-  if (rnt::plane_ok(k.t) && k.t->plane == 3) {
+  if (rnt::plane_ok(k.t) && k.t->plane >= 3) {
     LAUNCH(k.t, rnt::K_PLANE_FUSED, rnt::launch_plane_fused(k, out->data, a->data, b->data, out->ws, ls),
            "plane fused product");
     out->in_ntt = 0;

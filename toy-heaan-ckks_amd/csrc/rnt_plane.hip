@@ -8,6 +8,7 @@
 // same (and the reference's).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "rnt_internal.hpp"
@@ -72,6 +73,52 @@ __host__ __device__ constexpr int slot(int r) {
 // chunks are template recursions, so every register index is a
 // compile-time constant (a loop the unroller gave up on would put the
 // plane in scratch memory).
+// Pass C's per-thread twiddles (stages at index bits 5..2: 1, 2, 4 and 8
+// of them), loaded ahead of the X2 exchange so the loads are in flight
+// during it instead of stalling each stage of the pass.
+#ifndef RNT_PLANE_PREC
+#define RNT_PLANE_PREC 3  // pass C stages whose twiddles are preloaded (0..4)
+#endif
+struct TwPreC {
+  const Tw<uint32_t>* b;
+  uint32_t node0;
+  Tw<uint32_t> s5[1], s4[2], s3[4], s2[8];
+};
+__device__ __forceinline__ TwPreC plane_prec(const Tw<uint32_t>* b, uint32_t node0) {
+  TwPreC p;
+  p.b = b;
+  p.node0 = node0;
+  if constexpr (RNT_PLANE_PREC >= 1) p.s5[0] = tw_get<uint32_t>(b, node0 >> 6, 0u);
+  if constexpr (RNT_PLANE_PREC >= 2) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) p.s4[m] = tw_get<uint32_t>(b, node0 >> 5, (uint32_t)m);
+  }
+  if constexpr (RNT_PLANE_PREC >= 3) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) p.s3[m] = tw_get<uint32_t>(b, node0 >> 4, (uint32_t)m);
+  }
+  if constexpr (RNT_PLANE_PREC >= 4) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) p.s2[m] = tw_get<uint32_t>(b, node0 >> 3, (uint32_t)m);
+  }
+  return p;
+}
+// Twiddle m of a stage chunk at index bit SL (+ BB): from the source, or
+// from the preloaded set.
+template <int SL, class TS>
+__device__ __forceinline__ Tw<uint32_t> tw_fetch(const TS& ts, uint32_t nb, uint32_t m) {
+  return tw_get<uint32_t>(ts, nb, m);
+}
+template <int SL>
+__device__ __forceinline__ Tw<uint32_t> tw_fetch(const TwPreC& p, uint32_t nb, uint32_t m) {
+  static_assert(SL >= 2 && SL <= 5, "pass C stages");
+  if constexpr (5 - SL >= RNT_PLANE_PREC) return tw_get<uint32_t>(p.b, nb, m);
+  else if constexpr (SL == 5) return p.s5[0];
+  else if constexpr (SL == 4) return p.s4[m];
+  else if constexpr (SL == 3) return p.s3[m];
+  else return p.s2[m];
+}
+
 // Butterflies as interleaved groups of four in inline asm (rnt_bfly4.hpp):
 // 1 (default) or 0 (the C++ butterflies of rnt_modarith.hpp, A/B).
 #ifndef RNT_PLANE_ASM
@@ -153,7 +200,7 @@ __device__ __forceinline__ void plane_ct_chunks(uint32_t (&x)[64], uint32_t nb, 
   Tw<uint32_t> t[n];
 #pragma unroll
   for (int j = 0; j < n; ++j)
-    t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_get<uint32_t>(tw, nb, (uint32_t)(M0 + j));
+    t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<BB + SL>(tw, nb, (uint32_t)(M0 + j));
   if constexpr (RNT_PLANE_ASM != 0) {
     constexpr bool SW = tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0;
     if constexpr (SL > SLLO) {
@@ -353,20 +400,21 @@ __device__ uint64_t g_plane_trace[2 * kTraceWg * 16 * kTraceStamps];
 #define RNT_PLANE_AUX 0
 #endif
 constexpr int kPlaneAux = RNT_PLANE_AUX;
-// Register prefetch depths of the fused kernel (k_plane_fused): b's words
-// during a's transform, a^ blocks during b's (A/B knobs).
-#ifndef RNT_PLANE_PFB
-#define RNT_PLANE_PFB 0
-#endif
-#ifndef RNT_PLANE_PFA
-#define RNT_PLANE_PFA 0
-#endif
-constexpr int kPlanePfB = RNT_PLANE_PFB, kPlanePfA = RNT_PLANE_PFA;
 // Twiddles per scalar-load chunk in pass A (64 SGPRs at 32)
 #ifndef RNT_PLANE_CHA
 #define RNT_PLANE_CHA 32
 #endif
 constexpr int kPlaneChA = RNT_PLANE_CHA;
+// a^ blocks in flight ahead of the degree-3 block products (0: loaded at use)
+#ifndef RNT_PLANE_AHD
+#define RNT_PLANE_AHD 4
+#endif
+constexpr int kPlaneAhd = RNT_PLANE_AHD;
+// ... and in pass B (wave-uniform too)
+#ifndef RNT_PLANE_CHB
+#define RNT_PLANE_CHB 16
+#endif
+constexpr int kPlaneChB = RNT_PLANE_CHB;
 
 // Load the L0 plane at src (64 coalesced dword loads a thread).
 __device__ __forceinline__ void plane_load(uint32_t (&x)[64], const uint32_t* src, uint32_t t) {
@@ -395,6 +443,28 @@ __device__ __forceinline__ uint32_t plane_cu_slot() {
 // The truncated forward transform of the plane in x (L0 in, L2 out).
 // SYNC1: other waves may still be using the LDS (their X2 buffers of an
 // earlier transform) when X1 starts.
+// a^ in the private layout through a buffer descriptor: block kk (4 words)
+// of thread t at byte (kk * 1024 + t) * 16 -- a per-lane offset and a
+// uniform one in the instruction, so no 64-bit addresses live in VGPRs.
+struct HatBuf {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ explicit HatBuf(const void* base)
+      : r(__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 1 << 18, 0x00020000)) {}
+  __device__ __forceinline__ void st(uint32_t t, int kk, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) const {
+    using V4 = decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0));
+    V4 v;
+    v[0] = a0;
+    v[1] = a1;
+    v[2] = a2;
+    v[3] = a3;
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, t * 16u, (uint32_t)kk << 14, 0);
+  }
+  __device__ __forceinline__ uint4 ld(uint32_t t, int kk) const {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, t * 16u, (uint32_t)kk << 14, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  }
+};
+
 struct NoHook {
   __device__ void operator()() const {}
 };
@@ -416,15 +486,16 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   PLANE_STAMP(K, 3);
   after_x1();
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
-  plane_ct<1, 6, 3, 0, 16>(x, N + (wu << 12), tws, mo);
+  plane_ct<1, 6, 3, 0, kPlaneChB>(x, N + (wu << 12), tws, mo);
   PLANE_STAMP(K, 4);
+  const TwPreC pc = plane_prec(tw, N + (t << 6));
   plane_x2<true>(x, lds, t);
   PLANE_STAMP(K, 5);
   after_x2();
   if constexpr ((RNT_PLANE_EXP & 1) != 0)
     plane_ct<2, 0, 5, 2, 8>(x, N, tws, mo);
   else
-    plane_ct<2, 0, 5, 2, 8>(x, N + (t << 6), tw, mo);
+    plane_ct<2, 0, 5, 2, 8>(x, N + (t << 6), pc, mo);
   PLANE_STAMP(K, 6);
 }
 
@@ -441,14 +512,39 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
   const uint32_t n0 = 1u << 16;
   // degree-3 block products: block (t << 4) | kk, zeta = (-1)^kk psi_rev[N/8 + (t << 3) + kk/2]
   const uint32_t zb = (n0 >> 3) + (t << 3);
+  // a^ blocks and zeta twiddles are loaded AHD blocks ahead of their use
+  // (pinned by scheduling barriers: left to itself hipcc issues each load
+  // just before its product, so every block waits out a memory latency)
+  constexpr int D = kPlaneAhd, Z = D > 0 ? (D + 1) / 2 + 1 : 1;  // zeta j serves blocks 2j, 2j + 1
+  uint4 abuf[D > 0 ? D : 1];
+  Tw<uint32_t> zbuf[Z];
+  if constexpr (D > 0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) abuf[d] = ah(d);
+#pragma unroll
+    for (int j = 0; j < Z; ++j) zbuf[j] = tw[zb + j];
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) {
-    const uint4 av = (RNT_PLANE_EXP & 2) != 0 ? make_uint4(t * 7u + kk, t * 11u, t + 3u * kk, t ^ 0x55u)
-                                              : ah(kk);
+    uint4 av;
+    Tw<uint32_t> w;
+    if constexpr ((RNT_PLANE_EXP & 2) != 0) {
+      av = make_uint4(t * 7u + kk, t * 11u, t + 3u * kk, t ^ 0x55u);
+      w = tw[zb + (kk >> 1)];
+    } else if constexpr (D > 0) {
+      av = abuf[kk % D];
+      w = zbuf[(kk >> 1) % Z];
+      if (kk + D < 16) abuf[kk % D] = ah(kk + D);
+      if ((kk & 1) && (kk >> 1) + Z < 8) zbuf[(kk >> 1) % Z] = tw[zb + (kk >> 1) + Z];
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      av = ah(kk);
+      w = tw[zb + (kk >> 1)];
+    }
     const uint32_t aa[4] = {av.x, av.y, av.z, av.w};
     const uint32_t bb[4] = {x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
                             x[plane::slot2(4 * kk + 3)]};
-    const Tw<uint32_t> w = tw[zb + (kk >> 1)];
     const uint32_t zeta = (kk & 1) ? lc.q - w.w : w.w;
     const uint32_t zeta_p = (kk & 1) ? ~w.p : w.p;
     uint32_t cc[4];
@@ -466,7 +562,7 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
   plane_x2<false>(x, lds, t);
   PLANE_STAMP(K, 9);
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
-  plane_gs<1, 6, 0, 3, 16, false>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+  plane_gs<1, 6, 0, 3, kPlaneChB, false>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
   PLANE_STAMP(K, 10);
   plane_x1<false, true>(x, lds, t);  // other waves may still be in their X2
   PLANE_STAMP(K, 11);
@@ -480,12 +576,12 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
 }
 
 // a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
-__device__ __forceinline__ void plane_store_hat(uint4* dst, const uint32_t (&x)[64], uint32_t t) {
+__device__ __forceinline__ void plane_store_hat(const HatBuf& dst, const uint32_t (&x)[64], uint32_t t) {
   if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) return;
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk)
-    dst[kk * 1024 + t] = make_uint4(x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)],
-                                    x[plane::slot2(4 * kk + 2)], x[plane::slot2(4 * kk + 3)]);
+    dst.st(t, kk, x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
+           x[plane::slot2(4 * kk + 3)]);
 }
 
 // One workgroup per plane, grid (B, L).
@@ -504,7 +600,7 @@ k_plane_fwd(uint32_t* __restrict__ ahat, const uint32_t* __restrict__ a, TabPtrs
   plane_load(x, a + off, t);
   PLANE_STAMP(0, 1);
   plane_fwd<0, false>(x, lds, t, tp.tw + (uint64_t)l * N, mod_of(tp.lc[l]), trace_id);
-  plane_store_hat((uint4*)(ahat + off), x, t);
+  plane_store_hat(HatBuf(ahat + off), x, t);
   PLANE_STAMP(0, 7);
 }
 
@@ -527,7 +623,8 @@ k_plane_mul(uint32_t* __restrict__ c, const uint32_t* __restrict__ b, const uint
   PLANE_STAMP(1, 1);
   plane_fwd<1, false>(x, lds, t, tw, mo, trace_id);
   const uint4* ah = (const uint4*)(ahat + off);
-  plane_mul_tail<1>(x, lds, t, [ah, t](int kk) { return ah[kk * 1024 + t]; }, c + off, tw, tp.itw + (uint64_t)l * N,
+  const HatBuf hb(ah);
+  plane_mul_tail<1>(x, lds, t, [hb, t](int kk) { return hb.ld(t, kk); }, c + off, tw, tp.itw + (uint64_t)l * N,
                     lc, mo, trace_id);
 }
 
@@ -536,87 +633,65 @@ k_plane_mul(uint32_t* __restrict__ c, const uint32_t* __restrict__ b, const uint
 // served by the Infinity Cache or L2 rather than HBM), then b -> c as
 // k_plane_mul.  One launch per batch; the store of a^ and the load of b
 // are back to back and overlap.
-__global__ void __launch_bounds__(plane::T, 1)
-k_plane_fused(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
-              TabPtrs<uint32_t> tp, uint64_t ls, uint32_t cu_slots) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  uint32_t* lds = (uint32_t*)smem_raw;
-  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
-  const uint32_t trace_id = poly + l * gridDim.x;
+// The product of one (poly, limb) plane pair; the body of both fused kernels.
+__device__ __forceinline__ void plane_fused_one(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b,
+                                                uint32_t* ah, const TabPtrs<uint32_t>& tp, uint64_t ls, uint32_t poly,
+                                                uint32_t l, uint32_t* lds, uint32_t t, uint32_t trace_id) {
   const uint64_t N = 1ull << 16;
   const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
   const LimbConst<uint32_t> lc = tp.lc[l];
   const Mod<uint32_t> mo = mod_of(lc);
   const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
-  // a^ goes to a scratch plane: per (poly, limb), or (cu_slots) per CU, so
-  // the launch's scratch footprint is 256 KiB per CU (64 MiB on 256 CUs),
-  // rewritten by the CU's next workgroup while it may still sit in the
-  // Infinity Cache
-  uint4* ah = (uint4*)(scratch + (cu_slots ? (uint64_t)plane_cu_slot() * N : off));
   uint32_t x[64];
   PLANE_STAMP(0, 0);
   plane_load(x, a + off, t);
   PLANE_STAMP(0, 1);
-#if RNT_PLANE_PFB > 0 || RNT_PLANE_PFA > 0
-  // b's first PFB registers are loaded during a's passes B and C, the first
-  // PFA blocks of a^ during b's pass C: in flight while the VALU works
-  // (a CU runs one of these workgroups, so nothing else hides a load)
-  constexpr int PFB = kPlanePfB, PFA = kPlanePfA;
-  uint32_t y[PFB > 0 ? PFB : 1];
-  plane_fwd<0, false>(x, lds, t, tw, mo, trace_id, [&]() {
-    if constexpr (PFB > 0) {
-      const uint32_t* bp = b + off;
-      asm volatile("" : "+s"(bp));
-      const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc((void*)bp, 0, (int)(4u << 16), 0x00020000);
-#pragma unroll
-      for (int r = 0; r < PFB; ++r) y[r] = __builtin_amdgcn_raw_buffer_load_b32(gb, t * 4u, (uint32_t)r << 12, kPlaneAux);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  });
-  plane_store_hat(ah, x, t);
-  PLANE_STAMP(0, 7);
-  PLANE_STAMP(1, 0);
-  {
-    const uint32_t* bp = b + off;
-    asm volatile("" : "+s"(bp));
-    const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc((void*)bp, 0, (int)(4u << 16), 0x00020000);
-#pragma unroll
-    for (int r = 0; r < 64; ++r)
-      x[r] = r < PFB ? y[r < PFB ? r : 0] : __builtin_amdgcn_raw_buffer_load_b32(gb, t * 4u, (uint32_t)r << 12, kPlaneAux);
-  }
-  PLANE_STAMP(1, 1);
-  // a^ comes back from this thread's own stores above; an opaque copy of
-  // the base keeps the compiler from holding the 16 store addresses live
-  // (in scratch) across b's transform
-  const uint4* ah2 = ah;
-  asm volatile("" : "+s"(ah2));
-  uint4 ap[PFA > 0 ? PFA : 1];
-  plane_fwd<1, true>(x, lds, t, tw, mo, trace_id, NoHook{}, [&ap, ah2, t]() {
-#pragma unroll
-    for (int kk = 0; kk < PFA; ++kk) ap[kk] = ah2[kk * 1024 + t];
-    __builtin_amdgcn_sched_barrier(0);
-  });
-  // (the block source captures the base by value: a by-reference capture
-  // undoes the opaque copy, and the store addresses go to scratch again)
-  plane_mul_tail<1>(x, lds, t, [&ap, ah2, t](int kk) { return kk < PFA ? ap[kk < PFA ? kk : 0] : ah2[kk * 1024 + t]; }, c + off,
-                    tw, tp.itw + (uint64_t)l * N, lc, mo, trace_id);
-#else
   plane_fwd<0, false>(x, lds, t, tw, mo, trace_id);
-  plane_store_hat(ah, x, t);
+  plane_store_hat(HatBuf(ah), x, t);
   PLANE_STAMP(0, 7);
   PLANE_STAMP(1, 0);
   plane_load(x, b + off, t);
   PLANE_STAMP(1, 1);
   plane_fwd<1, true>(x, lds, t, tw, mo, trace_id);
-  // a^ comes back from this thread's own stores above; an opaque copy of
-  // the base keeps the compiler from holding the 16 store addresses live
-  // (in scratch) across b's transform (the block source captures it by
-  // value: a by-reference capture undoes the copy)
-  const uint4* ah2 = ah;
+  // a^ comes back from this thread's own stores above (the descriptor is
+  // rebuilt from an opaque copy of the base, so nothing of the stores'
+  // addressing stays live across b's transform)
+  uint32_t* ah2 = ah;
   asm volatile("" : "+s"(ah2));
-  plane_mul_tail<1>(x, lds, t, [ah2, t](int kk) { return ah2[kk * 1024 + t]; }, c + off, tw,
-                    tp.itw + (uint64_t)l * N, lc, mo, trace_id);
-#endif
+  const HatBuf hb(ah2);
+  plane_mul_tail<1>(x, lds, t, [hb, t](int kk) { return hb.ld(t, kk); }, c + off, tw, tp.itw + (uint64_t)l * N, lc,
+                    mo, trace_id);
+}
+
+
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_fused(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
+              TabPtrs<uint32_t> tp, uint64_t ls, uint32_t cu_slots) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const uint32_t poly = blockIdx.x, l = blockIdx.y;
+  const uint64_t N = 1ull << 16;
+  // a^ goes to a scratch plane: per (poly, limb), or (cu_slots) per CU, so
+  // the launch's scratch footprint is 256 KiB per CU (64 MiB on 256 CUs),
+  // rewritten by the CU's next workgroup while it may still sit in the
+  // Infinity Cache
+  uint32_t* ah = scratch + (cu_slots ? (uint64_t)plane_cu_slot() * N : (uint64_t)l * ls + (uint64_t)poly * N);
+  plane_fused_one(c, a, b, ah, tp, ls, poly, l, (uint32_t*)smem_raw, threadIdx.x, poly + l * gridDim.x);
+}
+
+// Persistent form (RNT_PLANE=4): one workgroup per CU walks the planes p =
+// blockIdx.x, + gridDim.x, ... (poly p % B, limb p / B, so the chip works on
+// one limb's twiddles at a time), with its own a^ scratch plane: a plane's
+// product stores and the next plane's loads meet in one wave's queue instead
+// of a workgroup ending and the next one starting.
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_fused_p(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
+                TabPtrs<uint32_t> tp, uint64_t ls, uint32_t B, uint32_t planes) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* ah = scratch + (uint64_t)blockIdx.x * (1ull << 16);
+  for (uint32_t p = blockIdx.x; p < planes; p += gridDim.x) {
+    const uint32_t l = p / B, poly = p - l * B;
+    plane_fused_one(c, a, b, ah, tp, ls, poly, l, (uint32_t*)smem_raw, threadIdx.x, p);
+  }
 }
 
 #ifdef RNT_PLANE_TRACE
@@ -664,10 +739,33 @@ bool plane_fused_slots(const Launch& k) {
   return RNT_PLANE_SLOTS && (uint64_t)k.B * k.L >= kPlaneSlots;
 }
 
+static int plane_cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      n = v > 0 ? v : 256;
+    else
+      n = 256;
+  }
+  return n;
+}
+
 hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls) {
   if (k.B == 0 || k.L == 0) return hipSuccess;
   if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
   const size_t lds = (size_t)plane::LDS_WORDS * 4;
+  const uint64_t planes = (uint64_t)k.B * k.L;
+  if (k.t->plane == 4 && planes < 0xffffffffull) {
+    // one workgroup per CU, each with one a^ scratch plane (planes >= grid)
+    const unsigned grid = (unsigned)std::min<uint64_t>(planes, (uint64_t)plane_cu_count());
+    hipError_t e = allow_lds(k_plane_fused_p, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_plane_fused_p, dim3(grid), dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)a,
+                       (const uint32_t*)b, (uint32_t*)scratch, tab_ptrs<uint32_t>(k.t), ls, (uint32_t)k.B,
+                       (uint32_t)planes);
+    return hipGetLastError();
+  }
   hipError_t e = allow_lds(k_plane_fused, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_plane_fused, dim3((unsigned)k.B, (unsigned)k.L), dim3(plane::T), lds, k.s, (uint32_t*)out,
