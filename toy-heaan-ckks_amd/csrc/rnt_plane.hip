@@ -65,54 +65,80 @@ __host__ __device__ constexpr int slot(int r) {
 }
 }  // namespace plane
 
-// CT stages on logical register bits SLHI .. SLLO of layout LY (index bits
-// [BB, BB + 6)); node0 = 2^16 + the thread's index with register bits 0.
-// Twiddles in chunks of CH per stage (bounded registers beside the plane).
-// As in pass_ct, outputs the next stage of the pass only multiplies stay
-// in [0, 2q); the last stage leaves everything canonical.  Stages and
-// chunks are template recursions, so every register index is a
-// compile-time constant (a loop the unroller gave up on would put the
-// plane in scratch memory).
+// Cache policy (buffer aux bits) of the streamed operand loads and the
+// product store: 0 default, 2 non-temporal (A/B knob, -DRNT_PLANE_AUX=2).
+#ifndef RNT_PLANE_AUX
+#define RNT_PLANE_AUX 0
+#endif
+constexpr int kPlaneAux = RNT_PLANE_AUX;
+// Twiddles per scalar-load chunk in pass A (64 SGPRs at 32)
+#ifndef RNT_PLANE_CHA
+#define RNT_PLANE_CHA 32
+#endif
+constexpr int kPlaneChA = RNT_PLANE_CHA;
+// a^ blocks in flight ahead of the degree-3 block products (0: loaded at use)
+#ifndef RNT_PLANE_AHD
+#define RNT_PLANE_AHD 4
+#endif
+constexpr int kPlaneAhd = RNT_PLANE_AHD;
+// X1 through 8-byte LDS words (1) or 4-byte ones (0, default: the 8-byte
+// form measured flat, profiles/r03/ab_plane_x1wide_preg.txt)
+#ifndef RNT_PLANE_X1W
+#define RNT_PLANE_X1W 0
+#endif
+constexpr bool kPlaneX1Wide = RNT_PLANE_X1W != 0;
+
 // Pass C's per-thread twiddles (stages at index bits 5..2: 1, 2, 4 and 8
 // of them), loaded ahead of the X2 exchange so the loads are in flight
 // during it instead of stalling each stage of the pass.
 #ifndef RNT_PLANE_PREC
-#define RNT_PLANE_PREC 3  // pass C stages whose twiddles are preloaded (0..4)
+#define RNT_PLANE_PREC 3  // forward pass C stages whose twiddles are preloaded (0..4)
 #endif
-struct TwPreC {
+#ifndef RNT_PLANE_PREG
+#define RNT_PLANE_PREG 0  // inverse pass C stages preloaded (0..4; 1 measured flat)
+#endif
+// Pass C's per-thread twiddles (stages at index bits 5..2: 1, 2, 4 and 8 of
+// them), the stages in MASK (bit SL - 2) loaded ahead: before the X2
+// exchange in the forward transforms, during the last block products in the
+// inverse, so the loads are in flight while other work runs instead of
+// stalling the stage that needs them.  Other stages fetch at the stage.
+template <int MASK>
+struct TwPre {
   const Tw<uint32_t>* b;
-  uint32_t node0;
   Tw<uint32_t> s5[1], s4[2], s3[4], s2[8];
 };
-__device__ __forceinline__ TwPreC plane_prec(const Tw<uint32_t>* b, uint32_t node0) {
-  TwPreC p;
+template <int MASK>
+__device__ __forceinline__ TwPre<MASK> plane_pre(const Tw<uint32_t>* b, uint32_t node0) {
+  TwPre<MASK> p;
   p.b = b;
-  p.node0 = node0;
-  if constexpr (RNT_PLANE_PREC >= 1) p.s5[0] = tw_get<uint32_t>(b, node0 >> 6, 0u);
-  if constexpr (RNT_PLANE_PREC >= 2) {
+  if constexpr (MASK & 8) p.s5[0] = tw_get<uint32_t>(b, node0 >> 6, 0u);
+  if constexpr (MASK & 4) {
 #pragma unroll
     for (int m = 0; m < 2; ++m) p.s4[m] = tw_get<uint32_t>(b, node0 >> 5, (uint32_t)m);
   }
-  if constexpr (RNT_PLANE_PREC >= 3) {
+  if constexpr (MASK & 2) {
 #pragma unroll
     for (int m = 0; m < 4; ++m) p.s3[m] = tw_get<uint32_t>(b, node0 >> 4, (uint32_t)m);
   }
-  if constexpr (RNT_PLANE_PREC >= 4) {
+  if constexpr (MASK & 1) {
 #pragma unroll
     for (int m = 0; m < 8; ++m) p.s2[m] = tw_get<uint32_t>(b, node0 >> 3, (uint32_t)m);
   }
   return p;
 }
+// Forward: the first PREC stages (5, 4, ...); inverse: the first PREG (2, 3, ...).
+constexpr int kPreFwd = (0xF0 >> RNT_PLANE_PREC) & 0xF;
+constexpr int kPreInv = (1 << RNT_PLANE_PREG) - 1;
 // Twiddle m of a stage chunk at index bit SL (+ BB): from the source, or
 // from the preloaded set.
 template <int SL, class TS>
 __device__ __forceinline__ Tw<uint32_t> tw_fetch(const TS& ts, uint32_t nb, uint32_t m) {
   return tw_get<uint32_t>(ts, nb, m);
 }
-template <int SL>
-__device__ __forceinline__ Tw<uint32_t> tw_fetch(const TwPreC& p, uint32_t nb, uint32_t m) {
+template <int SL, int MASK>
+__device__ __forceinline__ Tw<uint32_t> tw_fetch(const TwPre<MASK>& p, uint32_t nb, uint32_t m) {
   static_assert(SL >= 2 && SL <= 5, "pass C stages");
-  if constexpr (5 - SL >= RNT_PLANE_PREC) return tw_get<uint32_t>(p.b, nb, m);
+  if constexpr (!(MASK & (1 << (SL - 2)))) return tw_get<uint32_t>(p.b, nb, m);
   else if constexpr (SL == 5) return p.s5[0];
   else if constexpr (SL == 4) return p.s4[m];
   else if constexpr (SL == 3) return p.s3[m];
@@ -193,6 +219,14 @@ __device__ __forceinline__ void plane_gs_groups(uint32_t (&x)[64], const Tw<uint
   }
 }
 
+// CT stages on logical register bits SLHI .. SLLO of layout LY (index bits
+// [BB, BB + 6)); node0 = 2^16 + the thread's index with register bits 0.
+// Twiddles in chunks of CH per stage (bounded registers beside the plane).
+// As in pass_ct, outputs the next stage of the pass only multiplies stay
+// in [0, 2q); the last stage leaves everything canonical.  Stages and
+// chunks are template recursions, so every register index is a
+// compile-time constant (a loop the unroller gave up on would put the
+// plane in scratch memory).
 template <int LY, int BB, int SL, int SLLO, int M0, int CH, class TS>
 __device__ __forceinline__ void plane_ct_chunks(uint32_t (&x)[64], uint32_t nb, const TS& tw,
                                                 const Mod<uint32_t>& mo) {
@@ -242,7 +276,7 @@ __device__ __forceinline__ void plane_gs_chunks(uint32_t (&x)[64], uint32_t nb, 
   Tw<uint32_t> t[n];
 #pragma unroll
   for (int j = 0; j < n; ++j)
-    t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_get<uint32_t>(itw, nb, (uint32_t)(M0 + j));
+    t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<BB + SL>(itw, nb, (uint32_t)(M0 + j));
   if constexpr (RNT_PLANE_ASM != 0) {
     plane_gs_groups<LY, SL, M0, tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0>(x, t, mo);
     if constexpr (M0 + CH < cnt) plane_gs_chunks<LY, BB, SL, M0 + CH, CH>(x, nb, itw, mo);
@@ -285,6 +319,40 @@ __device__ __forceinline__ void plane_x1(uint32_t (&x)[64], uint32_t* lds, uint3
   const uint32_t w = t >> 6, lam = t & 63u;
   if constexpr ((RNT_PLANE_EXP & 16) != 0) return;
   if constexpr (SYNC_FIRST) __syncthreads();
+  if constexpr (kPlaneX1Wide) {
+    // 8-byte LDS words: pairs differing in index bit 11, a register bit on
+    // both sides (L0 registers 4m + h, 4m + 2 + h; L1 registers 2k + h,
+    // 2k + 32 + h); pair address = the index without bits 10 and 11.
+    // ds_write_b64 / ds_read_b64 move 85 / 256 B per clock against 64 / 128
+    // for the 4-byte forms, and every access stays 16 (32) consecutive pairs
+    // per lane group: conflict-free.
+    uint2* lp = (uint2*)lds;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if constexpr (TO_L1)
+          lp[((uint32_t)m << 10) | t] = make_uint2(x[4 * m + h], x[4 * m + 2 + h]);
+        else
+          lp[(w << 10) | ((uint32_t)m << 6) | lam] = make_uint2(x[2 * m + h], x[2 * m + 32 + h]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if constexpr (TO_L1) {
+          const uint2 v = lp[(w << 10) | ((uint32_t)m << 6) | lam];
+          x[2 * m + h] = v.x;
+          x[2 * m + 32 + h] = v.y;
+        } else {
+          const uint2 v = lp[((uint32_t)m << 10) | t];
+          x[4 * m + h] = v.x;
+          x[4 * m + 2 + h] = v.y;
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -394,22 +462,6 @@ __device__ uint64_t g_plane_trace[2 * kTraceWg * 16 * kTraceStamps];
 // bit 1: no plane loads (synthetic words); bit 2: no plane stores;
 // bit 3: no twiddle loads in the passes (one constant); bit 4: no X1 / X2.
 
-// Cache policy (buffer aux bits) of the streamed operand loads and the
-// product store: 0 default, 2 non-temporal (A/B knob, -DRNT_PLANE_AUX=2).
-#ifndef RNT_PLANE_AUX
-#define RNT_PLANE_AUX 0
-#endif
-constexpr int kPlaneAux = RNT_PLANE_AUX;
-// Twiddles per scalar-load chunk in pass A (64 SGPRs at 32)
-#ifndef RNT_PLANE_CHA
-#define RNT_PLANE_CHA 32
-#endif
-constexpr int kPlaneChA = RNT_PLANE_CHA;
-// a^ blocks in flight ahead of the degree-3 block products (0: loaded at use)
-#ifndef RNT_PLANE_AHD
-#define RNT_PLANE_AHD 4
-#endif
-constexpr int kPlaneAhd = RNT_PLANE_AHD;
 // ... and in pass B (wave-uniform too)
 #ifndef RNT_PLANE_CHB
 #define RNT_PLANE_CHB 16
@@ -488,7 +540,7 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
   plane_ct<1, 6, 3, 0, kPlaneChB>(x, N + (wu << 12), tws, mo);
   PLANE_STAMP(K, 4);
-  const TwPreC pc = plane_prec(tw, N + (t << 6));
+  const auto pc = plane_pre<kPreFwd>(tw, N + (t << 6));
   plane_x2<true>(x, lds, t);
   PLANE_STAMP(K, 5);
   after_x2();
@@ -518,6 +570,8 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
   constexpr int D = kPlaneAhd, Z = D > 0 ? (D + 1) / 2 + 1 : 1;  // zeta j serves blocks 2j, 2j + 1
   uint4 abuf[D > 0 ? D : 1];
   Tw<uint32_t> zbuf[Z];
+  TwPre<kPreInv> gpre;  // the inverse pass C's first stages, loaded during the last products
+  if constexpr (D == 0) gpre = plane_pre<kPreInv>(itw, n0 + (t << 6));
   if constexpr (D > 0) {
 #pragma unroll
     for (int d = 0; d < D; ++d) abuf[d] = ah(d);
@@ -536,6 +590,7 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
       av = abuf[kk % D];
       w = zbuf[(kk >> 1) % Z];
       if (kk + D < 16) abuf[kk % D] = ah(kk + D);
+      if (kk == 16 - D) gpre = plane_pre<kPreInv>(itw, n0 + (t << 6));
       if ((kk & 1) && (kk >> 1) + Z < 8) zbuf[(kk >> 1) % Z] = tw[zb + (kk >> 1) + Z];
       __builtin_amdgcn_sched_barrier(0);
     } else {
@@ -557,7 +612,7 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
   if constexpr ((RNT_PLANE_EXP & 1) != 0)
     plane_gs<2, 0, 2, 5, 8, false>(x, n0, itws, mo, Fold<uint32_t>{});
   else
-    plane_gs<2, 0, 2, 5, 8, false>(x, n0 + (t << 6), itw, mo, Fold<uint32_t>{});
+    plane_gs<2, 0, 2, 5, 8, false>(x, n0 + (t << 6), gpre, mo, Fold<uint32_t>{});
   PLANE_STAMP(K, 8);
   plane_x2<false>(x, lds, t);
   PLANE_STAMP(K, 9);
