@@ -254,6 +254,21 @@ def uniform(rng, mods, count, n):
     return rng.integers(0, 1 << 62, size=(count, len(mods), n), dtype=np.uint64) % q
 
 
+def pmc_field(kernel, workload, batch, log_n, L, field):
+    """Another per-launch field (e.g. SQ_INSTS_VALU) of the same committed
+    pass as traffic_for; None when none of this shape is committed."""
+    tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(tpath) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for e in t.get("entries", []):
+        if (e.get("workload"), e.get("batch"), e.get("log_n"), e.get("L")) == (workload, batch, log_n, L):
+            return e.get("kernels", {}).get(kernel, {}).get(field)
+    return None
+
+
 def traffic_for(kernel, workload, batch, log_n, L):
     """HBM bytes per launch of `kernel` (2 x FETCH_SIZE + WRITE_SIZE, the
     gfx950 correction of MI355X_MICROARCH.md § HBM) from the committed
@@ -435,6 +450,25 @@ def run_polymul(args, comm, world, rank, local_rank):
         kroof["row_mul"].update(valu_unit="butterflies/s", bfly_per_launch=rb,
                                 row_stages_per_transform=stages, truncated_transform=trunc,
                                 valu_achieved=ra, valu_peak=VALU_PEAK_BFLY, valu_frac=ra / VALU_PEAK_BFLY)
+    if "plane_fused" in kernels:
+        # the whole-plane kernel is bound by VALU issue: its
+        # butterflies per second (three truncated 14-stage transforms per
+        # (poly, limb); block products not counted) against VALU_PEAK_BFLY,
+        # and its VALU wave-instructions (committed PMC pass of this shape)
+        # per second against one wave64 instruction per 4 cycles per SIMD at
+        # 2.4 GHz -- the issue cost tools/bflyrate.hip measures for these
+        # 32-bit integer ops.
+        pb = 21 * elem * args.steps / kernels["plane_fused"]["launches"]
+        pa = pb / (kernels["plane_fused"]["avg_ms"] * 1e-3)
+        kroof["plane_fused"].update(valu_unit="butterflies/s", bfly_per_launch=pb, valu_achieved=pa,
+                                    valu_peak=VALU_PEAK_BFLY, valu_frac=pa / VALU_PEAK_BFLY)
+        vi = pmc_field("plane_fused", "polymul", batch, args.log_n, Lr, "SQ_INSTS_VALU") \
+            if args.prime_bits == 31 else None
+        if vi:
+            ipeak = 1024 * 2.4e9 / 4
+            ia = vi / (kernels["plane_fused"]["avg_ms"] * 1e-3)
+            kroof["plane_fused"].update(valu_instr_per_launch_pmc=vi, valu_issue_per_s=ia,
+                                        valu_issue_peak=ipeak, valu_issue_frac=ia / ipeak)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(mod, n, args.cpu_seconds)
