@@ -65,6 +65,11 @@ __host__ __device__ constexpr int slot(int r) {
 }
 }  // namespace plane
 
+// Butterflies as interleaved groups of four in inline asm (rnt_bfly4.hpp):
+// 1 (default) or 0 (the C++ butterflies of rnt_modarith.hpp, A/B).
+#ifndef RNT_PLANE_ASM
+#define RNT_PLANE_ASM 1
+#endif
 // Cache policy (buffer aux bits) of the streamed operand loads and the
 // product store: 0 default, 2 non-temporal (A/B knob, -DRNT_PLANE_AUX=2).
 #ifndef RNT_PLANE_AUX
@@ -87,6 +92,13 @@ constexpr int kPlaneAhd = RNT_PLANE_AHD;
 #define RNT_PLANE_X1W 0
 #endif
 constexpr bool kPlaneX1Wide = RNT_PLANE_X1W != 0;
+// X1 in two rounds with pass B (gs B) of one half between them (1, needs
+// the asm butterflies, which can run one half of the L1 registers) or as
+// one exchange (0)
+#ifndef RNT_PLANE_X1SPLIT
+#define RNT_PLANE_X1SPLIT 1
+#endif
+constexpr bool kPlaneX1Split = RNT_PLANE_X1SPLIT != 0 && RNT_PLANE_ASM != 0;
 
 // Pass C's per-thread twiddles (stages at index bits 5..2: 1, 2, 4 and 8
 // of them), loaded ahead of the X2 exchange so the loads are in flight
@@ -145,11 +157,6 @@ __device__ __forceinline__ Tw<uint32_t> tw_fetch(const TwPre<MASK>& p, uint32_t 
   else return p.s2[m];
 }
 
-// Butterflies as interleaved groups of four in inline asm (rnt_bfly4.hpp):
-// 1 (default) or 0 (the C++ butterflies of rnt_modarith.hpp, A/B).
-#ifndef RNT_PLANE_ASM
-#define RNT_PLANE_ASM 1
-#endif
 template <class TS>
 constexpr bool tw_uniform() {
   return std::is_same<TS, TwScalar<uint32_t>>::value;
@@ -160,62 +167,76 @@ constexpr bool tw_uniform() {
 // set (i & (d >> 1)) are the lazy ones (both outputs only multiplied next);
 // each class is grouped on its own.  Butterfly m of class CLS: twiddle j =
 // m / HALF, e = CLS * HALF + m % HALF.
-template <int LY, int SL, int M0, int HALF, bool LAZY, bool SW, int n>
+template <int LY, int SL, int M0, int HALF, bool LAZY, bool SW, int HM, int n>
 __device__ __forceinline__ void plane_ct_groups(uint32_t (&x)[64], const Tw<uint32_t> (&t)[n], const Mod<uint32_t>& mo) {
   constexpr int d = 1 << SL, per = n * HALF, e0 = LAZY ? HALF : 0;
-  static_assert(per % 4 == 0, "butterfly groups of four");
+  // HM >= 0: only the butterflies of logical registers with bit 4 == HM
+  // (one half of the L1 registers, which X1 delivers in two rounds)
+  int jl[per], il[per];
+  int cnt = 0;
+#pragma unroll
+  for (int m = 0; m < per; ++m) {
+    const int j = m / HALF, i = ((M0 + j) << (SL + 1)) | (e0 + m % HALF);
+    if (HM < 0 || ((i >> 4) & 1) == HM) {
+      jl[cnt] = j;
+      il[cnt] = i;
+      ++cnt;
+    }
+  }
 #pragma unroll
   for (int g = 0; g < per / 4; ++g) {
-    int il[4], jj[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int m = 4 * g + k;
-      jj[k] = m / HALF;
-      il[k] = ((M0 + jj[k]) << (SL + 1)) | (e0 + m % HALF);
-    }
+    if (4 * g + 3 >= cnt) break;
+    const int* ii = il + 4 * g;
+    const int* jj = jl + 4 * g;
     const uint32_t w[4] = {t[jj[0]].w, t[jj[1]].w, t[jj[2]].w, t[jj[3]].w};
     const uint32_t wp[4] = {t[jj[0]].p, t[jj[1]].p, t[jj[2]].p, t[jj[3]].p};
     uint64_t P[4];
-    b4::shoup_prod4<SW>(P, x[plane::slot<LY>(il[0] | d)], x[plane::slot<LY>(il[1] | d)],
-                        x[plane::slot<LY>(il[2] | d)], x[plane::slot<LY>(il[3] | d)], w, wp, mo.nq);
+    b4::shoup_prod4<SW>(P, x[plane::slot<LY>(ii[0] | d)], x[plane::slot<LY>(ii[1] | d)],
+                        x[plane::slot<LY>(ii[2] | d)], x[plane::slot<LY>(ii[3] | d)], w, wp, mo.nq);
     uint32_t pl[4] = {(uint32_t)P[0], (uint32_t)P[1], (uint32_t)P[2], (uint32_t)P[3]};
     if constexpr (LAZY)
-      b4::ct_reduce4_lazy(x[plane::slot<LY>(il[0])], x[plane::slot<LY>(il[1])], x[plane::slot<LY>(il[2])],
-                          x[plane::slot<LY>(il[3])], x[plane::slot<LY>(il[0] | d)], x[plane::slot<LY>(il[1] | d)],
-                          x[plane::slot<LY>(il[2] | d)], x[plane::slot<LY>(il[3] | d)], pl, mo.q);
+      b4::ct_reduce4_lazy(x[plane::slot<LY>(ii[0])], x[plane::slot<LY>(ii[1])], x[plane::slot<LY>(ii[2])],
+                          x[plane::slot<LY>(ii[3])], x[plane::slot<LY>(ii[0] | d)], x[plane::slot<LY>(ii[1] | d)],
+                          x[plane::slot<LY>(ii[2] | d)], x[plane::slot<LY>(ii[3] | d)], pl, mo.q);
     else
-      b4::ct_reduce4(x[plane::slot<LY>(il[0])], x[plane::slot<LY>(il[1])], x[plane::slot<LY>(il[2])],
-                     x[plane::slot<LY>(il[3])], x[plane::slot<LY>(il[0] | d)], x[plane::slot<LY>(il[1] | d)],
-                     x[plane::slot<LY>(il[2] | d)], x[plane::slot<LY>(il[3] | d)], pl, mo.q);
+      b4::ct_reduce4(x[plane::slot<LY>(ii[0])], x[plane::slot<LY>(ii[1])], x[plane::slot<LY>(ii[2])],
+                     x[plane::slot<LY>(ii[3])], x[plane::slot<LY>(ii[0] | d)], x[plane::slot<LY>(ii[1] | d)],
+                     x[plane::slot<LY>(ii[2] | d)], x[plane::slot<LY>(ii[3] | d)], pl, mo.q);
   }
 }
 
 // GS butterflies of a stage chunk in groups of four: (u, v) <- (u + v,
 // (u - v) w), every output canonical.
-template <int LY, int SL, int M0, bool SW, int n>
+template <int LY, int SL, int M0, bool SW, int HM, int n>
 __device__ __forceinline__ void plane_gs_groups(uint32_t (&x)[64], const Tw<uint32_t> (&t)[n], const Mod<uint32_t>& mo) {
   constexpr int d = 1 << SL, per = n * d;
-  static_assert(per % 4 == 0, "butterfly groups of four");
+  int jl[per], il[per];
+  int cnt = 0;
+#pragma unroll
+  for (int m = 0; m < per; ++m) {
+    const int j = m / d, i = ((M0 + j) << (SL + 1)) | (m % d);
+    if (HM < 0 || ((i >> 4) & 1) == HM) {
+      jl[cnt] = j;
+      il[cnt] = i;
+      ++cnt;
+    }
+  }
 #pragma unroll
   for (int g = 0; g < per / 4; ++g) {
-    int il[4], jj[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int m = 4 * g + k;
-      jj[k] = m / d;
-      il[k] = ((M0 + jj[k]) << (SL + 1)) | (m % d);
-    }
+    if (4 * g + 3 >= cnt) break;
+    const int* ii = il + 4 * g;
+    const int* jj = jl + 4 * g;
     const uint32_t w[4] = {t[jj[0]].w, t[jj[1]].w, t[jj[2]].w, t[jj[3]].w};
     const uint32_t wp[4] = {t[jj[0]].p, t[jj[1]].p, t[jj[2]].p, t[jj[3]].p};
     uint32_t dd[4];
-    b4::gs_pre4(x[plane::slot<LY>(il[0])], x[plane::slot<LY>(il[1])], x[plane::slot<LY>(il[2])],
-                x[plane::slot<LY>(il[3])], x[plane::slot<LY>(il[0] | d)], x[plane::slot<LY>(il[1] | d)],
-                x[plane::slot<LY>(il[2] | d)], x[plane::slot<LY>(il[3] | d)], dd, mo.q);
+    b4::gs_pre4(x[plane::slot<LY>(ii[0])], x[plane::slot<LY>(ii[1])], x[plane::slot<LY>(ii[2])],
+                x[plane::slot<LY>(ii[3])], x[plane::slot<LY>(ii[0] | d)], x[plane::slot<LY>(ii[1] | d)],
+                x[plane::slot<LY>(ii[2] | d)], x[plane::slot<LY>(ii[3] | d)], dd, mo.q);
     uint64_t P[4];
     b4::shoup_prod4<SW>(P, dd[0], dd[1], dd[2], dd[3], w, wp, mo.nq);
     const uint32_t pl[4] = {(uint32_t)P[0], (uint32_t)P[1], (uint32_t)P[2], (uint32_t)P[3]};
-    b4::csub4(x[plane::slot<LY>(il[0] | d)], x[plane::slot<LY>(il[1] | d)], x[plane::slot<LY>(il[2] | d)],
-              x[plane::slot<LY>(il[3] | d)], pl, mo.q);
+    b4::csub4(x[plane::slot<LY>(ii[0] | d)], x[plane::slot<LY>(ii[1] | d)], x[plane::slot<LY>(ii[2] | d)],
+              x[plane::slot<LY>(ii[3] | d)], pl, mo.q);
   }
 }
 
@@ -227,7 +248,7 @@ __device__ __forceinline__ void plane_gs_groups(uint32_t (&x)[64], const Tw<uint
 // chunks are template recursions, so every register index is a
 // compile-time constant (a loop the unroller gave up on would put the
 // plane in scratch memory).
-template <int LY, int BB, int SL, int SLLO, int M0, int CH, class TS>
+template <int LY, int BB, int SL, int SLLO, int M0, int CH, int HM = -1, class TS>
 __device__ __forceinline__ void plane_ct_chunks(uint32_t (&x)[64], uint32_t nb, const TS& tw,
                                                 const Mod<uint32_t>& mo) {
   constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
@@ -238,12 +259,12 @@ __device__ __forceinline__ void plane_ct_chunks(uint32_t (&x)[64], uint32_t nb, 
   if constexpr (RNT_PLANE_ASM != 0) {
     constexpr bool SW = tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0;
     if constexpr (SL > SLLO) {
-      plane_ct_groups<LY, SL, M0, d / 2, false, SW>(x, t, mo);
-      plane_ct_groups<LY, SL, M0, d / 2, true, SW>(x, t, mo);
+      plane_ct_groups<LY, SL, M0, d / 2, false, SW, HM>(x, t, mo);
+      plane_ct_groups<LY, SL, M0, d / 2, true, SW, HM>(x, t, mo);
     } else {
-      plane_ct_groups<LY, SL, M0, d, false, SW>(x, t, mo);
+      plane_ct_groups<LY, SL, M0, d, false, SW, HM>(x, t, mo);
     }
-    if constexpr (M0 + CH < cnt) plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH>(x, nb, tw, mo);
+    if constexpr (M0 + CH < cnt) plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH, HM>(x, nb, tw, mo);
     return;
   }
 #pragma unroll
@@ -259,17 +280,17 @@ __device__ __forceinline__ void plane_ct_chunks(uint32_t (&x)[64], uint32_t nb, 
   }
   if constexpr (M0 + CH < cnt) plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH>(x, nb, tw, mo);
 }
-template <int LY, int BB, int SL, int SLLO, int CH, class TS>
+template <int LY, int BB, int SL, int SLLO, int CH, int HM = -1, class TS>
 __device__ __forceinline__ void plane_ct(uint32_t (&x)[64], uint32_t node0, const TS& tw,
                                          const Mod<uint32_t>& mo) {
-  plane_ct_chunks<LY, BB, SL, SLLO, 0, CH>(x, node0 >> (BB + SL + 1), tw, mo);
-  if constexpr (SL > SLLO) plane_ct<LY, BB, SL - 1, SLLO, CH>(x, node0, tw, mo);
+  plane_ct_chunks<LY, BB, SL, SLLO, 0, CH, HM>(x, node0 >> (BB + SL + 1), tw, mo);
+  if constexpr (SL > SLLO) plane_ct<LY, BB, SL - 1, SLLO, CH, HM>(x, node0, tw, mo);
 }
 
 // GS stages on logical register bits SLLO .. SLHI; FOLD: the stage at
 // index bit 15 applies the folded constants (4/N with the Montgomery
 // factor, LimbConst c1t/c2t) instead of its twiddle.
-template <int LY, int BB, int SL, int M0, int CH, class TS>
+template <int LY, int BB, int SL, int M0, int CH, int HM = -1, class TS>
 __device__ __forceinline__ void plane_gs_chunks(uint32_t (&x)[64], uint32_t nb, const TS& itw,
                                                 const Mod<uint32_t>& mo) {
   constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
@@ -278,8 +299,8 @@ __device__ __forceinline__ void plane_gs_chunks(uint32_t (&x)[64], uint32_t nb, 
   for (int j = 0; j < n; ++j)
     t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<BB + SL>(itw, nb, (uint32_t)(M0 + j));
   if constexpr (RNT_PLANE_ASM != 0) {
-    plane_gs_groups<LY, SL, M0, tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0>(x, t, mo);
-    if constexpr (M0 + CH < cnt) plane_gs_chunks<LY, BB, SL, M0 + CH, CH>(x, nb, itw, mo);
+    plane_gs_groups<LY, SL, M0, tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0, HM>(x, t, mo);
+    if constexpr (M0 + CH < cnt) plane_gs_chunks<LY, BB, SL, M0 + CH, CH, HM>(x, nb, itw, mo);
     return;
   }
 #pragma unroll
@@ -292,7 +313,7 @@ __device__ __forceinline__ void plane_gs_chunks(uint32_t (&x)[64], uint32_t nb, 
   }
   if constexpr (M0 + CH < cnt) plane_gs_chunks<LY, BB, SL, M0 + CH, CH>(x, nb, itw, mo);
 }
-template <int LY, int BB, int SL, int SLHI, int CH, bool FOLD, class TS>
+template <int LY, int BB, int SL, int SLHI, int CH, bool FOLD, int HM = -1, class TS>
 __device__ __forceinline__ void plane_gs(uint32_t (&x)[64], uint32_t node0, const TS& itw,
                                          const Mod<uint32_t>& mo, const Fold<uint32_t>& f) {
   constexpr int d = 1 << SL;
@@ -304,9 +325,9 @@ __device__ __forceinline__ void plane_gs(uint32_t (&x)[64], uint32_t node0, cons
       x[plane::slot<LY>(e | d)] = shoup_mul(u - v + mo.q, f.c2, f.c2p, mo);
     }
   } else {
-    plane_gs_chunks<LY, BB, SL, 0, CH>(x, node0 >> (BB + SL + 1), itw, mo);
+    plane_gs_chunks<LY, BB, SL, 0, CH, HM>(x, node0 >> (BB + SL + 1), itw, mo);
   }
-  if constexpr (SL < SLHI) plane_gs<LY, BB, SL + 1, SLHI, CH, FOLD>(x, node0, itw, mo, f);
+  if constexpr (SL < SLHI) plane_gs<LY, BB, SL + 1, SLHI, CH, FOLD, HM>(x, node0, itw, mo, f);
 }
 
 // X1, L0 <-> L1 through LDS.  Round h carries the words with index bit
@@ -370,6 +391,28 @@ __device__ __forceinline__ void plane_x1(uint32_t (&x)[64], uint32_t* lds, uint3
     }
     __syncthreads();
   }
+}
+
+// One round of X1 (4-byte words), as plane_x1: WRITE puts round H's
+// registers into LDS, !WRITE takes them out.  plane_fwd / plane_mul_tail
+// split X1 into these so that pass B (gs B) of the half already delivered
+// (still to be sent) runs while the other round's LDS traffic drains.
+template <bool TO_L1, int H, bool WRITE>
+__device__ __forceinline__ void plane_x1_round(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
+  if constexpr ((RNT_PLANE_EXP & 16) != 0) return;
+  const uint32_t w = t >> 6, lam = t & 63u;
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    const uint32_t j0 = ((uint32_t)k << 10) | t;
+    const uint32_t j1 = ((((w << 1) | ((uint32_t)k >> 4))) << 10) | (((uint32_t)k & 15u) << 6) | lam;
+    if constexpr (WRITE)
+      lds[TO_L1 ? j0 : j1] = x[2 * k + H];
+    else
+      x[2 * k + H] = lds[TO_L1 ? j1 : j0];
+  }
+}
+__device__ __forceinline__ void plane_sync() {
+  if constexpr ((RNT_PLANE_EXP & 16) == 0) __syncthreads();
 }
 
 // Lane bit 5 <-> L1 register bit 5 and lane bit 4 <-> register bit 4
@@ -534,11 +577,28 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   // wave-uniform (scalar loads)
   plane_ct<0, 10, 5, 0, kPlaneChA>(x, N, tws, mo);
   PLANE_STAMP(K, 2);
-  plane_x1<true, SYNC1>(x, lds, t);
-  PLANE_STAMP(K, 3);
-  after_x1();
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
-  plane_ct<1, 6, 3, 0, kPlaneChB>(x, N + (wu << 12), tws, mo);
+  if constexpr (kPlaneX1Split) {
+    // X1 in its two rounds, pass B of round 0's half while round 1 drains
+    if constexpr (SYNC1) plane_sync();
+    plane_x1_round<true, 0, true>(x, lds, t);
+    plane_sync();
+    plane_x1_round<true, 0, false>(x, lds, t);
+    plane_sync();
+    plane_x1_round<true, 1, true>(x, lds, t);
+    PLANE_STAMP(K, 3);
+    after_x1();
+    plane_ct<1, 6, 3, 0, kPlaneChB, 0>(x, N + (wu << 12), tws, mo);
+    plane_sync();
+    plane_x1_round<true, 1, false>(x, lds, t);
+    plane_ct<1, 6, 3, 0, kPlaneChB, 1>(x, N + (wu << 12), tws, mo);
+    plane_sync();  // X2's buffers overlap the X1 region
+  } else {
+    plane_x1<true, SYNC1>(x, lds, t);
+    PLANE_STAMP(K, 3);
+    after_x1();
+    plane_ct<1, 6, 3, 0, kPlaneChB>(x, N + (wu << 12), tws, mo);
+  }
   PLANE_STAMP(K, 4);
   const auto pc = plane_pre<kPreFwd>(tw, N + (t << 6));
   plane_x2<true>(x, lds, t);
@@ -617,9 +677,25 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
   plane_x2<false>(x, lds, t);
   PLANE_STAMP(K, 9);
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
-  plane_gs<1, 6, 0, 3, kPlaneChB, false>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
-  PLANE_STAMP(K, 10);
-  plane_x1<false, true>(x, lds, t);  // other waves may still be in their X2
+  if constexpr (kPlaneX1Split) {
+    // gs B of round 0's half, X1 round 0 written while gs B of the other half runs
+    plane_gs<1, 6, 0, 3, kPlaneChB, false, 0>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+    plane_sync();  // other waves may still be in their X2
+    plane_x1_round<false, 0, true>(x, lds, t);
+    plane_gs<1, 6, 0, 3, kPlaneChB, false, 1>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+    PLANE_STAMP(K, 10);
+    plane_sync();
+    plane_x1_round<false, 0, false>(x, lds, t);
+    plane_sync();
+    plane_x1_round<false, 1, true>(x, lds, t);
+    plane_sync();
+    plane_x1_round<false, 1, false>(x, lds, t);
+    plane_sync();
+  } else {
+    plane_gs<1, 6, 0, 3, kPlaneChB, false>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+    PLANE_STAMP(K, 10);
+    plane_x1<false, true>(x, lds, t);  // other waves may still be in their X2
+  }
   PLANE_STAMP(K, 11);
   plane_gs<0, 10, 0, 5, kPlaneChA, true>(x, n0, itws, mo, Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p});
   PLANE_STAMP(K, 12);
