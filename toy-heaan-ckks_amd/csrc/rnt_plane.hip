@@ -76,6 +76,11 @@ __host__ __device__ constexpr int slot(int r) {
 #define RNT_PLANE_AUX 0
 #endif
 constexpr int kPlaneAux = RNT_PLANE_AUX;
+// plane loads in pass A's first-stage order (1) or register order (0)
+#ifndef RNT_PLANE_LOAD_ORDER
+#define RNT_PLANE_LOAD_ORDER 1
+#endif
+constexpr bool kPlaneLoadOrder = RNT_PLANE_LOAD_ORDER != 0;
 // Twiddles per scalar-load chunk in pass A (64 SGPRs at 32)
 #ifndef RNT_PLANE_CHA
 #define RNT_PLANE_CHA 32
@@ -503,7 +508,8 @@ __device__ uint64_t g_plane_trace[2 * kTraceWg * 16 * kTraceStamps];
 // Measurement builds (tools/build_variant.sh, wrong results by design):
 // RNT_PLANE_EXP bit 0: pass C / inverse pass C twiddles wave-uniform;
 // bit 1: no plane loads (synthetic words); bit 2: no plane stores;
-// bit 3: no twiddle loads in the passes (one constant); bit 4: no X1 / X2.
+// bit 3: no twiddle loads in the passes (one constant); bit 4: no X1 / X2;
+// bit 5: no product store; bit 6: no a^ store (the a^ loads stay).
 
 // ... and in pass B (wave-uniform too)
 #ifndef RNT_PLANE_CHB
@@ -519,8 +525,14 @@ __device__ __forceinline__ void plane_load(uint32_t (&x)[64], const uint32_t* sr
     return;
   }
   const __amdgpu_buffer_rsrc_t g = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)(4u << 16), 0x00020000);
+  // in the order pass A's first stage consumes them (groups of four pairs
+  // r, r + 32), so its butterflies start while the rest of the plane is
+  // still arriving (loads return in order; each use waits only for its own)
 #pragma unroll
-  for (int r = 0; r < 64; ++r) x[r] = __builtin_amdgcn_raw_buffer_load_b32(g, t * 4u, (uint32_t)r << 12, kPlaneAux);
+  for (int q = 0; q < 64; ++q) {
+    const int r = kPlaneLoadOrder ? (((q >> 3) << 2) | (q & 3)) + ((q & 4) ? 32 : 0) : q;
+    x[r] = __builtin_amdgcn_raw_buffer_load_b32(g, t * 4u, (uint32_t)r << 12, kPlaneAux);
+  }
 }
 
 // The CU this workgroup runs on, as a dense id below kPlaneSlots: XCC_ID
@@ -699,7 +711,7 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
   PLANE_STAMP(K, 11);
   plane_gs<0, 10, 0, 5, kPlaneChA, true>(x, n0, itws, mo, Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p});
   PLANE_STAMP(K, 12);
-  if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) return;
+  if ((RNT_PLANE_EXP & (4 | 32)) != 0 && x[0] != 0xffffffffu) return;
   const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc((void*)c, 0, (int)(4u << 16), 0x00020000);
 #pragma unroll
   for (int r = 0; r < 64; ++r) __builtin_amdgcn_raw_buffer_store_b32(x[r], dst, t * 4u, (uint32_t)r << 12, kPlaneAux);
@@ -708,7 +720,7 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
 
 // a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
 __device__ __forceinline__ void plane_store_hat(const HatBuf& dst, const uint32_t (&x)[64], uint32_t t) {
-  if ((RNT_PLANE_EXP & 4) != 0 && x[0] != 0xffffffffu) return;
+  if ((RNT_PLANE_EXP & (4 | 64)) != 0 && x[0] != 0xffffffffu) return;
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk)
     dst.st(t, kk, x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
@@ -799,8 +811,8 @@ __global__ void __launch_bounds__(plane::T, 1)
 k_plane_fused(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
               TabPtrs<uint32_t> tp, uint64_t ls, uint32_t cu_slots) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  const uint32_t poly = blockIdx.x, l = blockIdx.y;
   const uint64_t N = 1ull << 16;
+  const uint32_t poly = blockIdx.x, l = blockIdx.y;
   // a^ goes to a scratch plane: per (poly, limb), or (cu_slots) per CU, so
   // the launch's scratch footprint is 256 KiB per CU (64 MiB on 256 CUs),
   // rewritten by the CU's next workgroup while it may still sit in the
@@ -821,7 +833,15 @@ k_plane_fused_p(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, 
   uint32_t* ah = scratch + (uint64_t)blockIdx.x * (1ull << 16);
   for (uint32_t p = blockIdx.x; p < planes; p += gridDim.x) {
     const uint32_t l = p / B, poly = p - l * B;
-    plane_fused_one(c, a, b, ah, tp, ls, poly, l, (uint32_t*)smem_raw, threadIdx.x, p);
+    // opaque per-iteration copies of the bases: nothing derived from them is
+    // hoisted out of the loop and held (in spilled registers) across a body
+    uint32_t* c1 = c;
+    const uint32_t *a1 = a, *b1 = b;
+    uint32_t* ah1 = ah;
+    TabPtrs<uint32_t> tp1 = tp;
+    asm volatile("" : "+s"(c1), "+s"(a1), "+s"(b1), "+s"(ah1));
+    asm volatile("" : "+s"(tp1.tw), "+s"(tp1.itw), "+s"(tp1.lc));
+    plane_fused_one(c1, a1, b1, ah1, tp1, ls, poly, l, (uint32_t*)smem_raw, threadIdx.x, p);
   }
 }
 
