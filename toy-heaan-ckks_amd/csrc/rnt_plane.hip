@@ -19,14 +19,16 @@
 namespace rnt {
 
 // ---- whole-plane product (rnt_mul at N = 2^16, u32 canonical bases) ------
-// Two launches per batch instead of three, 5 planes of HBM traffic per
-// (poly, limb) instead of 9 (the 5-plane traffic measured
-// 142k poly-muls/s against 122k for the shipped 9):
-//   k_plane_fwd: a -> a^ (the whole truncated forward transform of one
-//                plane in one workgroup's registers; a^ goes to a private
-//                layout), 2 planes;
-//   k_plane_mul: b -> b^ the same way, a^ (x) b^ (degree-3 block products),
-//                the whole truncated inverse, c, 3 planes.
+// 5 planes of HBM traffic per (poly, limb) instead of the four-step path's
+// 9.  The shipped form is one launch, k_plane_fused: a
+// workgroup transforms a, writes a^ to a scratch plane in a private layout,
+// transforms b, reads a^ back (pipelined 4 blocks ahead), forms the degree-3
+// block products and runs the inverse, storing c.  k_plane_fwd + k_plane_mul
+// split the same work over two launches (RNT_PLANE=1), k_plane_fused_p is the
+// persistent form (RNT_PLANE=4).  The butterflies run as 4-way interleaved
+// inline asm (rnt_bfly4.hpp; the kernel is bound by VALU issue), pass C's
+// twiddles are loaded ahead of X2, and X1 runs in its two rounds with pass B
+// (gs B) of one register half between them.
 // A workgroup = 1024 threads holds one 2^16-word plane, 64 words a thread.
 // Thread t = (w << 6) | lam (wave w, lane lam); the 16-bit index i is split
 // three ways:
