@@ -1050,7 +1050,7 @@ def run_ntt(args, comm, world, rank, local_rank):
     comm.barrier()
     elapsed = comm.max(t1 - t0)
     kernels = {}
-    for k in ("col_fwd", "row_fwd", "row_inv", "col_inv"):
+    for k in ("col_fwd", "row_fwd", "row_inv", "col_inv", "plane_ntt_fwd", "plane_ntt_inv"):
         cnt, ms = B.profile_read(k)
         if cnt:
             kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
@@ -1109,7 +1109,11 @@ def run_ntt(args, comm, world, rank, local_rank):
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic_for(dom, "ntt", batch, args.log_n, L),
                      "alg_bytes_per_launch": alg,
-                     "whole_op_GBs": value / world * 4 * alg / batch / 1e9,
+                     # bytes the device moves per pair: each launch moves the batch once in
+                     # and once out (four launches per pair on the four-step kernels, two
+                     # on the whole-plane ones)
+                     "whole_op_GBs": value / world * (sum(v["launches"] for v in kernels.values())
+                                                      / args.steps) * alg / batch / 1e9,
                      "kernels": kernels},
         "cpu_baseline": cpu,
         "power": power,

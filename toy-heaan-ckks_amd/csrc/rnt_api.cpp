@@ -83,7 +83,7 @@ thread_local Capture* g_capture = nullptr;
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
-    "sfft", "sample", "copy", "plane_fwd", "plane_mul", "plane_fused"};
+    "sfft", "sample", "copy", "plane_fwd", "plane_mul", "plane_fused", "plane_ntt_fwd", "plane_ntt_inv"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -402,6 +402,10 @@ int to_coeff_into(const rnt_buf* src, void* dst) {
     HIP_TRY(hipMemcpyAsync(dst, src->data, poly_words(src) * word_bytes(k.t),
                            hipMemcpyDeviceToDevice, k.s),
             "hipMemcpyAsync");
+  if (rnt::plane_ok(k.t)) {
+    LAUNCH(k.t, rnt::K_PLANE_NTT_INV, rnt::launch_plane_ntt(k, 1, dst, ls), "plane inverse transform");
+    return RNT_OK;
+  }
   LAUNCH(k.t, rnt::K_ROW_INV, rnt::launch_row(k, 1, dst, nullptr, ls), "row inverse");
   LAUNCH(k.t, rnt::K_COL_INV, rnt::launch_col_inv(k, dst, ls, dst, ls, 0, nullptr), "column inverse");
   return RNT_OK;
@@ -1066,8 +1070,14 @@ extern "C" int rnt_ntt_fwd(rnt_buf* b) {
   if (int rc = set_device(b->ctx)) return rc;
   rnt::Launch k = launch_for(b);
   const uint64_t ls = limb_stride(b);
-  LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, b->data, b->data, nullptr, nullptr, ls, ls), "column forward");
-  LAUNCH(k.t, rnt::K_ROW_FWD, rnt::launch_row(k, 0, b->data, nullptr, ls), "row forward");
+  if (rnt::plane_ok(k.t)) {
+    // N = 2^16, u32 bases: the whole-plane transform (rnt_plane.hip)
+    LAUNCH(k.t, rnt::K_PLANE_NTT_FWD, rnt::launch_plane_ntt(k, 0, b->data, ls), "plane forward transform");
+  } else {
+    LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, b->data, b->data, nullptr, nullptr, ls, ls),
+           "column forward");
+    LAUNCH(k.t, rnt::K_ROW_FWD, rnt::launch_row(k, 0, b->data, nullptr, ls), "row forward");
+  }
   b->in_ntt = 1;
   return RNT_OK;
 }

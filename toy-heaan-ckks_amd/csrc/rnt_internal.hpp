@@ -116,7 +116,7 @@ struct Tables {
 enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
-  K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FWD, K_PLANE_MUL, K_PLANE_FUSED, K_COUNT
+  K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FWD, K_PLANE_MUL, K_PLANE_FUSED, K_PLANE_NTT_FWD, K_PLANE_NTT_INV, K_COUNT
 };
 
 struct Prof {
@@ -199,6 +199,8 @@ bool plane_ok(const Tables* t);
 hipError_t launch_plane(const Launch& k, int which, void* out, const void* in, const void* ahat,
                         uint64_t ls);
 hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls);
+// standalone whole-plane transforms in place (N = 2^16, u32; plane_ok)
+hipError_t launch_plane_ntt(const Launch& k, int inverse, void* data, uint64_t ls);
 // Whether rnt_mul's row kernel stops its transforms two stages early and
 // multiplies degree-3 residues (u32 canonical bases, row length 2^(4k));
 // its inverse column pass then takes rfold = 2.

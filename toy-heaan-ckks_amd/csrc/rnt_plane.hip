@@ -83,6 +83,11 @@ constexpr int kPlaneAux = RNT_PLANE_AUX;
 #define RNT_PLANE_LOAD_ORDER 1
 #endif
 constexpr bool kPlaneLoadOrder = RNT_PLANE_LOAD_ORDER != 0;
+// b's loads issued ahead of a^'s stores (0: none)
+#ifndef RNT_PLANE_BEARLY
+#define RNT_PLANE_BEARLY 0
+#endif
+constexpr int kPlaneBEarly = RNT_PLANE_BEARLY;
 // Twiddles per scalar-load chunk in pass A (64 SGPRs at 32)
 #ifndef RNT_PLANE_CHA
 #define RNT_PLANE_CHA 32
@@ -156,8 +161,9 @@ __device__ __forceinline__ Tw<uint32_t> tw_fetch(const TS& ts, uint32_t nb, uint
 }
 template <int SL, int MASK>
 __device__ __forceinline__ Tw<uint32_t> tw_fetch(const TwPre<MASK>& p, uint32_t nb, uint32_t m) {
-  static_assert(SL >= 2 && SL <= 5, "pass C stages");
-  if constexpr (!(MASK & (1 << (SL - 2)))) return tw_get<uint32_t>(p.b, nb, m);
+  static_assert(SL >= 0 && SL <= 5, "pass C stages");
+  if constexpr (SL < 2) return tw_get<uint32_t>(p.b, nb, m);  // the full transform's last two stages
+  else if constexpr (!(MASK & (1 << (SL - 2)))) return tw_get<uint32_t>(p.b, nb, m);
   else if constexpr (SL == 5) return p.s5[0];
   else if constexpr (SL == 4) return p.s4[m];
   else if constexpr (SL == 3) return p.s3[m];
@@ -519,6 +525,11 @@ __device__ uint64_t g_plane_trace[2 * kTraceWg * 16 * kTraceStamps];
 #endif
 constexpr int kPlaneChB = RNT_PLANE_CHB;
 
+// Register of the q-th plane load.
+__host__ __device__ constexpr int plane_load_reg(int q) {
+  return kPlaneLoadOrder ? (((q >> 3) << 2) | (q & 3)) + ((q & 4) ? 32 : 0) : q;
+}
+
 // Load the L0 plane at src (64 coalesced dword loads a thread).
 __device__ __forceinline__ void plane_load(uint32_t (&x)[64], const uint32_t* src, uint32_t t) {
   if constexpr ((RNT_PLANE_EXP & 2) != 0) {
@@ -532,7 +543,7 @@ __device__ __forceinline__ void plane_load(uint32_t (&x)[64], const uint32_t* sr
   // still arriving (loads return in order; each use waits only for its own)
 #pragma unroll
   for (int q = 0; q < 64; ++q) {
-    const int r = kPlaneLoadOrder ? (((q >> 3) << 2) | (q & 3)) + ((q & 4) ? 32 : 0) : q;
+    const int r = plane_load_reg(q);
     x[r] = __builtin_amdgcn_raw_buffer_load_b32(g, t * 4u, (uint32_t)r << 12, kPlaneAux);
   }
 }
@@ -579,7 +590,7 @@ struct NoHook {
 };
 // AFTER_X1 / AFTER_X2 run right after the exchanges (prefetches of the next
 // operand: issued there, they are in flight during the passes that follow).
-template <int K, bool SYNC1, class H1 = NoHook, class H2 = NoHook>
+template <int K, bool SYNC1, class H1 = NoHook, class H2 = NoHook, bool FULL = false>
 __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint32_t t,
                                           const Tw<uint32_t>* tw, const Mod<uint32_t>& mo, uint32_t trace_id,
                                           const H1& after_x1 = H1{}, const H2& after_x2 = H2{}) {
@@ -618,11 +629,63 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   plane_x2<true>(x, lds, t);
   PLANE_STAMP(K, 5);
   after_x2();
+  // pass C: bits 5..2 for the product (bits 1..0 are its truncated
+  // stages), bits 5..0 for a standalone transform (FULL)
+  constexpr int SLLO_C = FULL ? 0 : 2;
   if constexpr ((RNT_PLANE_EXP & 1) != 0)
-    plane_ct<2, 0, 5, 2, 8>(x, N, tws, mo);
+    plane_ct<2, 0, 5, SLLO_C, 8>(x, N, tws, mo);
   else
-    plane_ct<2, 0, 5, 2, 8>(x, N + (t << 6), pc, mo);
+    plane_ct<2, 0, 5, SLLO_C, 8>(x, N + (t << 6), pc, mo);
   PLANE_STAMP(K, 6);
+}
+
+// The inverse transform from pass C's layout (L2) to the store of c in L0:
+// gs C on bits SLLO_C..5 (2 after a truncated product, 0 for a standalone
+// transform), X2, gs B, X1 (split as the forward one), gs A with the folded
+// last-stage constants F (4/N with the Montgomery factor after a product,
+// 1/N for a standalone transform).
+template <int K, int SLLO_C, class TSC>
+__device__ __forceinline__ void plane_inv_tail(uint32_t (&x)[64], uint32_t* lds, uint32_t t, uint32_t* c,
+                                               const Tw<uint32_t>* itw, const TSC& gsrc, const Mod<uint32_t>& mo,
+                                               const Fold<uint32_t>& F, uint32_t trace_id) {
+  (void)trace_id;
+  const uint32_t n0 = 1u << 16;
+  const TwScalar<uint32_t> itws{(const RNT_CONST_AS Tw<uint32_t>*)itw};
+  if constexpr ((RNT_PLANE_EXP & 1) != 0)
+    plane_gs<2, 0, SLLO_C, 5, 8, false>(x, n0, itws, mo, Fold<uint32_t>{});
+  else
+    plane_gs<2, 0, SLLO_C, 5, 8, false>(x, n0 + (t << 6), gsrc, mo, Fold<uint32_t>{});
+  PLANE_STAMP(K, 8);
+  plane_x2<false>(x, lds, t);
+  PLANE_STAMP(K, 9);
+  const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
+  if constexpr (kPlaneX1Split) {
+    // gs B of round 0's half, X1 round 0 written while gs B of the other half runs
+    plane_gs<1, 6, 0, 3, kPlaneChB, false, 0>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+    plane_sync();  // other waves may still be in their X2
+    plane_x1_round<false, 0, true>(x, lds, t);
+    plane_gs<1, 6, 0, 3, kPlaneChB, false, 1>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+    PLANE_STAMP(K, 10);
+    plane_sync();
+    plane_x1_round<false, 0, false>(x, lds, t);
+    plane_sync();
+    plane_x1_round<false, 1, true>(x, lds, t);
+    plane_sync();
+    plane_x1_round<false, 1, false>(x, lds, t);
+    plane_sync();
+  } else {
+    plane_gs<1, 6, 0, 3, kPlaneChB, false>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+    PLANE_STAMP(K, 10);
+    plane_x1<false, true>(x, lds, t);  // other waves may still be in their X2
+  }
+  PLANE_STAMP(K, 11);
+  plane_gs<0, 10, 0, 5, kPlaneChA, true>(x, n0, itws, mo, F);
+  PLANE_STAMP(K, 12);
+  if ((RNT_PLANE_EXP & (4 | 32)) != 0 && x[0] != 0xffffffffu) return;
+  const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc((void*)c, 0, (int)(4u << 16), 0x00020000);
+#pragma unroll
+  for (int r = 0; r < 64; ++r) __builtin_amdgcn_raw_buffer_store_b32(x[r], dst, t * 4u, (uint32_t)r << 12, kPlaneAux);
+  PLANE_STAMP(K, 13);
 }
 
 // The rest of the product once b^ is in x (L2): the degree-3 block
@@ -682,42 +745,7 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
     for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = cc[e];
   }
   PLANE_STAMP(K, 7);
-  const TwScalar<uint32_t> itws{(const RNT_CONST_AS Tw<uint32_t>*)itw};
-  if constexpr ((RNT_PLANE_EXP & 1) != 0)
-    plane_gs<2, 0, 2, 5, 8, false>(x, n0, itws, mo, Fold<uint32_t>{});
-  else
-    plane_gs<2, 0, 2, 5, 8, false>(x, n0 + (t << 6), gpre, mo, Fold<uint32_t>{});
-  PLANE_STAMP(K, 8);
-  plane_x2<false>(x, lds, t);
-  PLANE_STAMP(K, 9);
-  const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
-  if constexpr (kPlaneX1Split) {
-    // gs B of round 0's half, X1 round 0 written while gs B of the other half runs
-    plane_gs<1, 6, 0, 3, kPlaneChB, false, 0>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
-    plane_sync();  // other waves may still be in their X2
-    plane_x1_round<false, 0, true>(x, lds, t);
-    plane_gs<1, 6, 0, 3, kPlaneChB, false, 1>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
-    PLANE_STAMP(K, 10);
-    plane_sync();
-    plane_x1_round<false, 0, false>(x, lds, t);
-    plane_sync();
-    plane_x1_round<false, 1, true>(x, lds, t);
-    plane_sync();
-    plane_x1_round<false, 1, false>(x, lds, t);
-    plane_sync();
-  } else {
-    plane_gs<1, 6, 0, 3, kPlaneChB, false>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
-    PLANE_STAMP(K, 10);
-    plane_x1<false, true>(x, lds, t);  // other waves may still be in their X2
-  }
-  PLANE_STAMP(K, 11);
-  plane_gs<0, 10, 0, 5, kPlaneChA, true>(x, n0, itws, mo, Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p});
-  PLANE_STAMP(K, 12);
-  if ((RNT_PLANE_EXP & (4 | 32)) != 0 && x[0] != 0xffffffffu) return;
-  const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc((void*)c, 0, (int)(4u << 16), 0x00020000);
-#pragma unroll
-  for (int r = 0; r < 64; ++r) __builtin_amdgcn_raw_buffer_store_b32(x[r], dst, t * 4u, (uint32_t)r << 12, kPlaneAux);
-  PLANE_STAMP(K, 13);
+  plane_inv_tail<K, 2>(x, lds, t, c, itw, gpre, mo, Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p}, trace_id);
 }
 
 // a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
@@ -792,10 +820,34 @@ __device__ __forceinline__ void plane_fused_one(uint32_t* __restrict__ c, const 
   plane_load(x, a + off, t);
   PLANE_STAMP(0, 1);
   plane_fwd<0, false>(x, lds, t, tw, mo, trace_id);
-  plane_store_hat(HatBuf(ah), x, t);
-  PLANE_STAMP(0, 7);
-  PLANE_STAMP(1, 0);
-  plane_load(x, b + off, t);
+  if constexpr (kPlaneBEarly > 0) {
+    // b's first KB loads (in plane_load's order) go out before a^'s stores,
+    // so waiting for them does not wait for the stores (one in-order vmcnt
+    // counter): pass A of b starts on them while the stores drain
+    constexpr int KB = kPlaneBEarly;
+    const uint32_t* bp = b + off;
+    asm volatile("" : "+s"(bp));
+    const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc((void*)bp, 0, (int)(4u << 16), 0x00020000);
+    uint32_t y[KB > 0 ? KB : 1];
+#pragma unroll
+    for (int q = 0; q < KB; ++q) {
+      const int r = plane_load_reg(q);
+      y[q] = __builtin_amdgcn_raw_buffer_load_b32(gb, t * 4u, (uint32_t)r << 12, kPlaneAux);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    plane_store_hat(HatBuf(ah), x, t);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 64; ++q) {
+      const int r = plane_load_reg(q);
+      x[r] = q < KB ? y[q < KB ? q : 0] : __builtin_amdgcn_raw_buffer_load_b32(gb, t * 4u, (uint32_t)r << 12, kPlaneAux);
+    }
+  } else {
+    plane_store_hat(HatBuf(ah), x, t);
+    PLANE_STAMP(0, 7);
+    PLANE_STAMP(1, 0);
+    plane_load(x, b + off, t);
+  }
   PLANE_STAMP(1, 1);
   plane_fwd<1, true>(x, lds, t, tw, mo, trace_id);
   // a^ comes back from this thread's own stores above (the descriptor is
@@ -847,6 +899,56 @@ k_plane_fused_p(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, 
   }
 }
 
+// Standalone transforms at N = 2^16, u32 bases (rnt_ntt_fwd / rnt_ntt_inv,
+// to_ntt_domain / to_coeff_domain, poly.rs:136-166): one workgroup per
+// (poly, limb) plane, in place.  Forward: the L0 load, all 16 stages (pass C
+// runs bits 5..0), and the L2 layout stored as it stands -- thread t holds
+// the 64 consecutive device-order words (t << 6) .. (t << 6) + 63, the same
+// bit-reversed order the four-step kernels write.  Inverse: those words in,
+// gs C from bit 0, then as after a product with the plain 1/N fold.  2
+// planes of HBM traffic per transform against the four-step kernels' 4.
+template <bool INV>
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_ntt(uint32_t* __restrict__ data, TabPtrs<uint32_t> tp, uint64_t ls) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
+  const uint64_t N = 1ull << 16;
+  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
+  const LimbConst<uint32_t> lc = tp.lc[l];
+  const Mod<uint32_t> mo = mod_of(lc);
+  uint32_t x[64];
+  if constexpr (!INV) {
+    plane_load(x, data + off, t);
+    plane_fwd<0, false, NoHook, NoHook, true>(x, lds, t, tp.tw + (uint64_t)l * N, mo, poly + l * gridDim.x);
+    uint32_t* dp = data + off;
+    asm volatile("" : "+s"(dp));
+    const __amdgpu_buffer_rsrc_t g = __builtin_amdgcn_make_buffer_rsrc((void*)dp, 0, (int)(4u << 16), 0x00020000);
+    using V4 = decltype(__builtin_amdgcn_raw_buffer_load_b128(g, 0, 0, 0));
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      V4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = x[plane::slot2(4 * kk + e)];
+      __builtin_amdgcn_raw_buffer_store_b128(v, g, t * 256u, (uint32_t)kk * 16u, kPlaneAux);
+    }
+  } else {
+    const __amdgpu_buffer_rsrc_t g =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(data + off), 0, (int)(4u << 16), 0x00020000);
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(g, t * 256u, (uint32_t)kk * 16u, kPlaneAux);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = v[e];
+    }
+    const Tw<uint32_t>* itw = tp.itw + (uint64_t)l * N;
+    TwPre<0> gsrc;
+    gsrc.b = itw;
+    plane_inv_tail<1, 0>(x, lds, t, data + off, itw, gsrc, mo, Fold<uint32_t>{lc.c1, lc.c1_p, lc.c2, lc.c2_p},
+                         poly + l * gridDim.x);
+  }
+}
+
 #ifdef RNT_PLANE_TRACE
 extern "C" __attribute__((visibility("default"))) int rnt_debug_plane_trace(uint64_t* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_plane_trace), sizeof(g_plane_trace));
@@ -890,6 +992,23 @@ hipError_t launch_plane(const Launch& k, int which, void* out, const void* in, c
 // (the workspace, one plane per (poly, limb), then holds every slot).
 bool plane_fused_slots(const Launch& k) {
   return RNT_PLANE_SLOTS && (uint64_t)k.B * k.L >= kPlaneSlots;
+}
+
+hipError_t launch_plane_ntt(const Launch& k, int inverse, void* data, uint64_t ls) {
+  if (k.B == 0 || k.L == 0) return hipSuccess;
+  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  const size_t lds = (size_t)plane::LDS_WORDS * 4;
+  const dim3 grid((unsigned)k.B, (unsigned)k.L);
+  if (inverse) {
+    hipError_t e = allow_lds(k_plane_ntt<true>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_plane_ntt<true>, grid, dim3(plane::T), lds, k.s, (uint32_t*)data, tab_ptrs<uint32_t>(k.t), ls);
+  } else {
+    hipError_t e = allow_lds(k_plane_ntt<false>, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_plane_ntt<false>, grid, dim3(plane::T), lds, k.s, (uint32_t*)data, tab_ptrs<uint32_t>(k.t), ls);
+  }
+  return hipGetLastError();
 }
 
 static int plane_cu_count() {
