@@ -253,6 +253,29 @@ __device__ __forceinline__ void plane_gs_groups(uint32_t (&x)[64], const Tw<uint
   }
 }
 
+// One chunk of a stage's twiddles.  In pass C (per-lane twiddles, LY = 2)
+// the next chunk of a stage is loaded before the current chunk's
+// butterflies run, so only a stage's first chunk waits for memory.
+template <int n>
+struct TwChunk {
+  Tw<uint32_t> t[n];
+};
+template <int SLB, int M0, int n, class TS>
+__device__ __forceinline__ TwChunk<n> plane_chunk(const TS& tw, uint32_t nb) {
+  TwChunk<n> c;
+#pragma unroll
+  for (int j = 0; j < n; ++j)
+    c.t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<SLB>(tw, nb, (uint32_t)(M0 + j));
+  return c;
+}
+#ifndef RNT_PLANE_TPIPE
+#define RNT_PLANE_TPIPE 1
+#endif
+template <int LY, int SL, int M0, int CH>
+constexpr bool chunk_pipe() {
+  return RNT_PLANE_TPIPE != 0 && LY == 2 && M0 + CH < (32 >> SL);
+}
+
 // CT stages on logical register bits SLHI .. SLLO of layout LY (index bits
 // [BB, BB + 6)); node0 = 2^16 + the thread's index with register bits 0.
 // Twiddles in chunks of CH per stage (bounded registers beside the plane).
@@ -261,23 +284,36 @@ __device__ __forceinline__ void plane_gs_groups(uint32_t (&x)[64], const Tw<uint
 // chunks are template recursions, so every register index is a
 // compile-time constant (a loop the unroller gave up on would put the
 // plane in scratch memory).
-template <int LY, int BB, int SL, int SLLO, int M0, int CH, int HM = -1, class TS>
+template <int LY, int BB, int SL, int SLLO, int M0, int CH, int HM = -1, class TS, int NP = 1>
 __device__ __forceinline__ void plane_ct_chunks(uint32_t (&x)[64], uint32_t nb, const TS& tw,
-                                                const Mod<uint32_t>& mo) {
+                                                const Mod<uint32_t>& mo, const TwChunk<NP>* pre = nullptr) {
   constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
   Tw<uint32_t> t[n];
+  if constexpr (NP == n && M0 > 0) {
 #pragma unroll
-  for (int j = 0; j < n; ++j)
-    t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<BB + SL>(tw, nb, (uint32_t)(M0 + j));
+    for (int j = 0; j < n; ++j) t[j] = pre->t[j];  // loaded during the previous chunk
+  } else {
+#pragma unroll
+    for (int j = 0; j < n; ++j)
+      t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<BB + SL>(tw, nb, (uint32_t)(M0 + j));
+  }
   if constexpr (RNT_PLANE_ASM != 0) {
     constexpr bool SW = tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0;
+    constexpr int n2 = (cnt - M0 - CH) < CH ? (cnt - M0 - CH) : CH;
+    TwChunk<(n2 > 0 ? n2 : 1)> nxt;
+    if constexpr (chunk_pipe<LY, SL, M0, CH>()) nxt = plane_chunk<BB + SL, M0 + CH, (n2 > 0 ? n2 : 1)>(tw, nb);
     if constexpr (SL > SLLO) {
       plane_ct_groups<LY, SL, M0, d / 2, false, SW, HM>(x, t, mo);
       plane_ct_groups<LY, SL, M0, d / 2, true, SW, HM>(x, t, mo);
     } else {
       plane_ct_groups<LY, SL, M0, d, false, SW, HM>(x, t, mo);
     }
-    if constexpr (M0 + CH < cnt) plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH, HM>(x, nb, tw, mo);
+    if constexpr (M0 + CH < cnt) {
+      if constexpr (chunk_pipe<LY, SL, M0, CH>())
+        plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH, HM, TS, (n2 > 0 ? n2 : 1)>(x, nb, tw, mo, &nxt);
+      else
+        plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH, HM>(x, nb, tw, mo);
+    }
     return;
   }
 #pragma unroll
@@ -303,17 +339,30 @@ __device__ __forceinline__ void plane_ct(uint32_t (&x)[64], uint32_t node0, cons
 // GS stages on logical register bits SLLO .. SLHI; FOLD: the stage at
 // index bit 15 applies the folded constants (4/N with the Montgomery
 // factor, LimbConst c1t/c2t) instead of its twiddle.
-template <int LY, int BB, int SL, int M0, int CH, int HM = -1, class TS>
+template <int LY, int BB, int SL, int M0, int CH, int HM = -1, class TS, int NP = 1>
 __device__ __forceinline__ void plane_gs_chunks(uint32_t (&x)[64], uint32_t nb, const TS& itw,
-                                                const Mod<uint32_t>& mo) {
+                                                const Mod<uint32_t>& mo, const TwChunk<NP>* pre = nullptr) {
   constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
   Tw<uint32_t> t[n];
+  if constexpr (NP == n && M0 > 0) {
 #pragma unroll
-  for (int j = 0; j < n; ++j)
-    t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<BB + SL>(itw, nb, (uint32_t)(M0 + j));
+    for (int j = 0; j < n; ++j) t[j] = pre->t[j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < n; ++j)
+      t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<BB + SL>(itw, nb, (uint32_t)(M0 + j));
+  }
   if constexpr (RNT_PLANE_ASM != 0) {
+    constexpr int n2 = (cnt - M0 - CH) < CH ? (cnt - M0 - CH) : CH;
+    TwChunk<(n2 > 0 ? n2 : 1)> nxt;
+    if constexpr (chunk_pipe<LY, SL, M0, CH>()) nxt = plane_chunk<BB + SL, M0 + CH, (n2 > 0 ? n2 : 1)>(itw, nb);
     plane_gs_groups<LY, SL, M0, tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0, HM>(x, t, mo);
-    if constexpr (M0 + CH < cnt) plane_gs_chunks<LY, BB, SL, M0 + CH, CH, HM>(x, nb, itw, mo);
+    if constexpr (M0 + CH < cnt) {
+      if constexpr (chunk_pipe<LY, SL, M0, CH>())
+        plane_gs_chunks<LY, BB, SL, M0 + CH, CH, HM, TS, (n2 > 0 ? n2 : 1)>(x, nb, itw, mo, &nxt);
+      else
+        plane_gs_chunks<LY, BB, SL, M0 + CH, CH, HM>(x, nb, itw, mo);
+    }
     return;
   }
 #pragma unroll
