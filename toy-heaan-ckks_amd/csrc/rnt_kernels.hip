@@ -793,6 +793,40 @@ __host__ __device__ constexpr int ks_kpad_words(int c) {
 // reads of 16 lanes at 64-byte strides (a row's E = 16 consecutive words per
 // thread) start on 16 distinct 4-bank groups, and 16-byte alignment holds.
 __device__ __forceinline__ uint32_t ks_pad(uint32_t w) { return w + ((w >> 6) << 2); }
+#ifndef RNT_KS_SPRE
+#define RNT_KS_SPRE 0
+#endif
+// LDS plan of k_ks_rows<W, LOG_C, NP>, shared by the kernel and its launcher.
+//  * KEYGLDS: u32 rows of >= 64 words take the key rows global -> LDS
+//    directly (global_load_lds);
+//  * KDOUBLE: two key buffers (the next limb's keys are written while the
+//    last ones may still be read) when they fit beside the exchange region in
+//    a quarter of the LDS, else one buffer and a barrier per limb;
+//  * SPRE: the next source limb's S rows also go global -> LDS, one limb
+//    ahead, into a buffer of RPW rows (row stride C + T words, so the T
+//    lanes of each of a wave's rows read distinct banks), when a wave's
+//    lanes own whole rows (T <= 64), the keys are double-buffered and it all
+//    still fits in a quarter of the LDS (4 workgroups per CU).  Off by
+//    default: it applies to the 2^16 ct-mul grid (NP = 16) and measured
+//    slower there, ks_rows 2.40 against 2.31 ms per 64-ct chunk
+//    (profiles/r03/ab_ks_spre.txt), as register prefetch of the next limb
+//    did before it -- the rows kernel does not wait on the S loads.
+template <class W, int LOG_C, int NP>
+struct KsCfg {
+  using G = RowGeo<LOG_C>;
+  static constexpr int KROWS = G::RPW / NP;
+  static constexpr int KPAD = ks_kpad_words<W>(G::C);
+  static constexpr bool KEYGLDS = sizeof(W) == 4 && G::C >= 64 && (NP > 1 || LOG_C >= kKsGldsWideMinLogC);
+  static constexpr bool KDOUBLE =
+      (size_t)(G::REGION + 4 * KROWS * KPAD) * sizeof(W) <= 40u * 1024u || KROWS == 1;
+  static constexpr int SSTRIDE = G::C + G::S::T;
+  static constexpr int SWORDS = G::RPW * SSTRIDE;
+  static constexpr int KWORDS = (KDOUBLE ? 4 : 2) * KROWS * KPAD;
+  static constexpr bool SPRE = RNT_KS_SPRE != 0 && KEYGLDS && KDOUBLE && G::S::T <= 64 &&
+                               (size_t)(G::REGION + KWORDS + SWORDS) * sizeof(W) <= 40u * 1024u;
+  static constexpr size_t LDS_BYTES = (size_t)(G::REGION + KWORDS + (SPRE ? SWORDS : 0)) * sizeof(W);
+};
+
 // 16 bytes of LDS into registers (p is 16-byte aligned by construction:
 // key rows start on ks_kpad_words boundaries, and ks_pad keeps every
 // thread's run of E words within a row on a 16-byte boundary).
@@ -849,24 +883,24 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   // padded key row (ks_pad), rounded up to 16 bytes so every key row --
   // hence every thread's 16-byte LDS read -- starts 16-byte aligned also for
   // short rows (C = 16/32, where C + C/16 alone is 17 or 34 words)
-  constexpr int KPAD = ks_kpad_words<W>(C);
+  using K = KsCfg<W, LOG_C, NP>;
+  constexpr int KPAD = K::KPAD;
   // NP polys x KROWS consecutive rows per workgroup (NP = RPW: one row r
   // for RPW polys; NP = 1: one poly, RPW rows); the key rows of a source
   // limb are staged per workgroup, KROWS of each key
   static_assert(NP >= 1 && G::RPW % NP == 0, "polys per workgroup");
-  constexpr int KROWS = G::RPW / NP;
+  constexpr int KROWS = K::KROWS;
   constexpr bool WIDE = NP < G::RPW;
   constexpr int KPT = (2 * KROWS * C + G::THREADS - 1) / G::THREADS;  // key words per thread per i
-  constexpr bool kKeyGlds = sizeof(W) == 4 && C >= 64 && (NP > 1 || LOG_C >= kKsGldsWideMinLogC);
-  // two key buffers (the next limb's keys are written while the last ones
-  // may still be read) when they fit beside the exchange region in a
-  // quarter of the LDS; else one buffer and a barrier per limb
-  constexpr bool KDOUBLE =
-      (size_t)(G::REGION + 4 * KROWS * KPAD) * sizeof(W) <= 40u * 1024u || KROWS == 1;
+  constexpr bool kKeyGlds = K::KEYGLDS;
+  constexpr bool KDOUBLE = K::KDOUBLE;
+  constexpr bool SPRE = K::SPRE;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
   // [buffers][key_b rows | key_a rows]
   W* kbuf = lds + G::REGION;
+  // [RPW rows of SSTRIDE]: the S rows of the next source limb (SPRE)
+  W* sbuf = kbuf + K::KWORDS;
   // XCD-aware deal: hardware block b runs on XCD b % 8; consecutive logical
   // blocks (one (j, r), successive poly groups) get the same b % 8
   const uint32_t per_xcd = (nblocks + 7) / 8;
@@ -918,19 +952,83 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     acc[0][e] = init0 ? init0[ibase + pos] : (W)0;
     acc[1][e] = init1 ? init1[ibase + pos] : (W)0;
   }
+  constexpr uint32_t KW = (uint32_t)(KROWS * C);  // words per key
+  // SPRE: key rows and S rows of source limb i go global -> LDS (no
+  // registers) during limb i - 1's transform and accumulate.  A wave's lanes
+  // own whole rows (T <= 64), so a wave loads exactly the S rows it reads
+  // back; the key rows are shared, published by a barrier.
+  [[maybe_unused]] const uint32_t wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  [[maybe_unused]] const uint32_t lane_u = threadIdx.x & 63u;
+  auto ks_issue = [&](uint32_t i, W* kb) {
+    if constexpr (SPRE) {
+    constexpr uint32_t SEG = KW / 64;  // segments per key
+    constexpr int WAVES = G::THREADS / 64;
+    const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + (WIDE ? (uint64_t)rbase * G::C : rowoff);
+#pragma unroll
+    for (int m = 0; m < (int)((2 * SEG + WAVES - 1) / WAVES); ++m) {
+      const uint32_t sg = wave_u + (uint32_t)m * WAVES;
+      if (sg < 2 * SEG) {
+        const uint32_t kk = sg >= SEG, rs = kk ? sg - SEG : sg;
+        const W* src = (kk ? key_a : key_b) + kbase + rs * 64u + lane_u;
+        W* dst = kb + kk * (KROWS * KPAD) + (rs / (C / 64)) * KPAD + ks_pad((rs % (C / 64)) * 64u);
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
+      }
+    }
+    if constexpr (SPRE) {
+      // the wave's rows: slots wave * 64 / T .. + 64 / T, C / 64 segments each
+      constexpr int SPW = 64 / G::S::T, SSEG = C / 64;
+#pragma unroll
+      for (int m = 0; m < SPW * SSEG; ++m) {
+        const uint32_t slot = wave_u * SPW + (uint32_t)(m / SSEG), sg = (uint32_t)(m % SSEG);
+        uint32_t p, r;
+        if constexpr (WIDE) {
+          r = rbase + slot / NP;
+          p = pg * NP + slot % NP;
+        } else {
+          r = rbase;
+          p = pg * G::RPW + slot;
+        }
+        p = p < B ? p : B - 1;
+        const W* src = S + (((uint64_t)j * L + i) * B + p) * N + (uint64_t)r * G::C + sg * 64u + lane_u;
+        W* dst = sbuf + slot * K::SSTRIDE + sg * 64u;
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
+      }
+    }
+    }
+  };
+  if constexpr (SPRE) ks_issue(0u, kbuf);
 #pragma unroll 1
   for (uint32_t i = 0; i < L; ++i) {
     // this limb's key rows (key poly i, limb j, rows rbase ..; limb stride
     // key_ls) and S rows: one batch of loads, one wait
     const uint64_t sbase = (((uint64_t)j * L + i) * B + rp.p) * N + rowoff;
     const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + (WIDE ? (uint64_t)rbase * G::C : rowoff);
-    constexpr uint32_t KW = (uint32_t)(KROWS * C);  // words per key
     W x[1][E];
+    if constexpr (SPRE) {
+      // limb i's rows have landed (this wave's loads), and every wave's
+      // (the barrier, which also orders every wave's reads of the key buffer
+      // limb i + 1 overwrites, two limbs ago, before the loads into it)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const W* sr = sbuf + rp.xp.slot * K::SSTRIDE + b0;
+#pragma unroll
+      for (int e = 0; e < E; ++e) x[0][e] = sr[(uint32_t)e << G::BB0];
+      // the reads complete before the next limb's rows overwrite them
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (i + 1 < L) ks_issue(i + 1, kbuf + ((i + 1) & 1u) * 2 * KROWS * KPAD);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     // one key buffer: every thread's reads of the previous limb's keys
     // finish before it is rewritten
     if constexpr (!KDOUBLE) __syncthreads();
     W* kb = KDOUBLE ? kbuf + (i & 1u) * 2 * KROWS * KPAD : kbuf;
-    if constexpr (kKeyGlds) {
+    if constexpr (SPRE) {
+      (void)sbase;
+      (void)kbase;
+    } else if constexpr (kKeyGlds) {
       // u32 rows of >= 64 words: the key rows go global -> LDS directly, one
       // 64-word segment (one ks_pad run) per wave instruction, no registers
       constexpr uint32_t SEG = KW / 64;  // segments per key
@@ -1699,9 +1797,8 @@ static hipError_t ks_rows_launch(const Launch& k, void* u0, void* u1, uint64_t l
   const unsigned launched = (unsigned)((blocks + 7) / 8 * 8);  // whole XCD rounds
   // exchange region + one or two buffers of {key_b, key_a} x KROWS rows
   // (the kernel's KDOUBLE rule)
-  const size_t region = row_lds<W, LOG_C>(1);
-  const bool kdouble = region + 4 * KROWS * KPADB <= 40u * 1024u || KROWS == 1;
-  const size_t lds = region + (kdouble ? 4 : 2) * KROWS * KPADB;
+  const size_t lds = KsCfg<W, LOG_C, NP>::LDS_BYTES;
+  static_assert(KsCfg<W, LOG_C, NP>::KPAD * sizeof(W) == KPADB, "key row pad");
   hipError_t e = allow_lds(k_ks_rows<W, LOG_C, NP>, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((k_ks_rows<W, LOG_C, NP>), dim3(launched), dim3(G::THREADS), lds, k.s,
