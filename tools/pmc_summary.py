@@ -27,6 +27,9 @@ PLANE = {"k_plane_fwd": "plane_fwd", "k_plane_mul": "plane_mul", "k_plane_fused"
 
 
 def short(kname):
+    m = re.search(r"\bk_plane_ntt<(true|false)>", kname)
+    if m:
+        return "plane_ntt_inv" if m.group(1) == "true" else "plane_ntt_fwd"
     m = re.search(r"\b(k_plane_\w+)\(", kname)
     if m:
         return PLANE.get(m.group(1))
