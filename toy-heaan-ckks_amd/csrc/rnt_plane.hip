@@ -573,6 +573,11 @@ __device__ uint64_t g_plane_trace[2 * kTraceWg * 16 * kTraceStamps];
 #define RNT_PLANE_CHB 16
 #endif
 constexpr int kPlaneChB = RNT_PLANE_CHB;
+// twiddles per chunk in pass C (per-lane twiddles)
+#ifndef RNT_PLANE_CHC
+#define RNT_PLANE_CHC 8
+#endif
+constexpr int kPlaneChC = RNT_PLANE_CHC;
 
 // Register of the q-th plane load.
 __host__ __device__ constexpr int plane_load_reg(int q) {
@@ -682,9 +687,9 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   // stages), bits 5..0 for a standalone transform (FULL)
   constexpr int SLLO_C = FULL ? 0 : 2;
   if constexpr ((RNT_PLANE_EXP & 1) != 0)
-    plane_ct<2, 0, 5, SLLO_C, 8>(x, N, tws, mo);
+    plane_ct<2, 0, 5, SLLO_C, kPlaneChC>(x, N, tws, mo);
   else
-    plane_ct<2, 0, 5, SLLO_C, 8>(x, N + (t << 6), pc, mo);
+    plane_ct<2, 0, 5, SLLO_C, kPlaneChC>(x, N + (t << 6), pc, mo);
   PLANE_STAMP(K, 6);
 }
 
@@ -701,9 +706,9 @@ __device__ __forceinline__ void plane_inv_tail(uint32_t (&x)[64], uint32_t* lds,
   const uint32_t n0 = 1u << 16;
   const TwScalar<uint32_t> itws{(const RNT_CONST_AS Tw<uint32_t>*)itw};
   if constexpr ((RNT_PLANE_EXP & 1) != 0)
-    plane_gs<2, 0, SLLO_C, 5, 8, false>(x, n0, itws, mo, Fold<uint32_t>{});
+    plane_gs<2, 0, SLLO_C, 5, kPlaneChC, false>(x, n0, itws, mo, Fold<uint32_t>{});
   else
-    plane_gs<2, 0, SLLO_C, 5, 8, false>(x, n0 + (t << 6), gsrc, mo, Fold<uint32_t>{});
+    plane_gs<2, 0, SLLO_C, 5, kPlaneChC, false>(x, n0 + (t << 6), gsrc, mo, Fold<uint32_t>{});
   PLANE_STAMP(K, 8);
   plane_x2<false>(x, lds, t);
   PLANE_STAMP(K, 9);
