@@ -147,12 +147,19 @@ int rnt_sync(const rnt_ctx* ctx);
  * (no upload, download, rnt_sync or allocation that misses the block cache)
  * and run the sequence once un-recorded first, so its workspaces are cached;
  * the graph keeps the workspace blocks its ops took until
- * rnt_graph_destroy.  Buffers the graph reads and writes must outlive it. */
+ * rnt_graph_destroy (recorded ops share one call-scoped workspace, so N
+ * recorded key-switches keep one block, not N).  Buffers the graph reads
+ * and writes must outlive it, and so must their private scratch: while a
+ * graph is alive, do not run an op on a larger batch into one of its output
+ * buffers (an op that grows a buffer's scratch releases the old block, which
+ * the graph's replays still write).  rnt_graph_workspace reports the blocks
+ * and bytes the graph holds. */
 typedef struct rnt_graph rnt_graph;
 int rnt_capture_begin(const rnt_ctx* ctx);
 int rnt_capture_end(const rnt_ctx* ctx, rnt_graph** out);
 int rnt_graph_launch(rnt_graph* graph);
 int rnt_graph_destroy(rnt_graph* graph);
+int rnt_graph_workspace(const rnt_graph* graph, size_t* blocks, size_t* bytes);
 
 /* ---- buffers == batches of RnsPoly ------------------------------------ */
 /* Allocates device storage for n_polys polynomials over ctx's basis, all

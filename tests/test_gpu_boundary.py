@@ -288,3 +288,53 @@ def test_graph_capture_replays_the_engine_call_shape(gpu):
     seq()
     Bd.sync()
     assert np.array_equal(t0.channels(), v0)
+
+
+def test_graph_records_share_one_keyswitch_workspace(gpu):
+    """N recorded key-switch ops keep one call-scoped workspace block (the
+    recorded ops are ordered on the one captured stream, so the second op
+    reuses the block the first handed back while recording), and the
+    replays of the 4-rotation graph are bit-exact against the oracle.  A
+    capture whose body raises destroys its graph (no leaked workspace)."""
+    rn = gpu
+    n, L = 1 << 12, 4
+    mods = rn.generate_primes(31, L, n)
+    Bd, Bo = rn.RnsBasis(mods, n), orc.Basis(mods, n)
+    rng = np.random.default_rng(78)
+    x0, x1 = _rand(rng, mods, n), _rand(rng, mods, n)
+    ra, rb = _rand(rng, mods, n, L), _rand(rng, mods, n, L)
+    rkey = rn.RnsGadgetKey.from_channels(ra, rb, Bd)
+    c0, c1 = rn.RnsPoly.from_channels(x0, Bd), rn.RnsPoly.from_channels(x1, Bd)
+    lib = rn.load()
+    outs = [(rn.RnsPoly(Bd), rn.RnsPoly(Bd)) for _ in range(4)]
+
+    def rec(m):
+        for t0, t1 in outs[:m]:
+            rn.check(lib.rnt_ct_rotate(t0.handle, t1.handle, c0.handle, c1.handle, 1, rkey.a.handle,
+                                       rkey.b.handle))
+
+    rec(4)  # warm
+    Bd.sync()
+    with Bd.capture() as g1:
+        rec(1)
+    with Bd.capture() as g4:
+        rec(4)
+    b1, by1 = g1.workspace()
+    b4, by4 = g4.workspace()
+    assert b1 >= 1 and (b4, by4) == (b1, by1), ((b1, by1), (b4, by4))
+    g4.replay()
+    Bd.sync()
+    v0, v1 = orc.rotate_ciphertext(Bo, x0, x1, 1, ra, rb)
+    for t0, t1 in outs:
+        assert np.array_equal(t0.channels(), v0) and np.array_equal(t1.channels(), v1)
+    del g1, g4
+    with pytest.raises(ZeroDivisionError):
+        with Bd.capture():
+            rec(1)
+            1 / 0
+    # the context records again after the failed capture
+    with Bd.capture() as g:
+        rec(2)
+    g.replay()
+    Bd.sync()
+    assert np.array_equal(outs[1][0].channels(), v0)

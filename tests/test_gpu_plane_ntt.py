@@ -1,0 +1,128 @@
+"""The default N = 2^16 transform path (k_plane_ntt: rnt_ntt_fwd / rnt_ntt_inv
+and every NTT-domain op that runs through them) against the oracle on random
+operands, at the metric's ring (N = 2^16, L = 16 x 31-bit), in the default
+mode (whole-plane kernels) and with RNT_PLANE=0 (four-step kernels).
+
+Reference: to_ntt_domain / to_coeff_domain (poly.rs:136-166), the
+NTT-domain MulAssign branch (poly.rs:297-306), rescale_into from the NTT
+domain (poly.rs:187-228) and automorphism of NTT-domain input
+(poly.rs:492-569).  Every poly of a batch of B = 4 is compared (the first
+and last of the batch included), so a poly-offset or layout error shared by
+the forward and inverse kernels cannot hide behind a round trip.  The
+cross-path tests feed one path's NTT-domain output to the other path's
+inverse (both contexts use the device's bit-reversed order).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import pyoracle as orc
+
+pytestmark = pytest.mark.gpu
+
+N, L, B = 1 << 16, 16, 4
+
+
+@pytest.fixture(scope="module")
+def ring(gpu):
+    rn = gpu
+    mod = rn.generate_primes(31, L, N)
+    Bo = orc.Basis(mod, N)
+    rng = np.random.default_rng(0x2_0016)
+    a_h = orc.uniform_poly(mod, N, rng, batch=B)
+    b_h = orc.uniform_poly(mod, N, rng, batch=B)
+    # NTT-domain operands drawn directly (random natural-order evaluations)
+    x_h = orc.uniform_poly(mod, N, rng, batch=B)
+    y_h = orc.uniform_poly(mod, N, rng, batch=B)
+    want = {
+        "fwd": [orc.to_ntt(Bo, a_h[i]) for i in range(B)],
+        "inv": [orc.to_coeff(Bo, x_h[i]) for i in range(B)],
+        "nmul": [orc.mul(Bo, x_h[i], y_h[i], ntt=True) for i in range(B)],
+        "rescale": [orc.rescale(Bo, x_h[i], in_ntt=True) for i in range(B)],
+    }
+    return rn, mod, Bo, a_h, b_h, x_h, y_h, want
+
+
+def _basis(rn, mod, monkeypatch, plane):
+    if plane is not None:
+        monkeypatch.setenv("RNT_PLANE", plane)
+    else:
+        monkeypatch.delenv("RNT_PLANE", raising=False)
+    return rn.RnsBasis(mod, N)
+
+
+@pytest.mark.parametrize("plane", [None, "0"])
+def test_forward_random_batch(ring, monkeypatch, plane):
+    rn, mod, Bo, a_h, _, _, _, want = ring
+    Bd = _basis(rn, mod, monkeypatch, plane)
+    t = rn.RnsPoly.from_channels(a_h, Bd)
+    t.to_ntt_domain()
+    assert t.is_ntt_domain()
+    got = t.channels()
+    for i in range(B):
+        assert np.array_equal(got[i], want["fwd"][i]), i
+
+
+@pytest.mark.parametrize("plane", [None, "0"])
+def test_inverse_random_ntt_upload(ring, monkeypatch, plane):
+    rn, mod, Bo, _, _, x_h, _, want = ring
+    Bd = _basis(rn, mod, monkeypatch, plane)
+    t = rn.RnsPoly.from_channels(x_h, Bd, in_ntt_domain=True)
+    # natural-order NTT-domain upload / download is the identity on the host view
+    assert np.array_equal(t.channels(), x_h)
+    t.to_coeff_domain()
+    assert not t.is_ntt_domain()
+    got = t.channels()
+    for i in range(B):
+        assert np.array_equal(got[i], want["inv"][i]), i
+
+
+@pytest.mark.parametrize("plane", [None, "0"])
+def test_ntt_domain_mul_assign(ring, monkeypatch, plane):
+    rn, mod, Bo, _, _, x_h, y_h, want = ring
+    Bd = _basis(rn, mod, monkeypatch, plane)
+    x = rn.RnsPoly.from_channels(x_h, Bd, in_ntt_domain=True)
+    y = rn.RnsPoly.from_channels(y_h, Bd, in_ntt_domain=True)
+    z = x * y
+    assert z.is_ntt_domain()
+    got = z.channels()
+    for i in range(B):
+        assert np.array_equal(got[i], want["nmul"][i]), i
+    x *= y  # in place
+    assert np.array_equal(x.channels(), got)
+
+
+@pytest.mark.parametrize("plane", [None, "0"])
+def test_rescale_and_automorphism_from_ntt(ring, monkeypatch, plane):
+    rn, mod, Bo, _, _, x_h, _, want = ring
+    Bd = _basis(rn, mod, monkeypatch, plane)
+    x = rn.RnsPoly.from_channels(x_h, Bd, in_ntt_domain=True)
+    r = x.rescale().channels()
+    for i in range(B):
+        assert np.array_equal(r[i], want["rescale"][i]), i
+    for g in (5, 2 * N - 1, 6):
+        out = x.automorphism(g)
+        got = out.channels()
+        for i in (0, B - 1):
+            w, f = orc.automorphism(Bo, x_h[i], g, in_ntt=True)
+            assert np.array_equal(got[i], w), (g, i)
+            assert out.is_ntt_domain() == f
+
+
+def test_cross_path_forward_inverse(ring, monkeypatch):
+    """Four-step forward output through the whole-plane inverse and the other
+    way round, and both forwards equal on the device order (downloaded
+    through the same natural-order permutation)."""
+    rn, mod, Bo, a_h, _, _, _, want = ring
+    B0 = _basis(rn, mod, monkeypatch, "0")
+    B3 = _basis(rn, mod, monkeypatch, None)
+    for src, dst in ((B0, B3), (B3, B0)):
+        t = rn.RnsPoly.from_channels(a_h, src)
+        t.to_ntt_domain()
+        nt = t.channels()
+        for i in range(B):
+            assert np.array_equal(nt[i], want["fwd"][i]), i
+        u = rn.RnsPoly.from_channels(nt, dst, in_ntt_domain=True)
+        u.to_coeff_domain()
+        assert np.array_equal(u.channels(), a_h)

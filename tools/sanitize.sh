@@ -16,7 +16,7 @@
 # Usage: tools/sanitize.sh [log]   (default log: profiles/r03_sanitizer_cpu.log)
 set -euo pipefail
 cd "$(dirname "$0")/.."
-LOG=${1:-profiles/r03_sanitizer_cpu.log}
+LOG=${1:-profiles/r04_sanitizer_cpu.log}
 LLVM=/opt/rocm/lib/llvm/bin
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 OUT=build/asan
@@ -29,18 +29,23 @@ done
 CS=toy-heaan-ckks_amd/csrc
 HIPFLAGS="--offload-arch=gfx950 -O1 -g -std=c++17 -fPIC"
 {
-  echo "# tools/sanitize.sh $(date -u +%Y-%m-%dT%H:%M:%SZ)"
+  echo "# tools/sanitize.sh $(date -u +%Y-%m-%dT%H:%M:%SZ) at commit $(git rev-parse --short HEAD)$(git diff --quiet HEAD -- toy-heaan-ckks_amd oracle include || echo ' (+ uncommitted changes)')"
   echo "# oracle: $LLVM/clang $SAN"
   echo "# librnsntt host code: $HIPCC $HIPFLAGS$HOSTSAN"
 } > "$LOG"
 $LLVM/clang -O1 -g -fPIC -std=c11 -Wall -pthread $SAN -shared-libsan -shared oracle/oracle.c -o $OUT/liboracle.so
+# the library's translation units, from the same list build() compiles
+SRCS=$(python -c "import __graft_entry__ as g; print(' '.join(g.SOURCES))")
+echo "# sources: $SRCS" >> "$LOG"
 pids=()
-for src in rnt_kernels.hip rnt_encode.hip rnt_sample.hip rnt_api.cpp; do
+objs=()
+for src in $SRCS; do
   $HIPCC $HIPFLAGS $HOSTSAN -c $CS/$src -o $OUT/${src%.*}.o & pids+=($!)
+  objs+=("$OUT/${src%.*}.o")
 done
 for p in "${pids[@]}"; do wait "$p"; done
 $HIPCC --offload-arch=gfx950 -shared -fPIC -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined \
-  -shared-libsan $OUT/rnt_kernels.o $OUT/rnt_encode.o $OUT/rnt_sample.o $OUT/rnt_api.o -o $OUT/librnsntt.so
+  -shared-libsan "${objs[@]}" -o $OUT/librnsntt.so
 RT=$($LLVM/clang -print-file-name=libclang_rt.asan-x86_64.so)
 echo "# runtime: $RT" >> "$LOG"
 # leaks: python and torch keep allocations alive at exit by design, so leak
@@ -53,7 +58,12 @@ LD_PRELOAD="$RT" ASAN_OPTIONS=detect_leaks=0:abort_on_error=1:halt_on_error=1 \
     -q -m "not gpu" -p no:cacheprovider >> "$LOG" 2>&1
 rc=$?
 set -e
-grep -c "ERROR: AddressSanitizer\|runtime error:" "$LOG" | sed 's/^/# sanitizer reports: /' >> "$LOG" || true
-echo "# exit status $rc" >> "$LOG"
+reports=$(grep -c "ERROR: AddressSanitizer\|runtime error:" "$LOG" || true)
+echo "# sanitizer reports: $reports" >> "$LOG"
+if [ "$rc" -ne 0 ]; then
+  echo "# FAILED: pytest exit status $rc" >> "$LOG"
+else
+  echo "# PASSED: pytest exit status 0" >> "$LOG"
+fi
 tail -5 "$LOG"
 exit $rc

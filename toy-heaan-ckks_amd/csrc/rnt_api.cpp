@@ -73,8 +73,20 @@ inline size_t word_bytes(const rnt::Tables* t) { return t->wide ? 8 : 4; }
 // (rnt_capture_begin .. rnt_capture_end): workspace blocks the captured ops
 // take stay with the graph, whose replays reuse those exact addresses, and
 // nothing that would synchronise the stream runs while recording.
+// Only blocks handed back on the recording's own device and stream go to the
+// graph (a block freed on another context while recording goes back to the
+// cache as usual).  Call-scoped workspace (CallWs) handed back while
+// recording is idle again for the next recorded op: `idle` blocks are taken
+// before the cache is asked, so N recorded key-switch ops share one
+// workspace (the recorded ops are ordered on the one captured stream), and
+// the graph keeps the distinct blocks only.
+struct OwnedBlock {
+  void* p;
+  size_t bytes;
+  bool idle;
+};
 struct Capture {
-  std::vector<std::pair<void*, size_t>> owned;
+  std::vector<OwnedBlock> owned;
   hipStream_t stream = nullptr;
   int device = 0;
 };
@@ -192,7 +204,17 @@ static void pool_release(const PoolBlock& w) {  // g_pool_mu NOT held
 // Smallest idle block on `device` of at least `bytes` (and at most twice
 // that, so a small request does not pin a multi-GiB block), made safe to use
 // on stream `s`; nullptr if none.
-static void* pool_take(int device, size_t bytes, hipStream_t s, size_t* got) {
+static void* pool_take(int device, size_t bytes, hipStream_t s, size_t* got, bool call_scoped) {
+  if (call_scoped && g_capture != nullptr && g_capture->device == device && g_capture->stream == s) {
+    OwnedBlock* best = nullptr;
+    for (OwnedBlock& o : g_capture->owned)
+      if (o.idle && o.bytes >= bytes && o.bytes / 2 <= bytes && (!best || o.bytes < best->bytes)) best = &o;
+    if (best) {
+      best->idle = false;
+      *got = best->bytes;
+      return best->p;
+    }
+  }
   PoolBlock w{};
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
@@ -225,8 +247,14 @@ static void* pool_take(int device, size_t bytes, hipStream_t s, size_t* got) {
 // oldest idle blocks of the device leave it while it is over its cap.
 static void pool_give(int device, void* p, size_t bytes, hipStream_t s) {
   if (!p) return;
-  if (g_capture != nullptr) {  // the recorded graph keeps using the block
-    g_capture->owned.push_back({p, bytes});
+  if (g_capture != nullptr && g_capture->device == device && g_capture->stream == s) {
+    // the recorded graph keeps using the block
+    for (OwnedBlock& o : g_capture->owned)
+      if (o.p == p) {
+        o.idle = true;
+        return;
+      }
+    g_capture->owned.push_back({p, bytes, true});
     return;
   }
   hipEvent_t ev = nullptr;
@@ -291,8 +319,9 @@ static size_t pool_drain(int device) {
 
 // A device block of at least `bytes` for work on stream `s`: from the cache,
 // else hipMalloc (after emptying the device's cache if that fails).
-static hipError_t pool_malloc(int device, size_t bytes, hipStream_t s, void** p, size_t* got) {
-  if ((*p = pool_take(device, bytes, s, got))) return hipSuccess;
+static hipError_t pool_malloc(int device, size_t bytes, hipStream_t s, void** p, size_t* got,
+                              bool call_scoped = false) {
+  if ((*p = pool_take(device, bytes, s, got, call_scoped))) return hipSuccess;
   hipError_t e = hipMalloc(p, bytes);
   if (e == hipErrorOutOfMemory) {
     (void)hipGetLastError();
@@ -342,7 +371,7 @@ struct CallWs {
   CallWs& operator=(const CallWs&) = delete;
   int get(size_t need) {
     size_t got = 0;
-    if (hipError_t e = pool_malloc(dev, need, s, &p, &got); e != hipSuccess)
+    if (hipError_t e = pool_malloc(dev, need, s, &p, &got, true); e != hipSuccess)
       return hip_fail(e, "hipMalloc(workspace)");
     bytes = got;
     return RNT_OK;
@@ -756,11 +785,18 @@ extern "C" int rnt_ctx_set_stream(const rnt_ctx* ctx, void* stream) {
 // ---------------------------------------------------------------------------
 // captured op sequences (hipGraph)
 // ---------------------------------------------------------------------------
+// A recorded graph owns the distinct workspace blocks its ops took (on
+// `device`); they go back to the cache when it is destroyed, behind an event
+// on `last` -- the stream the latest replay was queued on.  A replay on a
+// new stream (after rnt_ctx_set_stream) is first ordered after the previous
+// replays, so `last` covers every replay.
 struct rnt_graph {
   std::shared_ptr<rnt::Tables> t;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
-  std::vector<std::pair<void*, size_t>> owned;
+  std::vector<OwnedBlock> owned;
+  int device = 0;
+  hipStream_t last = nullptr;
 };
 
 extern "C" int rnt_capture_begin(const rnt_ctx* ctx) {
@@ -806,16 +842,18 @@ extern "C" int rnt_capture_end(const rnt_ctx* ctx, rnt_graph** out) {
     r->t = ctx->t;
     r->graph = g;
     r->owned = std::move(c->owned);
+    r->device = c->device;
+    r->last = c->stream;
     e = hipGraphInstantiate(&r->exec, g, nullptr, nullptr, 0);
   }
   if (e != hipSuccess) {
     const int dev = c->device;
     const hipStream_t st = c->stream;
-    std::vector<std::pair<void*, size_t>> owned = r ? std::move(r->owned) : std::move(c->owned);
+    std::vector<OwnedBlock> owned = r ? std::move(r->owned) : std::move(c->owned);
     if (g) (void)hipGraphDestroy(g);
     delete r;
     delete c;
-    for (auto& b : owned) pool_give(dev, b.first, b.second, st);
+    for (auto& b : owned) pool_give(dev, b.p, b.bytes, st);
     return hip_fail(e, "rnt_capture_end");
   }
   delete c;
@@ -826,20 +864,38 @@ extern "C" int rnt_capture_end(const rnt_ctx* ctx, rnt_graph** out) {
 extern "C" int rnt_graph_launch(rnt_graph* g) {
   if (!g) return fail(RNT_ERR_BAD_ARGUMENT, "null graph");
   if (g_capture != nullptr) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_graph_launch while recording");
-  HIP_TRY(hipSetDevice(g->t->device), "hipSetDevice");
-  HIP_TRY(hipGraphLaunch(g->exec, g->t->stream), "hipGraphLaunch");
+  HIP_TRY(hipSetDevice(g->device), "hipSetDevice");
+  hipStream_t s = g->t->stream;
+  if (g->last != s) {  // order this replay after the ones queued on the old stream
+    hipEvent_t ev = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+    hipError_t e = hipEventRecord(ev, g->last);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
+    (void)hipEventDestroy(ev);
+    HIP_TRY(e, "hipStreamWaitEvent");
+    g->last = s;
+  }
+  HIP_TRY(hipGraphLaunch(g->exec, s), "hipGraphLaunch");
   return RNT_OK;
 }
 
 extern "C" int rnt_graph_destroy(rnt_graph* g) {
   if (!g) return RNT_OK;
-  (void)hipSetDevice(g->t->device);
+  (void)hipSetDevice(g->device);
   // a replay may still be running: the blocks go back behind an event on
   // the stream the replays were queued on
-  for (auto& b : g->owned) pool_give(g->t->device, b.first, b.second, g->t->stream);
+  for (auto& b : g->owned) pool_give(g->device, b.p, b.bytes, g->last);
   if (g->exec) (void)hipGraphExecDestroy(g->exec);
   if (g->graph) (void)hipGraphDestroy(g->graph);
   delete g;
+  return RNT_OK;
+}
+
+extern "C" int rnt_graph_workspace(const rnt_graph* g, size_t* blocks, size_t* bytes) {
+  if (!g || !blocks || !bytes) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
+  *blocks = g->owned.size();
+  *bytes = 0;
+  for (const OwnedBlock& b : g->owned) *bytes += b.bytes;
   return RNT_OK;
 }
 

@@ -262,6 +262,17 @@ class Graph:
         if exc_type is None:
             check(rc)
             self._h = h
+        elif rc == 0 and h.value:
+            # the body raised: the graph (and the workspace it holds) is never replayed
+            load().rnt_graph_destroy(h)
+
+    def workspace(self) -> tuple[int, int]:
+        """(blocks, bytes) of device workspace the recorded graph holds."""
+        if self._h is None:
+            raise RuntimeError("graph was not recorded")
+        blocks, nbytes = ctypes.c_size_t(), ctypes.c_size_t()
+        check(load().rnt_graph_workspace(self._h, ctypes.byref(blocks), ctypes.byref(nbytes)))
+        return int(blocks.value), int(nbytes.value)
 
     def replay(self) -> None:
         if self._h is None:

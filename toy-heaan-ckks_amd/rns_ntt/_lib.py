@@ -110,6 +110,7 @@ SIGNATURES = {
     "rnt_capture_end": (c_int, [_P, POINTER(_P)]),
     "rnt_graph_launch": (c_int, [_P]),
     "rnt_graph_destroy": (c_int, [_P]),
+    "rnt_graph_workspace": (c_int, [_P, POINTER(c_size_t), POINTER(c_size_t)]),
     "rnt_buf_alloc": (c_int, [_P, c_size_t, POINTER(_P)]),
     "rnt_buf_free": (c_int, [_P]),
     "rnt_buf_n_polys": (c_int, [_P, POINTER(c_size_t)]),
