@@ -19,6 +19,10 @@ $(LIBDIR)/rnt_plane.o: $(CSRC)/rnt_plane.hip $(CSRC)/rnt_internal.hpp $(CSRC)/rn
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+$(LIBDIR)/rnt_mfma.o: $(CSRC)/rnt_mfma.hip $(CSRC)/rnt_internal.hpp $(CSRC)/rnt_hostmath.hpp
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 $(LIBDIR)/rnt_encode.o: $(CSRC)/rnt_encode.hip $(CSRC)/rnt_internal.hpp
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -31,7 +35,7 @@ $(LIBDIR)/rnt_api.o: $(CSRC)/rnt_api.cpp $(CSRC)/rnt_internal.hpp $(CSRC)/rnt_ho
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIBDIR)/librnsntt.so: $(LIBDIR)/rnt_kernels.o $(LIBDIR)/rnt_plane.o $(LIBDIR)/rnt_encode.o $(LIBDIR)/rnt_sample.o $(LIBDIR)/rnt_api.o
+$(LIBDIR)/librnsntt.so: $(LIBDIR)/rnt_kernels.o $(LIBDIR)/rnt_plane.o $(LIBDIR)/rnt_mfma.o $(LIBDIR)/rnt_encode.o $(LIBDIR)/rnt_sample.o $(LIBDIR)/rnt_api.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
 
 oracle/liboracle.so: oracle/oracle.c oracle/oracle.h

@@ -95,7 +95,8 @@ thread_local Capture* g_capture = nullptr;
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
-    "sfft", "sample", "copy", "plane_fwd", "plane_mul", "plane_fused", "plane_ntt_fwd", "plane_ntt_inv"};
+    "sfft", "sample", "copy", "plane_fwd", "plane_mul", "plane_fused", "plane_ntt_fwd", "plane_ntt_inv",
+    "mf_mul", "mf_ntt_fwd", "mf_ntt_inv"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -423,6 +424,23 @@ int check_same(const rnt_buf* a, const rnt_buf* b, const char* what) {
   return RNT_OK;
 }
 
+// The MFMA transform path (rnt_mfma.hip) for this context: RNT_PLANE=5 on
+// a basis it supports, its tables built on first use.
+bool use_mf(const rnt::Launch& k) {
+  rnt::Tables* t = const_cast<rnt::Tables*>(k.t);
+  if (t->plane != 5 || !rnt::mf_supported(t)) return false;
+  std::lock_guard<std::mutex> g(t->mf_mu);
+  if (!t->mf) {
+    std::string err;
+    if (rnt::mf_build(t, &err) != 0) {
+      fprintf(stderr, "rnsntt: %s; the MFMA path is off for this basis\n", err.c_str());
+      t->plane = 3;
+      return false;
+    }
+  }
+  return true;
+}
+
 // Inverse-transform src (NTT domain) into dst (same layout): dst may equal src.
 int to_coeff_into(const rnt_buf* src, void* dst) {
   rnt::Launch k = launch_for(src);
@@ -431,6 +449,10 @@ int to_coeff_into(const rnt_buf* src, void* dst) {
     HIP_TRY(hipMemcpyAsync(dst, src->data, poly_words(src) * word_bytes(k.t),
                            hipMemcpyDeviceToDevice, k.s),
             "hipMemcpyAsync");
+  if (use_mf(k)) {
+    LAUNCH(k.t, rnt::K_MF_NTT_INV, rnt::launch_mf_ntt(k, 1, dst, ls, 4), "MFMA inverse transform");
+    return RNT_OK;
+  }
   if (rnt::plane_ok(k.t)) {
     LAUNCH(k.t, rnt::K_PLANE_NTT_INV, rnt::launch_plane_ntt(k, 1, dst, ls), "plane inverse transform");
     return RNT_OK;
@@ -457,6 +479,7 @@ rnt::Tables::~Tables() {
   (void)hipFree(lconst);
   (void)hipFree(resc);
   (void)hipFree(resc_p);
+  (void)hipFree(mf);
   if (prof) {
     for (auto& r : prof->pending) {
       (void)hipEventDestroy(r.a);
@@ -1126,7 +1149,9 @@ extern "C" int rnt_ntt_fwd(rnt_buf* b) {
   if (int rc = set_device(b->ctx)) return rc;
   rnt::Launch k = launch_for(b);
   const uint64_t ls = limb_stride(b);
-  if (rnt::plane_ok(k.t)) {
+  if (use_mf(k)) {
+    LAUNCH(k.t, rnt::K_MF_NTT_FWD, rnt::launch_mf_ntt(k, 0, b->data, ls, 4), "MFMA forward transform");
+  } else if (rnt::plane_ok(k.t)) {
     // N = 2^16, u32 bases: the whole-plane transform (rnt_plane.hip)
     LAUNCH(k.t, rnt::K_PLANE_NTT_FWD, rnt::launch_plane_ntt(k, 0, b->data, ls), "plane forward transform");
   } else {
@@ -1135,6 +1160,18 @@ extern "C" int rnt_ntt_fwd(rnt_buf* b) {
     LAUNCH(k.t, rnt::K_ROW_FWD, rnt::launch_row(k, 0, b->data, nullptr, ls), "row forward");
   }
   b->in_ntt = 1;
+  return RNT_OK;
+}
+
+// Debug (tools/mfma_stage_check.py, not in include/rnsntt.h): the first
+// `stop` (2 or 3) MFMA forward passes in place, each word written canonical
+// at its in-place index; the buffer's domain flag is left as it was.
+extern "C" __attribute__((visibility("default"))) int rnt_debug_mf_stage(rnt_buf* b, int stop) {
+  if (int rc = check_buf(b, "rnt_debug_mf_stage")) return rc;
+  if (int rc = set_device(b->ctx)) return rc;
+  rnt::Launch k = launch_for(b);
+  if (!use_mf(k)) return fail(RNT_ERR_UNSUPPORTED, "the MFMA path is off (RNT_PLANE=5 at N = 2^16, u32)");
+  HIP_TRY(rnt::launch_mf_ntt(k, 0, b->data, limb_stride(b), stop), "MFMA stage");
   return RNT_OK;
 }
 
@@ -1173,6 +1210,11 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   // pointwise product, inverse rows), the inverse column pass.
   const uint64_t ls = limb_stride(out);
   if (int rc = ensure_ws(out, poly_words(out) * word_bytes(k.t))) return rc;
+  if (use_mf(k)) {
+    LAUNCH(k.t, rnt::K_MF_MUL, rnt::launch_mf_mul(k, out->data, a->data, b->data, out->ws, ls), "MFMA product");
+    out->in_ntt = 0;
+    return RNT_OK;
+  }
   if (rnt::plane_ok(k.t) && k.t->plane >= 3) {
     LAUNCH(k.t, rnt::K_PLANE_FUSED, rnt::launch_plane_fused(k, out->data, a->data, b->data, out->ws, ls),
            "plane fused product");

@@ -109,6 +109,10 @@ struct Tables {
   std::mutex sfft_mu;
   void* sfft_tw = nullptr;
   struct Prof* prof = nullptr;  // per-kernel event timing (rnt_profile_*)
+  // MFMA transform tables (rnt_mfma.hip: matrix operands, compensations and
+  // twists per limb), built on first use where mf_supported()
+  std::mutex mf_mu;
+  void* mf = nullptr;
   ~Tables();
 };
 
@@ -116,7 +120,8 @@ struct Tables {
 enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
-  K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FWD, K_PLANE_MUL, K_PLANE_FUSED, K_PLANE_NTT_FWD, K_PLANE_NTT_INV, K_COUNT
+  K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FWD, K_PLANE_MUL, K_PLANE_FUSED, K_PLANE_NTT_FWD, K_PLANE_NTT_INV,
+  K_MF_MUL, K_MF_NTT_FWD, K_MF_NTT_INV, K_COUNT
 };
 
 struct Prof {
@@ -201,6 +206,16 @@ hipError_t launch_plane(const Launch& k, int which, void* out, const void* in, c
 hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls);
 // standalone whole-plane transforms in place (N = 2^16, u32; plane_ok)
 hipError_t launch_plane_ntt(const Launch& k, int inverse, void* data, uint64_t ls);
+// The MFMA forms of the same (rnt_mfma.hip): radix-16 passes as i8 matrix
+// products.  mf_supported: u32 bases at N = 2^16 (the tables exist once
+// mf_build ran); mf_build: the per-limb tables into t->mf (0 ok, else err).
+inline bool mf_supported(const Tables* t) { return !t->wide && t->log_n == 16; }
+int mf_build(Tables* t, std::string* err);
+// out = a * b (coefficient domain; out may alias a or b; scratch: one word
+// per output word)
+hipError_t launch_mf_mul(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls);
+// in place; stop 4 = the whole transform, 2 / 3 = debug prefixes of the forward
+hipError_t launch_mf_ntt(const Launch& k, int inverse, void* data, uint64_t ls, int stop);
 // Whether rnt_mul's row kernel stops its transforms two stages early and
 // multiplies degree-3 residues (u32 canonical bases, row length 2^(4k));
 // its inverse column pass then takes rfold = 2.

@@ -1,0 +1,899 @@
+// rnt_mfma.hip -- the whole-plane poly-mul and transforms at N = 2^16 (u32
+// bases) on the matrix cores: radix-16 passes as i8 MFMA products.
+//
+// Reference unit: one coefficient-domain `a *= &b` (poly.rs:307-329:
+// to_ntt_domain of both operands, the pointwise mul_mod, to_coeff_domain)
+// and the standalone to_ntt_domain / to_coeff_domain (poly.rs:136-166).
+// The network is the four-step kernels' merged negacyclic CT / GS heap, so
+// the NTT-domain words are the same (device order = the in-place CT order)
+// and the product is the reference's word for word (R1: exact arithmetic).
+//
+// ---- the transform as four 16 x 16 matrix passes ----------
+// Pass p (p = 0..3) runs the four CT stages at index bits 15-4p .. 12-4p.
+// On each group of 16 words that differ only in those bits (k = the 4-bit
+// group index) it is one 16 x 16 matrix M_U, U = the index bits above the
+// pass: M_U[j][k] = z_{U,j}^k (a Vandermonde matrix on the 16 roots of the
+// group's modulus), and M_U = F . diag(beta_U^k) with ONE matrix F for every
+// pass and U (beta_U = psi_rev[(N >> (b_lo + 1)) + 8U], the heap node of the
+// pass's last stage at the group's first word; tools/mfma_model.py checks
+// both facts and the four passes against the oracle).  So:
+//   pass 0: M_0 itself (one matrix);
+//   pass 1: M_U with U = the wave's 4 bits (one matrix per wave);
+//   passes 2, 3: F, with the twist beta_U^k applied to the data first (one
+//            signed Montgomery product per word, twiddles from a table).
+// The inverse runs the inverse matrices in the mirror order (the twist
+// after F^-1); n^-1 and, after a product, the Montgomery factor 2^32 of the
+// pointwise product are folded into its last matrix.
+//
+// ---- exact integer matrix products on the i8 matrix cores -----------------
+// Words travel between passes as signed representatives r, |r| < q/2 + 2^14,
+// packed as four balanced byte digits: (r + 0x80808080) ^ 0x80808080 (byte b
+// of that is digit b, in [-128, 128)).  A pass computes, for each output j,
+//   T_j = sum_{k,b} E[j][k][b] * x_k^(b),   E[j][k][b] = centred(W[j][k] 2^(8b) 2^32 mod q)
+// with E split into four digit planes too: v_mfma_i32_16x16x64_i8 forms the
+// digit sums C_a (K = 64 = 16 words x 4 data digits, |C_a| <= 2^20), and
+//   T = (C_0 + 2^8 C_1) + 2^16 (C_2 + 2^8 C_3),  |T| < 2^46,
+//   r' = (T + m q) / 2^32,  m = T (-q^-1) mod 2^32  (signed Montgomery),
+// gives r' = sum_k W[j][k] x_k mod q in (-q/2 - 2^14, q/2 + 2^14), which packs
+// again (the +0x80808080 rides in the reduction's 64-bit addend).  About 7
+// VALU instructions per word per pass (10 with a twist) instead of 22 for
+// four radix-2 CT stages; the MFMAs (4 per 256 words) run beside them.
+//
+// ---- layouts -----------------------------------------------------------------
+// One 1024-thread workgroup per (poly, limb) plane, 64 words a thread as 16
+// chunks c of 4 registers i.  Thread t = (wave w, lane lam = 16 g + n).  An
+// MFMA tile is one chunk of one wave: K is split over the lane group g and
+// the chunk's 4 registers, the 16 columns (or rows) are n.  The index bits
+// of each layout (g = lane bits 5,4; n = lane bits 3..0):
+//   P1: i=(15,14) g=(13,12) n=(5,4,3,2) w=(11,9,8,6) c=(7,10,1,0)  [loads: 16 B/lane]
+//   P2: i=(11,10) g=(9,8)   n=(3..0)    w=(15..12)   c=(7,6,5,4)
+//   P3: i=(7,6)   g=(5,4)   n=(3..0)    w=(15..12)   c=(11..8)
+//   P4: i=(1,0)   g=(3,2)   n=(7..4)    w=(15..12)   c=(11..8)   [NTT-domain stores: 16 B/lane]
+//   Q3: i=(5,4)   g=(7,6)   n=(3..0)    w=(15..12)   c=(11..8)   (inverse)
+// P1 -> P2 goes through LDS (two rounds of 128 KiB split on bit 7, the pass
+// of one round's chunks running while the other round's words move); P2 ->
+// P3 and Q3 -> P2 trade lane bits 5,4 with two register bits
+// (v_permlane32_swap / v_permlane16_swap); P3 -> P4 and P4 -> Q3 are free:
+// the pass takes the data as the MFMA's A operand, whose result puts the
+// output index on the lanes and the data rows on lane group and register
+// (D[row][col] at lane 16 (row >> 2) + col, register row & 3).
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "rnt_internal.hpp"
+#include "rnt_hostmath.hpp"
+
+namespace rnt {
+namespace mf {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int kT = 1024;
+constexpr uint32_t kN = 1u << 16;
+constexpr uint32_t K32 = 0x80808080u;
+
+// ---- per-limb table (v4i units): MFMA operands, compensations, twists ----
+// Matrix slot s, digit plane a, lane lam: operand bytes of that lane.
+constexpr int S_F1 = 0, S_F2 = 1, S_F3 = 17, S_F4 = 18, S_I4 = 19, S_I3 = 20, S_I2 = 21, S_I1R = 37, S_I1 = 38;
+constexpr int kSlots = 39;
+constexpr int kMat = 0;
+constexpr int kCompF1 = kSlots * 4 * 64;  // [lam]: digit-0 accumulator start of pass 0 (input bias)
+constexpr int kCompI4 = kCompF1 + 64;     // [lam]: the same for the standalone inverse's first pass
+constexpr int kTw3f = kCompI4 + 64;       // [w][g][c], element i: pass 2 twist, P2 positions
+constexpr int kTw4f = kTw3f + 1024;       // [w][c][lam]: pass 3 twist, P4 positions
+constexpr int kTw4i = kTw4f + 16384;      // [w][c][lam]: inverse pass 3 twist, Q3 positions
+constexpr int kTw3i = kTw4i + 16384;      // [w][c][g]: inverse pass 2 twist, Q3 positions
+constexpr int kLimb = kTw3i + 1024;
+
+// Registers of a P3 / P4 / Q3 chunk (c, i) after the P2 -> P3 swap, as
+// physical slots of the P2 numbering 4c + i (see the header).
+__host__ __device__ constexpr int p3(int c, int i) {
+  return 4 * (8 * (i >> 1) + 4 * (i & 1) + 2 * ((c >> 1) & 1) + (c & 1)) + 2 * (c >> 3) + ((c >> 2) & 1);
+}
+// P2 chunk (c, i) after the inverse's Q3 -> P2 swap.
+__host__ __device__ constexpr int q2(int c, int i) {
+  return p3(8 * (i >> 1) + 4 * (i & 1) + 2 * (c >> 3) + ((c >> 2) & 1), 2 * ((c >> 1) & 1) + (c & 1));
+}
+
+struct Mc {
+  int32_t q;       // modulus < 2^31
+  uint32_t nqinv;  // -q^-1 mod 2^32
+  int64_t K;       // 0x80808080 << 32: the digit bias, added in a reduction's addend
+  int64_t K0;      // 0 (opaque)
+  int32_t one;     // opaque 1 and 2^16 (SGPR operands of v_mad_i64_i32)
+  int32_t s16;
+};
+
+// Every global access goes through a buffer descriptor (base and range in
+// SGPRs): a lane offset in a VGPR, the rest as the SGPR offset, so no 64-bit
+// addresses live in VGPRs.
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ v4i bld(Rsrc r, uint32_t voff, uint32_t soff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  return v4i{(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
+}
+__device__ __forceinline__ void bst(v4i x, Rsrc r, uint32_t voff, uint32_t soff) {
+  using V4 = decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0));
+  V4 v;
+  v[0] = (uint32_t)x[0];
+  v[1] = (uint32_t)x[1];
+  v[2] = (uint32_t)x[2];
+  v[3] = (uint32_t)x[3];
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+}
+
+__device__ __forceinline__ v4i mfma(v4i a, v4i b, v4i c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+// Output word from its four digit sums: r = T 2^-32 mod q (signed
+// representative), + 0x80808080 when WK (then ^ K32 packs it).
+template <bool WK>
+__device__ __forceinline__ int32_t recomb(int32_t c0, int32_t c1, int32_t c2, int32_t c3, const Mc& m) {
+  const int32_t lo = c0 + (int32_t)((uint32_t)c1 << 8);
+  const int32_t hi = c2 + (int32_t)((uint32_t)c3 << 8);
+  int64_t t;
+  t = (int64_t)lo * m.one + (WK ? m.K : m.K0);
+  t = (int64_t)hi * m.s16 + t;
+  const uint32_t mm = (uint32_t)t * m.nqinv;
+  const int64_t v = (int64_t)(int32_t)mm * m.q + t;
+  return (int32_t)(v >> 32);
+}
+// Signed Montgomery product a b 2^-32 mod q (|a|, |b| < 2^30.01), + 0x80808080 when WK.
+template <bool WK>
+__device__ __forceinline__ int32_t mont(int32_t a, int32_t b, const Mc& m) {
+  // one v_mad_i64_i32 (left to itself hipcc widens a -- the high word of
+  // the previous reduction -- to a 64-bit multiply of six instructions)
+  int64_t p;
+  uint64_t cc;
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(p), "=s"(cc) : "v"(a), "v"(b), "s"(WK ? m.K : m.K0));
+  const uint32_t mm = (uint32_t)p * m.nqinv;
+  const int64_t v = (int64_t)(int32_t)mm * m.q + p;
+  return (int32_t)(v >> 32);
+}
+// The end of one tile's work: hipcc would otherwise hoist later tiles'
+// MFMAs and loads above it and keep their digit sums live (spills).
+__device__ __forceinline__ void tile_fence() {
+#ifndef RNT_MF_NOFENCE
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+__device__ __forceinline__ uint32_t pk_canon(uint32_t x) { return (x + 0x40808080u) ^ K32; }  // x - 2^30, packed
+__device__ __forceinline__ uint32_t canon(int32_t r, int32_t q) { return (uint32_t)(r + ((r >> 31) & q)); }
+
+// One MFMA tile: the four digit planes of a 16 x 16 x 64 product.
+// DA: the data is the A operand (the matrix the B operand).
+template <bool DA>
+__device__ __forceinline__ void tile(v4i (&D)[4], const v4i (&M)[4], v4i dat, v4i c0) {
+  const v4i z = {0, 0, 0, 0};
+#pragma unroll
+  for (int a = 0; a < 4; ++a) D[a] = DA ? mfma(dat, M[a], a == 0 ? c0 : z) : mfma(M[a], dat, a == 0 ? c0 : z);
+}
+// the table of one limb; lo = lam * 16 (the lane's 16 bytes of an operand row)
+__device__ __forceinline__ void load_mat(v4i (&M)[4], Rsrc tab, uint32_t slot, uint32_t lo) {
+#pragma unroll
+  for (int a = 0; a < 4; ++a) M[a] = bld(tab, lo, (uint32_t)(kMat + (slot * 4 + a) * 64) * 16u);
+}
+
+struct Th {
+  uint32_t t, w, lam, g, n;
+  __device__ explicit Th(uint32_t tt)
+      : t(tt), w(__builtin_amdgcn_readfirstlane(tt >> 6)), lam(tt & 63u), g((tt >> 4) & 3u), n(tt & 15u) {}
+};
+
+// ---- P1 <-> P2 through LDS ----------------------------------------------------
+// LDS word of index bits (bit 7 = the round) -- conflict-free for 4-byte
+// accesses from both layouts (32-lane halves vary bits 12,5..2 in P1 and
+// 8,3..0 in P2):
+//   (b0^b4) + 2(b1^b5) + 4b2 + 8b3 + 16(b8^b12) + 32b10 + 64b14 + 128b15
+//   + 256b6 + 512b11 + 1024b4 + 2048b5 + 4096b12 + 8192b13 + 16384b9
+// Per thread: a base per value of the two register bits inside an XOR term,
+// the other register bits as instruction offsets.
+__device__ __forceinline__ void p1_bases(uint32_t (&wb)[4], const Th& h) {
+  const uint32_t n0 = h.n & 1, n1 = (h.n >> 1) & 1, n2 = (h.n >> 2) & 1, n3 = h.n >> 3;
+  const uint32_t g0 = h.g & 1, g1 = h.g >> 1;
+  const uint32_t w0 = h.w & 1, w1 = (h.w >> 1) & 1, w2 = (h.w >> 2) & 1, w3 = h.w >> 3;
+  const uint32_t rest = 4 * n0 + 8 * n1 + 16 * (w1 ^ g0) + 256 * w0 + 512 * w3 + 1024 * n2 + 2048 * n3 +
+                        4096 * g0 + 8192 * g1 + 16384 * w2;
+#pragma unroll
+  for (uint32_t e = 0; e < 4; ++e) wb[e] = rest + ((e & 1) ^ n2) + 2 * ((e >> 1) ^ n3);
+}
+__device__ __forceinline__ void p2_bases(uint32_t (&rb)[4], const Th& h) {
+  const uint32_t n0 = h.n & 1, n1 = (h.n >> 1) & 1, n2 = (h.n >> 2) & 1, n3 = h.n >> 3;
+  const uint32_t g0 = h.g & 1, g1 = h.g >> 1;
+  const uint32_t w0 = h.w & 1, w1 = (h.w >> 1) & 1, w2 = (h.w >> 2) & 1, w3 = h.w >> 3;
+  const uint32_t rest = 4 * n2 + 8 * n3 + 16 * (g0 ^ w0) + 64 * w2 + 128 * w3 + 4096 * w0 + 8192 * w1 + 16384 * g1;
+#pragma unroll
+  for (uint32_t e = 0; e < 4; ++e) rb[e] = rest + (n0 ^ (e & 1)) + 2 * (n1 ^ (e >> 1)) + 1024 * (e & 1) + 2048 * (e >> 1);
+}
+// P1 register (c, i) / P2 register (c, i): word offset beside the base.
+__host__ __device__ constexpr uint32_t p1_off(int c, int i) { return 32u * ((c >> 2) & 1) + 64u * (i & 1) + 128u * (i >> 1); }
+__host__ __device__ constexpr uint32_t p2_off(int c, int i) { return 32u * (i & 1) + 512u * (i >> 1) + 256u * ((c >> 2) & 1); }
+
+// Round H of P1 -> P2: P1 chunks 8H .. 8H+7 out, P2 chunks 8H .. 8H+7 in.
+template <int H>
+__device__ __forceinline__ void x_write_p1(const uint32_t (&x1)[64], uint32_t* lds, const uint32_t (&wb)[4]) {
+#pragma unroll
+  for (int c = 8 * H; c < 8 * H + 8; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lds[wb[c & 3] + p1_off(c, i)] = x1[4 * c + i];
+}
+template <int H>
+__device__ __forceinline__ void x_read_p2(uint32_t (&x2)[64], const uint32_t* lds, const uint32_t (&rb)[4]) {
+#pragma unroll
+  for (int c = 8 * H; c < 8 * H + 8; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x2[4 * c + i] = lds[rb[c & 3] + p2_off(c, i)];
+}
+// the inverse direction: P2 words at q2(c, i) out, P1 words in
+template <int H>
+__device__ __forceinline__ void x_write_p2(const uint32_t (&x2)[64], uint32_t* lds, const uint32_t (&rb)[4]) {
+#pragma unroll
+  for (int c = 8 * H; c < 8 * H + 8; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lds[rb[c & 3] + p2_off(c, i)] = x2[q2(c, i)];
+}
+template <int H>
+__device__ __forceinline__ void x_read_p1(uint32_t (&x1)[64], const uint32_t* lds, const uint32_t (&wb)[4]) {
+#pragma unroll
+  for (int c = 8 * H; c < 8 * H + 8; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x1[4 * c + i] = lds[wb[c & 3] + p1_off(c, i)];
+}
+
+// Lane bits 5, 4 <-> the register bits of chunk bits 1, 0: P2 -> P3.
+__device__ __forceinline__ void swap_p2p3(uint32_t (&x)[64]) {
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    if (c & 2) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane32_swap(x[4 * c + i], x[4 * (c | 2) + i], false, false);
+      x[4 * c + i] = r[0];
+      x[4 * (c | 2) + i] = r[1];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    if (c & 1) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane16_swap(x[4 * c + i], x[4 * (c | 1) + i], false, false);
+      x[4 * c + i] = r[0];
+      x[4 * (c | 1) + i] = r[1];
+    }
+  }
+}
+// Q3 -> P2 (the inverse): Q3 chunk bits 1, 0 (index bits 9, 8) <-> lane bits 5, 4.
+__device__ __forceinline__ void swap_q3p2(uint32_t (&x)[64]) {
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    if (c & 2) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane32_swap(x[p3(c, i)], x[p3(c | 2, i)], false, false);
+      x[p3(c, i)] = r[0];
+      x[p3(c | 2, i)] = r[1];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    if (c & 1) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane16_swap(x[p3(c, i)], x[p3(c | 1, i)], false, false);
+      x[p3(c, i)] = r[0];
+      x[p3(c | 1, i)] = r[1];
+    }
+  }
+}
+
+// ---- the passes -------------------------------------------------------------
+// pass 0 on P1 chunks [C0, C0 + 8): input canonical (BIAS: packed with the
+// -2^30 shift its compensation undoes) or packed; output packed.
+template <int C0, bool BIAS>
+__device__ __forceinline__ void pass_p1(uint32_t (&x1)[64], const v4i (&M)[4], v4i comp, const Mc& m) {
+  const v4i z = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = C0; c < C0 + 8; ++c) {
+    v4i b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = (int)(BIAS ? pk_canon(x1[4 * c + i]) : x1[4 * c + i]);
+    v4i D[4];
+    tile<false>(D, M, b, BIAS ? comp : z);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x1[4 * c + i] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
+    tile_fence();
+  }
+}
+// pass 1 (per-wave matrix) on P2 chunks [C0, C0 + 8), then the pass-2 twist
+// (TW: the table in P2 positions; DBG_NOTW leaves it out: measurement of pass 1).
+template <int C0, bool DBG_NOTW = false>
+__device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
+                                        const Mc& m) {
+  const v4i z = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = C0; c < C0 + 8; ++c) {
+    v4i b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = (int)x2[4 * c + i];
+    const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 16u);
+    v4i D[4];
+    tile<false>(D, M, b, z);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
+      x2[4 * c + i] = DBG_NOTW ? (uint32_t)(r + (int32_t)K32) ^ K32 : (uint32_t)mont<true>(r, tv[i], m) ^ K32;
+    }
+    tile_fence();
+  }
+}
+// pass 2 (F, data as A: P3 -> P4 positions), then the pass-3 twist.
+template <bool DBG_NOTW = false>
+__device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
+                                        const Mc& m) {
+  const v4i z = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    v4i a;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = (int)x[p3(c, i)];
+    const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 1024u);
+    v4i D[4];
+    tile<true>(D, M, a, z);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
+      x[p3(c, i)] = DBG_NOTW ? (uint32_t)(r + (int32_t)K32) ^ K32 : (uint32_t)mont<true>(r, tv[i], m) ^ K32;
+    }
+    tile_fence();
+  }
+}
+// pass 3 (F, P4 in place): each tile's centred outputs go to EPI(c, r, x)
+// at once (stored, or multiplied into the product), so no 64-bit reduction
+// result stays live beyond its tile.
+template <class EPI>
+__device__ __forceinline__ void pass_p4(uint32_t (&x)[64], const v4i (&M)[4], const Mc& m, const EPI& epi) {
+  const v4i z = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    v4i b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = (int)x[p3(c, i)];
+    v4i D[4];
+    tile<false>(D, M, b, z);
+    int32_t r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
+    epi(c, r, x);
+    tile_fence();
+  }
+}
+// inverse pass 3 (F^-1, data as A: P4 -> Q3), then its twist; packed output.
+__device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v4i comp, Rsrc tab, uint32_t tvo,
+                                         uint32_t tso, const Mc& m) {
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    v4i a;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = (int)x[p3(c, i)];
+    const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 1024u);
+    v4i D[4];
+    tile<true>(D, M, a, comp);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
+      x[p3(c, i)] = (uint32_t)mont<true>(r, tv[i], m) ^ K32;
+    }
+    tile_fence();
+  }
+}
+// inverse pass 2 (F^-1 in Q3), then its twist; packed output.
+__device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
+                                         const Mc& m) {
+  const v4i z = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    v4i b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = (int)x[p3(c, i)];
+    const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 64u);
+    v4i D[4];
+    tile<false>(D, M, b, z);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
+      x[p3(c, i)] = (uint32_t)mont<true>(r, tv[i], m) ^ K32;
+    }
+    tile_fence();
+  }
+}
+// inverse pass 1 (per-wave matrix) on P2 chunks [C0, C0 + 8) at q2 slots; packed output.
+template <int C0>
+__device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], const Mc& m) {
+  const v4i z = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = C0; c < C0 + 8; ++c) {
+    v4i b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = (int)x[q2(c, i)];
+    v4i D[4];
+    tile<false>(D, M, b, z);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[q2(c, i)] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
+    tile_fence();
+  }
+}
+// inverse pass 0 on P1 chunks [C0, C0 + 8): canonical output.
+template <int C0>
+__device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], const Mc& m) {
+  const v4i z = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = C0; c < C0 + 8; ++c) {
+    v4i b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = (int)x1[4 * c + i];
+    v4i D[4];
+    tile<false>(D, M, b, z);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x1[4 * c + i] = canon(recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m), m.q);
+    tile_fence();
+  }
+}
+
+// P1 plane byte offsets of load / store (i, hc): 4 consecutive words,
+// chunks c = 4 hc + e, e = 0..3.  Lane part (VGPR), wave part and the
+// register part (SGPR).
+__device__ __forceinline__ uint32_t p1_lane(const Th& h) { return ((h.g << 12) | (h.n << 2)) * 4u; }
+__device__ __forceinline__ uint32_t p1_wave(const Th& h) {
+  const uint32_t w = h.w;
+  return (((w >> 3) << 11) | (((w >> 2) & 1) << 9) | (((w >> 1) & 1) << 8) | ((w & 1) << 6)) * 4u;
+}
+__host__ __device__ constexpr uint32_t p1_reg(int i, int hc) {
+  return (((uint32_t)i << 14) | ((uint32_t)(hc & 1) << 10) | ((uint32_t)(hc >> 1) << 7)) * 4u;
+}
+__device__ __forceinline__ void load_p1(uint32_t (&x1)[64], Rsrc src, const Th& h) {
+  const uint32_t lo = p1_lane(h), wo = p1_wave(h);
+#pragma unroll
+  for (int hc = 0; hc < 4; ++hc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const v4i v = bld(src, lo, wo + p1_reg(i, hc));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) x1[4 * (4 * hc + e) + i] = (uint32_t)v[e];
+    }
+}
+__device__ __forceinline__ void store_p1(const uint32_t (&x1)[64], Rsrc dst, const Th& h) {
+  const uint32_t lo = p1_lane(h), wo = p1_wave(h);
+#pragma unroll
+  for (int hc = 0; hc < 4; ++hc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v4i v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (int)x1[4 * (4 * hc + e) + i];
+      bst(v, dst, lo, wo + p1_reg(i, hc));
+    }
+}
+// P4 (NTT-domain device order): chunk c's 4 words are consecutive.
+__device__ __forceinline__ uint32_t p4_lane(const Th& h) { return ((h.n << 4) | (h.g << 2)) * 4u; }
+__device__ __forceinline__ uint32_t p4_soff(const Th& h, int c) { return ((h.w << 12) | ((uint32_t)c << 8)) * 4u; }
+
+struct Tabs {
+  Rsrc tab;  // this limb's table
+  Mc m;
+};
+__device__ __forceinline__ Tabs tabs_of(const void* mf, const LimbConst<uint32_t>& lc, uint32_t l) {
+  Tabs r;
+  r.tab = rsrc((const v4i*)mf + (size_t)l * kLimb, (uint32_t)kLimb * 16u);
+  r.m.q = (int32_t)lc.q;
+  r.m.nqinv = 0u - lc.qinv;
+  int64_t K = (int64_t)((uint64_t)K32 << 32), K0 = 0;
+  int32_t one = 1, s16 = 65536;
+  asm volatile("" : "+s"(one), "+s"(s16), "+s"(K), "+s"(K0));
+  r.m.K = K;
+  r.m.K0 = K0;
+  r.m.one = one;
+  r.m.s16 = s16;
+  return r;
+}
+
+// The forward transform: canonical plane at src (P1) -> x2 in P4 positions,
+// centred representatives.  SYNC1: the LDS may still be in use by other waves.
+// STOP (measurement of a prefix, debug only): 1..4 passes.
+struct NoEpi {
+  __device__ void operator()(int, const int32_t (&)[4], uint32_t (&)[64]) const {}
+};
+template <bool SYNC1, int STOP = 4, class EPI = NoEpi>
+__device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds, const Th& h, const Tabs& T,
+                                    const EPI& epi = EPI{}) {
+  uint32_t x1[64];
+  load_p1(x1, src, h);
+  const Mc& m = T.m;
+  const uint32_t lo = h.lam * 16u;
+  v4i M[4];
+  load_mat(M, T.tab, S_F1, lo);
+  const v4i comp = bld(T.tab, lo, (uint32_t)kCompF1 * 16u);
+  pass_p1<0, true>(x1, M, comp, m);
+  if constexpr (SYNC1) __syncthreads();
+  uint32_t wb[4], rb[4];
+  p1_bases(wb, h);
+  x_write_p1<0>(x1, lds, wb);
+  pass_p1<8, true>(x1, M, comp, m);
+  __syncthreads();
+  p2_bases(rb, h);
+  x_read_p2<0>(x2, lds, rb);
+  __syncthreads();
+  p1_bases(wb, h);
+  x_write_p1<1>(x1, lds, wb);
+  load_mat(M, T.tab, S_F2 + h.w, lo);
+  const uint32_t t3v = h.g * 256u, t3s = (uint32_t)(kTw3f + h.w * 64) * 16u;
+  pass_p2<0, STOP == 2>(x2, M, T.tab, t3v, t3s, m);
+  __syncthreads();
+  p2_bases(rb, h);
+  x_read_p2<1>(x2, lds, rb);
+  pass_p2<8, STOP == 2>(x2, M, T.tab, t3v, t3s, m);
+  if constexpr (STOP <= 2) return;
+  swap_p2p3(x2);
+  load_mat(M, T.tab, S_F3, lo);
+  pass_p3<STOP == 3>(x2, M, T.tab, lo, (uint32_t)(kTw4f + h.w * 1024) * 16u, m);
+  if constexpr (STOP <= 3) return;
+  load_mat(M, T.tab, S_F4, lo);
+  pass_p4(x2, M, m, epi);
+}
+
+// The inverse from x2 (packed, P4 positions) to the canonical plane at dst
+// (P1); SLOT1: the last matrix (S_I1R after a product, S_I1 standalone);
+// comp: the first pass's digit-0 start (input bias of a standalone inverse).
+template <bool BIAS>
+__device__ __forceinline__ void inv(uint32_t (&x2)[64], Rsrc dst, uint32_t* lds, const Th& h, const Tabs& T,
+                                    uint32_t slot1) {
+  const Mc& m = T.m;
+  const uint32_t lo = h.lam * 16u;
+  v4i M[4];
+  load_mat(M, T.tab, S_I4, lo);
+  const v4i z = {0, 0, 0, 0};
+  ipass_p4(x2, M, BIAS ? bld(T.tab, lo, (uint32_t)kCompI4 * 16u) : z, T.tab, lo, (uint32_t)(kTw4i + h.w * 1024) * 16u,
+           m);
+  load_mat(M, T.tab, S_I3, lo);
+  ipass_p3(x2, M, T.tab, h.g * 16u, (uint32_t)(kTw3i + h.w * 64) * 16u, m);
+  swap_q3p2(x2);
+  load_mat(M, T.tab, S_I2 + h.w, lo);
+  uint32_t wb[4], rb[4];
+  uint32_t x1[64];
+  ipass_p2<0>(x2, M, m);
+  __syncthreads();  // other waves may still read the LDS (the last forward exchange)
+  p2_bases(rb, h);
+  x_write_p2<0>(x2, lds, rb);
+  ipass_p2<8>(x2, M, m);
+  __syncthreads();
+  p1_bases(wb, h);
+  x_read_p1<0>(x1, lds, wb);
+  __syncthreads();
+  p2_bases(rb, h);
+  x_write_p2<1>(x2, lds, rb);
+  load_mat(M, T.tab, slot1, lo);
+  ipass_p1<0>(x1, M, m);
+  __syncthreads();
+  p1_bases(wb, h);
+  x_read_p1<1>(x1, lds, wb);
+  ipass_p1<8>(x1, M, m);
+  store_p1(x1, dst, h);
+}
+
+constexpr size_t kLdsBytes = (size_t)(1u << 15) * 4;  // one exchange round
+
+}  // namespace mf
+
+// One workgroup per (poly, limb) plane pair, grid (B, L): c = a * b.
+// a^ goes to a scratch plane (this thread's words, 16 B per chunk) and
+// comes back for the pointwise product.
+__global__ void __launch_bounds__(mf::kT, 1)
+k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
+         const void* __restrict__ mft, const LimbConst<uint32_t>* __restrict__ lcs, uint64_t ls) {
+  using namespace mf;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const Th h(threadIdx.x);
+  const uint32_t poly = blockIdx.x, l = blockIdx.y;
+  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * kN;
+  const Tabs T = tabs_of(mft, lcs[l], l);
+  constexpr uint32_t PB = kN * 4u;
+  uint32_t x[64];
+  const Rsrc ah = rsrc(scratch + off, PB);
+  const uint32_t ao = h.t * 16u;
+  // a^: each tile of the last pass straight to the scratch plane
+  fwd<false>(x, rsrc(a + off, PB), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+    bst(v4i{r[0], r[1], r[2], r[3]}, ah, ao, (uint32_t)cc * (kT * 16u));
+  });
+  // b^: each tile of the last pass times a^ (Montgomery), packed for the inverse
+  fwd<true>(x, rsrc(b + off, PB), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
+    const v4i v = bld(ah, ao, (uint32_t)cc * (kT * 16u));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xx[p3(cc, i)] = (uint32_t)mont<true>(v[i], r[i], T.m) ^ K32;
+  });
+  inv<false>(x, rsrc(c + off, PB), lds, h, T, S_I1R);
+}
+
+// Standalone transforms in place (rnt_ntt_fwd / rnt_ntt_inv at N = 2^16).
+// STOP < 4 (debug: tools/mfma_stage_check.py): the first STOP forward
+// passes, the words written canonical at their in-place index.
+template <bool INV, int STOP = 4>
+__global__ void __launch_bounds__(mf::kT, 1)
+k_mf_ntt(uint32_t* __restrict__ data, const void* __restrict__ mft, const LimbConst<uint32_t>* __restrict__ lcs,
+         uint64_t ls) {
+  using namespace mf;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const Th h(threadIdx.x);
+  const uint32_t poly = blockIdx.x, l = blockIdx.y;
+  uint32_t* p = data + (uint64_t)l * ls + (uint64_t)poly * kN;
+  const Tabs T = tabs_of(mft, lcs[l], l);
+  const Rsrc pr = rsrc(p, kN * 4u);
+  uint32_t x[64];
+  if constexpr (!INV) {
+    // the last pass stores each tile, canonical, in the device order (in
+    // place: every wave read its words of the plane before the first
+    // exchange's barrier)
+    fwd<false, STOP>(x, pr, lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+      bst(v4i{(int)canon(r[0], T.m.q), (int)canon(r[1], T.m.q), (int)canon(r[2], T.m.q), (int)canon(r[3], T.m.q)}, pr,
+          p4_lane(h), p4_soff(h, cc));
+    });
+    if constexpr (STOP == 2) {
+      __syncthreads();
+      // P2 positions, packed (untwisted)
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int32_t r = (int32_t)((x[4 * cc + i] ^ K32) - K32);
+          p[(h.w << 12) | ((uint32_t)i << 10) | (h.g << 8) | ((uint32_t)cc << 4) | h.n] = canon(r % T.m.q, T.m.q);
+        }
+    } else if constexpr (STOP == 3) {
+      __syncthreads();
+      // P4 positions, packed (untwisted)
+#pragma unroll
+      for (int cc = 0; cc < 16; ++cc)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int32_t r = (int32_t)((x[p3(cc, i)] ^ K32) - K32);
+          p[((h.w << 12) | ((uint32_t)cc << 8) | (h.n << 4) | (h.g << 2)) + (uint32_t)i] = canon(r % T.m.q, T.m.q);
+        }
+    }
+  } else {
+#pragma unroll
+    for (int cc = 0; cc < 16; ++cc) {
+      const v4i v = bld(pr, p4_lane(h), p4_soff(h, cc));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[p3(cc, i)] = pk_canon((uint32_t)v[i]);
+    }
+    __syncthreads();  // every wave has read its words before any is written back
+    inv<true>(x, pr, lds, h, T, S_I1);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host: the per-limb table
+// ---------------------------------------------------------------------------
+namespace {
+using host::brv;
+using host::invmod;
+using host::mulmod;
+using host::powmod;
+
+int32_t centred(uint64_t v, uint64_t q) {
+  v %= q;
+  return v > q / 2 ? (int32_t)((int64_t)v - (int64_t)q) : (int32_t)v;
+}
+
+// W[out][in] (mod q) as MFMA operand bytes of digit planes a = 0..3 for the
+// 64 lanes (4 words each): E[o][k][b] = centred(W[o][k] 2^(8b) 2^32), its
+// balanced byte digits.  DA: the matrix is the B operand (lane 16 g + col,
+// output col); else the A operand (lane 16 g + row, output kappa(row >> 2,
+// row & 3)).  kappa(g, i) = 4i + g (KAP 0) or 4g + i (KAP 1): the group
+// index of the data in lane group g, register i.
+void expand(const uint64_t (&W)[16][16], uint64_t q, uint64_t R, bool DA, int KAP, int32_t* out) {
+  int32_t E[16][16][4];
+  for (int o = 0; o < 16; ++o)
+    for (int k = 0; k < 16; ++k)
+      for (int b = 0; b < 4; ++b) E[o][k][b] = centred(mulmod(mulmod(W[o][k], (1ull << (8 * b)) % q, q), R, q), q);
+  for (int a = 0; a < 4; ++a)
+    for (int lam = 0; lam < 64; ++lam)
+      for (int i = 0; i < 4; ++i) {
+        const int g = lam >> 4, r = lam & 15;
+        const int kin = KAP ? 4 * g + i : 4 * i + g;
+        const int jout = DA ? r : (KAP ? r : 4 * (r & 3) + (r >> 2));
+        uint32_t wd = 0;
+        for (int b = 0; b < 4; ++b) {
+          const uint32_t u = (uint32_t)E[jout][kin][b] + 0x80808080u;
+          wd |= ((((u >> (8 * a)) & 0xFFu) ^ 0x80u) & 0xFFu) << (8 * b);
+        }
+        out[(a * 64 + lam) * 4 + i] = (int32_t)wd;
+      }
+}
+
+}  // namespace
+
+// Builds the MFMA tables of every limb (u32 bases at N = 2^16) into t->mf.
+int mf_build(Tables* t, std::string* err) {
+  using namespace mf;
+  const size_t L = t->L;
+  const uint64_t n = kN;
+  std::vector<int32_t> all((size_t)L * kLimb * 4);
+  std::vector<uint64_t> tw(n), itw(n), pw(n), ipw(n);
+  for (size_t l = 0; l < L; ++l) {
+    const uint64_t q = t->moduli[l], psi = t->psi[l], psinv = invmod(psi, q);
+    uint64_t x = 1, y = 1;
+    for (uint64_t j = 0; j < n; ++j) {
+      pw[j] = x;
+      ipw[j] = y;
+      x = mulmod(x, psi, q);
+      y = mulmod(y, psinv, q);
+    }
+    for (uint64_t g = 0; g < n; ++g) {
+      tw[g] = pw[brv(g, 16)];
+      itw[g] = ipw[brv(g, 16)];
+    }
+    const uint64_t R = (uint64_t)(((host::u128)1 << 32) % q);
+    // pass 0's matrix by running its four CT stages on unit vectors
+    uint64_t M0[16][16];
+    for (int k = 0; k < 16; ++k) {
+      uint64_t v[16] = {};
+      v[k] = 1;
+      for (int sb = 3; sb >= 0; --sb) {
+        const int b = 12 + sb;
+        for (int kk = 0; kk < 16; ++kk) {
+          if (kk & (1 << sb)) continue;
+          const uint64_t i = (uint64_t)kk << 12;
+          const uint64_t w = tw[(n + i) >> (b + 1)];
+          const uint64_t x = v[kk], y = v[kk | (1 << sb)];
+          const uint64_t tt = mulmod(w, y, q);
+          v[kk] = (x + tt) % q;
+          v[kk | (1 << sb)] = (x + q - tt) % q;
+        }
+      }
+      for (int j = 0; j < 16; ++j) M0[j][k] = v[j];
+    }
+    const uint64_t beta1i = itw[8];
+    uint64_t F[16][16], Fi[16][16];
+    const uint64_t inv16 = invmod(16 % q, q);
+    for (int j = 0; j < 16; ++j)
+      for (int k = 0; k < 16; ++k) F[j][k] = mulmod(M0[j][k], powmod(beta1i, (uint64_t)k, q), q);
+    for (int j = 0; j < 16; ++j)
+      for (int k = 0; k < 16; ++k) Fi[k][j] = mulmod(inv16, invmod(F[j][k], q), q);
+    // F Fi == I (F is a DFT on the 16 roots of unity; checked, not assumed)
+    for (int j = 0; j < 16; ++j)
+      for (int k = 0; k < 16; ++k) {
+        uint64_t s = 0;
+        for (int x = 0; x < 16; ++x) s = (s + mulmod(F[j][x], Fi[x][k], q)) % q;
+        if (s != (j == k ? 1u : 0u)) {
+          *err = "MFMA tables: F is not invertible as a DFT";
+          return -1;
+        }
+      }
+    int32_t* lt = all.data() + l * (size_t)kLimb * 4;
+    auto slot = [&](int s) { return lt + (size_t)(kMat + s * 4 * 64) * 4; };
+    uint64_t W[16][16];
+    expand(M0, q, R, false, 0, slot(S_F1));
+    for (int U = 0; U < 16; ++U) {
+      const uint64_t be = tw[128 + 8 * U], bei = itw[128 + 8 * U];
+      for (int j = 0; j < 16; ++j)
+        for (int k = 0; k < 16; ++k) W[j][k] = mulmod(F[j][k], powmod(be, (uint64_t)k, q), q);
+      expand(W, q, R, false, 0, slot(S_F2 + U));
+      for (int k = 0; k < 16; ++k)
+        for (int j = 0; j < 16; ++j) W[k][j] = mulmod(powmod(bei, (uint64_t)k, q), Fi[k][j], q);
+      expand(W, q, R, false, 0, slot(S_I2 + U));
+    }
+    expand(F, q, R, true, 0, slot(S_F3));
+    expand(F, q, R, false, 1, slot(S_F4));
+    expand(Fi, q, R, true, 1, slot(S_I4));
+    expand(Fi, q, R, false, 1, slot(S_I3));
+    for (int k = 0; k < 16; ++k)
+      for (int j = 0; j < 16; ++j) W[k][j] = mulmod(powmod(beta1i, (uint64_t)k, q), Fi[k][j], q);
+    expand(W, q, R, false, 0, slot(S_I1));
+    for (int k = 0; k < 16; ++k)
+      for (int j = 0; j < 16; ++j) W[k][j] = mulmod(W[k][j], R, q);
+    expand(W, q, R, false, 0, slot(S_I1R));
+    // input-bias compensations: the data digits carry x - 2^30
+    const uint64_t bias = mulmod(R, (1ull << 30) % q, q);
+    {
+      int32_t cf[16], ci[16];
+      for (int j = 0; j < 16; ++j) {
+        uint64_t s0 = 0, s1 = 0;
+        for (int k = 0; k < 16; ++k) {
+          s0 = (s0 + M0[j][k]) % q;
+          s1 = (s1 + Fi[j][k]) % q;
+        }
+        cf[j] = centred(mulmod(bias, s0, q), q);
+        ci[j] = centred(mulmod(bias, s1, q), q);
+      }
+      int32_t* c1 = lt + (size_t)kCompF1 * 4;
+      int32_t* c4 = lt + (size_t)kCompI4 * 4;
+      for (int lam = 0; lam < 64; ++lam)
+        for (int i = 0; i < 4; ++i) {
+          c1[lam * 4 + i] = cf[4 * i + (lam >> 4)];
+          c4[lam * 4 + i] = ci[lam & 15];
+        }
+    }
+    // twists (Montgomery form, centred)
+    auto mr = [&](uint64_t v) { return centred(mulmod(v, R, q), q); };
+    int32_t* t3f = lt + (size_t)kTw3f * 4;
+    int32_t* t3i = lt + (size_t)kTw3i * 4;
+    for (int w = 0; w < 16; ++w)
+      for (int g = 0; g < 4; ++g)
+        for (int c = 0; c < 16; ++c)
+          for (int i = 0; i < 4; ++i) {
+            const int U3 = (w << 4) | (i << 2) | g;
+            t3f[((w * 4 + g) * 16 + c) * 4 + i] = mr(powmod(tw[2048 + 8 * U3], (uint64_t)c, q));
+          }
+    for (int w = 0; w < 16; ++w)
+      for (int c = 0; c < 16; ++c)
+        for (int g = 0; g < 4; ++g)
+          for (int i = 0; i < 4; ++i) {
+            const int U3 = (w << 4) | c;
+            t3i[((w * 16 + c) * 4 + g) * 4 + i] = mr(powmod(itw[2048 + 8 * U3], (uint64_t)(4 * g + i), q));
+          }
+    int32_t* t4f = lt + (size_t)kTw4f * 4;
+    int32_t* t4i = lt + (size_t)kTw4i * 4;
+    for (int w = 0; w < 16; ++w)
+      for (int c = 0; c < 16; ++c)
+        for (int lam = 0; lam < 64; ++lam)
+          for (int i = 0; i < 4; ++i) {
+            const int g = lam >> 4, nn = lam & 15;
+            const int Uf = (w << 8) | (c << 4) | nn;
+            t4f[((w * 16 + c) * 64 + lam) * 4 + i] = mr(powmod(tw[32768 + 8 * Uf], (uint64_t)(4 * g + i), q));
+            const int Ui = (w << 8) | (c << 4) | (4 * g + i);
+            t4i[((w * 16 + c) * 64 + lam) * 4 + i] = mr(powmod(itw[32768 + 8 * Ui], (uint64_t)nn, q));
+          }
+  }
+  const size_t bytes = all.size() * sizeof(int32_t);
+  if (hipMalloc(&t->mf, bytes) != hipSuccess) {
+    *err = "hipMalloc(MFMA tables)";
+    return -2;
+  }
+  if (hipMemcpy(t->mf, all.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    *err = "hipMemcpy(MFMA tables)";
+    return -2;
+  }
+  return 0;
+}
+
+bool mf_ok(const Tables* t) { return t->mf != nullptr && t->plane == 5; }
+
+hipError_t launch_mf_mul(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls) {
+  if (k.B == 0 || k.L == 0) return hipSuccess;
+  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  hipError_t e = hipFuncSetAttribute((const void*)k_mf_mul, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mf::kLdsBytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_mf_mul, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), mf::kLdsBytes, k.s, (uint32_t*)out,
+                     (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)scratch, (const void*)k.t->mf,
+                     (const LimbConst<uint32_t>*)k.t->lconst, ls);
+  return hipGetLastError();
+}
+
+template <bool INV, int STOP>
+static hipError_t launch_ntt_t(const Launch& k, void* data, uint64_t ls) {
+  hipError_t e = hipFuncSetAttribute((const void*)k_mf_ntt<INV, STOP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)mf::kLdsBytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_mf_ntt<INV, STOP>), dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), mf::kLdsBytes, k.s,
+                     (uint32_t*)data, (const void*)k.t->mf, (const LimbConst<uint32_t>*)k.t->lconst, ls);
+  return hipGetLastError();
+}
+
+// stop: 4 = the whole transform; 1..3 = the debug prefixes (forward only)
+hipError_t launch_mf_ntt(const Launch& k, int inverse, void* data, uint64_t ls, int stop) {
+  if (k.B == 0 || k.L == 0) return hipSuccess;
+  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  if (inverse) return launch_ntt_t<true, 4>(k, data, ls);
+  switch (stop) {
+    case 2: return launch_ntt_t<false, 2>(k, data, ls);
+    case 3: return launch_ntt_t<false, 3>(k, data, ls);
+    default: return launch_ntt_t<false, 4>(k, data, ls);
+  }
+}
+
+}  // namespace rnt
