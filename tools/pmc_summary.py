@@ -27,6 +27,11 @@ PLANE = {"k_plane_fwd": "plane_fwd", "k_plane_mul": "plane_mul", "k_plane_fused"
 
 
 def short(kname):
+    m = re.search(r"\bk_mf_ntt<(true|false), 4>", kname)
+    if m:
+        return "mf_ntt_inv" if m.group(1) == "true" else "mf_ntt_fwd"
+    if re.search(r"\bk_mf_mul\(", kname):
+        return "mf_mul"
     m = re.search(r"\bk_plane_ntt<(true|false)>", kname)
     if m:
         return "plane_ntt_inv" if m.group(1) == "true" else "plane_ntt_fwd"

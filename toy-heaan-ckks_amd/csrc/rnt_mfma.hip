@@ -63,6 +63,9 @@
 
 #include "rnt_internal.hpp"
 #include "rnt_hostmath.hpp"
+#include "rnt_modarith.hpp"
+#include "rnt_device.hpp"
+#include "rnt_bfly4.hpp"
 
 namespace rnt {
 namespace mf {
@@ -74,16 +77,23 @@ constexpr uint32_t K32 = 0x80808080u;
 
 // ---- per-limb table (v4i units): MFMA operands, compensations, twists ----
 // Matrix slot s, digit plane a, lane lam: operand bytes of that lane.
+// F1..I1: the standalone transforms (four MFMA passes); F3B, I3B, I1H: the
+// product's pass 2 with the data as B (P3 layout kept) and its inverse, and
+// the product's last inverse matrix (2^32 / 4: the Montgomery block products
+// and the two GS stages' factor 2 each).
 constexpr int S_F1 = 0, S_F2 = 1, S_F3 = 17, S_F4 = 18, S_I4 = 19, S_I3 = 20, S_I2 = 21, S_I1R = 37, S_I1 = 38;
-constexpr int kSlots = 39;
+constexpr int S_F3B = 39, S_I3B = 40, S_I1H = 41;
+constexpr int kSlots = 42;
 constexpr int kMat = 0;
 constexpr int kCompF1 = kSlots * 4 * 64;  // [lam]: digit-0 accumulator start of pass 0 (input bias)
 constexpr int kCompI4 = kCompF1 + 64;     // [lam]: the same for the standalone inverse's first pass
-constexpr int kTw3f = kCompI4 + 64;       // [w][g][c], element i: pass 2 twist, P2 positions
+constexpr int kCompI3 = kCompI4 + 64;     // [lam]: the same for the product's inverse pass 2 (S_I3B)
+constexpr int kTw3f = kCompI3 + 64;       // [w][g][c], element i: pass 2 twist, P2 positions
 constexpr int kTw4f = kTw3f + 1024;       // [w][c][lam]: pass 3 twist, P4 positions
 constexpr int kTw4i = kTw4f + 16384;      // [w][c][lam]: inverse pass 3 twist, Q3 positions
 constexpr int kTw3i = kTw4i + 16384;      // [w][c][g]: inverse pass 2 twist, Q3 positions
-constexpr int kLimb = kTw3i + 1024;
+constexpr int kTw3iB = kTw3i + 1024;      // [w][c][g]: inverse pass 2 twist, P3 positions (product)
+constexpr int kLimb = kTw3iB + 1024;
 
 // Registers of a P3 / P4 / Q3 chunk (c, i) after the P2 -> P3 swap, as
 // physical slots of the P2 numbering 4c + i (see the header).
@@ -161,6 +171,12 @@ __device__ __forceinline__ void tile_fence() {
   __builtin_amdgcn_sched_barrier(0);
 #endif
 }
+// Pins a tile's four outputs as computed at this point: IR-level code motion
+// (sched_barrier orders only the machine scheduler) would otherwise sink the
+// reductions to the words' next use and keep their partial sums live.
+__device__ __forceinline__ void pin4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  asm volatile("" ::"v"(a), "v"(b), "v"(c), "v"(d));
+}
 __device__ __forceinline__ uint32_t pk_canon(uint32_t x) { return (x + 0x40808080u) ^ K32; }  // x - 2^30, packed
 __device__ __forceinline__ uint32_t canon(int32_t r, int32_t q) { return (uint32_t)(r + ((r >> 31) & q)); }
 
@@ -213,6 +229,24 @@ __device__ __forceinline__ void p2_bases(uint32_t (&rb)[4], const Th& h) {
 __host__ __device__ constexpr uint32_t p1_off(int c, int i) { return 32u * ((c >> 2) & 1) + 64u * (i & 1) + 128u * (i >> 1); }
 __host__ __device__ constexpr uint32_t p2_off(int c, int i) { return 32u * (i & 1) + 512u * (i >> 1) + 256u * ((c >> 2) & 1); }
 
+// LDS reads with the register part of the address as the instruction
+// offset: left to itself hipcc pairs them into ds_read2_b32, whose 8-bit
+// offsets cannot hold it, and keeps one address VGPR per pair (spilled).
+// The reads are asm, so hipcc does not count them: lds_wait() (every
+// destination named as read-write) ends each group before its first use.
+template <uint32_t OFF>
+__device__ __forceinline__ uint32_t lds_rd(uint32_t addr) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+template <int B0>
+__device__ __forceinline__ void lds_wait8(uint32_t (&x)[64]) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(x[B0 + 0]), "+v"(x[B0 + 1]), "+v"(x[B0 + 2]), "+v"(x[B0 + 3]), "+v"(x[B0 + 4]),
+                 "+v"(x[B0 + 5]), "+v"(x[B0 + 6]), "+v"(x[B0 + 7]));
+}
+
 // Round H of P1 -> P2: P1 chunks 8H .. 8H+7 out, P2 chunks 8H .. 8H+7 in.
 template <int H>
 __device__ __forceinline__ void x_write_p1(const uint32_t (&x1)[64], uint32_t* lds, const uint32_t (&wb)[4]) {
@@ -221,27 +255,53 @@ __device__ __forceinline__ void x_write_p1(const uint32_t (&x1)[64], uint32_t* l
 #pragma unroll
     for (int i = 0; i < 4; ++i) lds[wb[c & 3] + p1_off(c, i)] = x1[4 * c + i];
 }
+template <int H, int C, int I>
+__device__ __forceinline__ void x_read_p2_one(uint32_t (&x2)[64], uint32_t lds0, const uint32_t (&rb)[4]) {
+  x2[4 * C + I] = lds_rd<p2_off(C, I) * 4u>(lds0 + rb[C & 3] * 4u);
+}
 template <int H>
 __device__ __forceinline__ void x_read_p2(uint32_t (&x2)[64], const uint32_t* lds, const uint32_t (&rb)[4]) {
-#pragma unroll
-  for (int c = 8 * H; c < 8 * H + 8; ++c)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x2[4 * c + i] = lds[rb[c & 3] + p2_off(c, i)];
+  const uint32_t l0 = (uint32_t)(uintptr_t)lds;
+#define RNT_MF_RD(C)                      \
+  x_read_p2_one<H, C, 0>(x2, l0, rb);     \
+  x_read_p2_one<H, C, 1>(x2, l0, rb);     \
+  x_read_p2_one<H, C, 2>(x2, l0, rb);     \
+  x_read_p2_one<H, C, 3>(x2, l0, rb);
+  RNT_MF_RD(8 * H + 0) RNT_MF_RD(8 * H + 1) RNT_MF_RD(8 * H + 2) RNT_MF_RD(8 * H + 3)
+  RNT_MF_RD(8 * H + 4) RNT_MF_RD(8 * H + 5) RNT_MF_RD(8 * H + 6) RNT_MF_RD(8 * H + 7)
+#undef RNT_MF_RD
+  lds_wait8<32 * H + 0>(x2);
+  lds_wait8<32 * H + 8>(x2);
+  lds_wait8<32 * H + 16>(x2);
+  lds_wait8<32 * H + 24>(x2);
 }
 // the inverse direction: P2 words at q2(c, i) out, P1 words in
-template <int H>
+template <int H, bool Q2 = true>
 __device__ __forceinline__ void x_write_p2(const uint32_t (&x2)[64], uint32_t* lds, const uint32_t (&rb)[4]) {
 #pragma unroll
   for (int c = 8 * H; c < 8 * H + 8; ++c)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) lds[rb[c & 3] + p2_off(c, i)] = x2[q2(c, i)];
+    for (int i = 0; i < 4; ++i) lds[rb[c & 3] + p2_off(c, i)] = x2[(Q2 ? q2(c, i) : 4 * c + i)];
+}
+template <int H, int C, int I>
+__device__ __forceinline__ void x_read_p1_one(uint32_t (&x1)[64], uint32_t lds0, const uint32_t (&wb)[4]) {
+  x1[4 * C + I] = lds_rd<p1_off(C, I) * 4u>(lds0 + wb[C & 3] * 4u);
 }
 template <int H>
 __device__ __forceinline__ void x_read_p1(uint32_t (&x1)[64], const uint32_t* lds, const uint32_t (&wb)[4]) {
-#pragma unroll
-  for (int c = 8 * H; c < 8 * H + 8; ++c)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x1[4 * c + i] = lds[wb[c & 3] + p1_off(c, i)];
+  const uint32_t l0 = (uint32_t)(uintptr_t)lds;
+#define RNT_MF_RD(C)                      \
+  x_read_p1_one<H, C, 0>(x1, l0, wb);     \
+  x_read_p1_one<H, C, 1>(x1, l0, wb);     \
+  x_read_p1_one<H, C, 2>(x1, l0, wb);     \
+  x_read_p1_one<H, C, 3>(x1, l0, wb);
+  RNT_MF_RD(8 * H + 0) RNT_MF_RD(8 * H + 1) RNT_MF_RD(8 * H + 2) RNT_MF_RD(8 * H + 3)
+  RNT_MF_RD(8 * H + 4) RNT_MF_RD(8 * H + 5) RNT_MF_RD(8 * H + 6) RNT_MF_RD(8 * H + 7)
+#undef RNT_MF_RD
+  lds_wait8<32 * H + 0>(x1);
+  lds_wait8<32 * H + 8>(x1);
+  lds_wait8<32 * H + 16>(x1);
+  lds_wait8<32 * H + 24>(x1);
 }
 
 // Lane bits 5, 4 <-> the register bits of chunk bits 1, 0: P2 -> P3.
@@ -306,6 +366,7 @@ __device__ __forceinline__ void pass_p1(uint32_t (&x1)[64], const v4i (&M)[4], v
     tile<false>(D, M, b, BIAS ? comp : z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) x1[4 * c + i] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
+    pin4(x1[4 * c + 0], x1[4 * c + 1], x1[4 * c + 2], x1[4 * c + 3]);
     tile_fence();
   }
 }
@@ -328,6 +389,7 @@ __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], R
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
       x2[4 * c + i] = DBG_NOTW ? (uint32_t)(r + (int32_t)K32) ^ K32 : (uint32_t)mont<true>(r, tv[i], m) ^ K32;
     }
+    pin4(x2[4 * c + 0], x2[4 * c + 1], x2[4 * c + 2], x2[4 * c + 3]);
     tile_fence();
   }
 }
@@ -349,6 +411,7 @@ __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rs
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
       x[p3(c, i)] = DBG_NOTW ? (uint32_t)(r + (int32_t)K32) ^ K32 : (uint32_t)mont<true>(r, tv[i], m) ^ K32;
     }
+    pin4(x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
     tile_fence();
   }
 }
@@ -388,6 +451,7 @@ __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
       x[p3(c, i)] = (uint32_t)mont<true>(r, tv[i], m) ^ K32;
     }
+    pin4(x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
     tile_fence();
   }
 }
@@ -408,22 +472,29 @@ __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], R
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
       x[p3(c, i)] = (uint32_t)mont<true>(r, tv[i], m) ^ K32;
     }
+    pin4(x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
     tile_fence();
   }
 }
 // inverse pass 1 (per-wave matrix) on P2 chunks [C0, C0 + 8) at q2 slots; packed output.
-template <int C0>
+// P2 register of chunk (c, i): after the inverse's Q3 -> P2 swap (Q2) or
+// after a swap back from P3 (the product)
+template <bool Q2>
+__host__ __device__ constexpr int p2r(int c, int i) { return Q2 ? q2(c, i) : 4 * c + i; }
+template <int C0, bool Q2 = true>
 __device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], const Mc& m) {
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = C0; c < C0 + 8; ++c) {
     v4i b;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) b[i] = (int)x[q2(c, i)];
+    for (int i = 0; i < 4; ++i) b[i] = (int)x[p2r<Q2>(c, i)];
     v4i D[4];
     tile<false>(D, M, b, z);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) x[q2(c, i)] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
+    for (int i = 0; i < 4; ++i)
+      x[p2r<Q2>(c, i)] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
+    pin4(x[p2r<Q2>(c, 0)], x[p2r<Q2>(c, 1)], x[p2r<Q2>(c, 2)], x[p2r<Q2>(c, 3)]);
     tile_fence();
   }
 }
@@ -440,6 +511,7 @@ __device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], 
     tile<false>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) x1[4 * c + i] = canon(recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m), m.q);
+    pin4(x1[4 * c + 0], x1[4 * c + 1], x1[4 * c + 2], x1[4 * c + 3]);
     tile_fence();
   }
 }
@@ -584,38 +656,278 @@ __device__ __forceinline__ void inv(uint32_t (&x2)[64], Rsrc dst, uint32_t* lds,
   store_p1(x1, dst, h);
 }
 
-constexpr size_t kLdsBytes = (size_t)(1u << 15) * 4;  // one exchange round
+// ---- the product: MFMA passes 0-2 (index bits 15..4), then the truncated
+// tail as in rnt_plane.hip (CT stages at bits 3, 2; degree-3 block products
+// mod X^4 - zeta; GS stages back) -------------------------------------------
+// P5 layout (the tail): registers y[16 i + d] hold index bits 7,6 (i) and
+// 3..0 (d); lanes: g = (5,4), lane bits 3..0 = index bits 11..8; w = 15..12.
+constexpr int kXS = 17;                         // transpose buffer row stride (words)
+constexpr int kXW = 64 * kXS;                   // one wave's transpose buffer
+constexpr int kTrWords = 16 * 2 * kXW;          // two per wave
+constexpr size_t kLdsBytes = (size_t)((1u << 15) > (uint32_t)kTrWords ? (1u << 15) : (uint32_t)kTrWords) * 4;
+
+// pass 2 with the data as B (P3 layout in place), canonical output for the tail.
+__device__ __forceinline__ void pass_p3b(uint32_t (&x)[64], const v4i (&M)[4], const Mc& m) {
+  const v4i z = {0, 0, 0, 0};
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    v4i b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = (int)x[p3(c, i)];
+    v4i D[4];
+    tile<false>(D, M, b, z);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[p3(c, i)] = canon(recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m), m.q);
+    pin4(x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
+    tile_fence();
+  }
+}
+// inverse pass 2 (F^-1, data as B in the P3 layout): canonical input (biased,
+// comp undoes it), output twisted and packed.
+__device__ __forceinline__ void ipass_p3b(uint32_t (&x)[64], const v4i (&M)[4], v4i comp, Rsrc tab, uint32_t tvo,
+                                          uint32_t tso, const Mc& m) {
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    v4i b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b[i] = (int)pk_canon(x[p3(c, i)]);
+    const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 64u);
+    v4i D[4];
+    tile<false>(D, M, b, comp);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
+      x[p3(c, i)] = (uint32_t)mont<true>(r, tv[i], m) ^ K32;
+    }
+    pin4(x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
+    tile_fence();
+  }
+}
+
+// P3 <-> P5: per register i and lane group g a 16 x 16 transpose of lane
+// bits 3..0 (index bits 3..0 in P3, 11..8 in P5) and chunk bits (11..8 in
+// P3, 3..0 in P5) through the wave's own LDS buffers (4 rounds, 2 buffers;
+// rows of 17 words: conflict-free both ways).  No workgroup barrier: a wave
+// reads only what it wrote (its LDS instructions execute in order).
+template <bool TO_P5>
+__device__ __forceinline__ void tr_p3p5(uint32_t (&x)[64], uint32_t (&y)[64], uint32_t* lds, const Th& h) {
+  uint32_t* base = lds + h.w * (2 * kXW);
+  const uint32_t rowa = h.lam * kXS;                           // + c
+  const uint32_t rowb = (h.g * 16u) * kXS + h.n;               // + d * kXS
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t* buf = base + (i & 1) * kXW;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      if constexpr (TO_P5)
+        buf[rowa + c] = x[p3(c, i)];
+      else
+        buf[rowb + c * kXS] = y[16 * i + c];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      if constexpr (TO_P5)
+        y[16 * i + c] = buf[rowb + c * kXS];
+      else
+        x[p3(c, i)] = buf[rowa + c];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Twiddle pairs {w, w'} of the limb's table by heap node (8-byte loads).
+__device__ __forceinline__ Tw<uint32_t> twl(Rsrc t, uint32_t node) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(t, node * 8u, 0, 0);
+  return Tw<uint32_t>{(uint32_t)v[0], (uint32_t)v[1]};
+}
+
+// Four CT butterflies (y[A + k], y[A + k + D]), k = 0..3, one twiddle, as
+// interleaved asm (rnt_bfly4.hpp: no s_nop hazard pads); LAZY: outputs in
+// [0, 2q] (both only multiplied next).
+template <int A, int D, bool LAZY>
+__device__ __forceinline__ void ct4(uint32_t (&y)[64], Tw<uint32_t> t, const Mod<uint32_t>& mo) {
+  const uint32_t w[4] = {t.w, t.w, t.w, t.w}, wp[4] = {t.p, t.p, t.p, t.p};
+  uint64_t P[4];
+  b4::shoup_prod4<false>(P, y[A + D], y[A + D + 1], y[A + D + 2], y[A + D + 3], w, wp, mo.nq);
+  uint32_t pl[4] = {(uint32_t)P[0], (uint32_t)P[1], (uint32_t)P[2], (uint32_t)P[3]};
+  if constexpr (LAZY)
+    b4::ct_reduce4_lazy(y[A], y[A + 1], y[A + 2], y[A + 3], y[A + D], y[A + D + 1], y[A + D + 2], y[A + D + 3], pl,
+                        mo.q);
+  else
+    b4::ct_reduce4(y[A], y[A + 1], y[A + 2], y[A + 3], y[A + D], y[A + D + 1], y[A + D + 2], y[A + D + 3], pl, mo.q);
+}
+template <int A, int D>
+__device__ __forceinline__ void gs4(uint32_t (&y)[64], Tw<uint32_t> t, const Mod<uint32_t>& mo) {
+  const uint32_t w[4] = {t.w, t.w, t.w, t.w}, wp[4] = {t.p, t.p, t.p, t.p};
+  uint32_t dd[4];
+  b4::gs_pre4(y[A], y[A + 1], y[A + 2], y[A + 3], y[A + D], y[A + D + 1], y[A + D + 2], y[A + D + 3], dd, mo.q);
+  uint64_t P[4];
+  b4::shoup_prod4<false>(P, dd[0], dd[1], dd[2], dd[3], w, wp, mo.nq);
+  const uint32_t pl[4] = {(uint32_t)P[0], (uint32_t)P[1], (uint32_t)P[2], (uint32_t)P[3]};
+  b4::csub4(y[A + D], y[A + D + 1], y[A + D + 2], y[A + D + 3], pl, mo.q);
+}
+
+// CT stages at index bits 3 and 2 in P5 (hi4 = index >> 4 without the i bits).
+// Bit 3's butterflies with bit 2 set only feed bit 2's multiplicands (lazy).
+template <int I>
+__device__ __forceinline__ void tail_ct_i(uint32_t (&y)[64], Rsrc tw, uint32_t hi4, const Mod<uint32_t>& mo) {
+  const uint32_t h6 = hi4 | ((uint32_t)I << 2);
+  const Tw<uint32_t> t3 = twl(tw, (kN >> 4) + h6);
+  const Tw<uint32_t> t20 = twl(tw, (kN >> 3) + (h6 << 1)), t21 = twl(tw, (kN >> 3) + (h6 << 1) + 1);
+  ct4<16 * I, 8, false>(y, t3, mo);
+  ct4<16 * I + 4, 8, true>(y, t3, mo);
+  ct4<16 * I, 4, false>(y, t20, mo);
+  ct4<16 * I + 8, 4, false>(y, t21, mo);
+}
+__device__ __forceinline__ void tail_ct(uint32_t (&y)[64], Rsrc tw, uint32_t hi4, const Mod<uint32_t>& mo) {
+  tail_ct_i<0>(y, tw, hi4, mo);
+  tail_ct_i<1>(y, tw, hi4, mo);
+  tail_ct_i<2>(y, tw, hi4, mo);
+  tail_ct_i<3>(y, tw, hi4, mo);
+}
+// GS stages at index bits 2 and 3 (the inverse of tail_ct times 4).
+template <int I>
+__device__ __forceinline__ void tail_gs_i(uint32_t (&y)[64], Rsrc itw, uint32_t hi4, const Mod<uint32_t>& mo) {
+  const uint32_t h6 = hi4 | ((uint32_t)I << 2);
+  const Tw<uint32_t> t20 = twl(itw, (kN >> 3) + (h6 << 1)), t21 = twl(itw, (kN >> 3) + (h6 << 1) + 1);
+  const Tw<uint32_t> t3 = twl(itw, (kN >> 4) + h6);
+  gs4<16 * I, 4>(y, t20, mo);
+  gs4<16 * I + 8, 4>(y, t21, mo);
+  gs4<16 * I, 8>(y, t3, mo);
+  gs4<16 * I + 4, 8>(y, t3, mo);
+}
+__device__ __forceinline__ void tail_gs(uint32_t (&y)[64], Rsrc itw, uint32_t hi4, const Mod<uint32_t>& mo) {
+  tail_gs_i<0>(y, itw, hi4, mo);
+  tail_gs_i<1>(y, itw, hi4, mo);
+  tail_gs_i<2>(y, itw, hi4, mo);
+  tail_gs_i<3>(y, itw, hi4, mo);
+}
+
+// The product's forward transform (14 stages): canonical plane at src -> y
+// (P5 layout, canonical, blocks of 4 words at y[16 i + 4 bb ..]).
+template <bool SYNC1>
+__device__ __forceinline__ void fwd_h(uint32_t (&y)[64], Rsrc src, uint32_t* lds, const Th& h, const Tabs& T,
+                                      Rsrc tw, uint32_t hi4, const Mod<uint32_t>& mo) {
+  uint32_t x[64];
+  {
+    uint32_t x1[64];
+    load_p1(x1, src, h);
+    const Mc& m = T.m;
+    const uint32_t lo = h.lam * 16u;
+    v4i M[4];
+    load_mat(M, T.tab, S_F1, lo);
+    const v4i comp = bld(T.tab, lo, (uint32_t)kCompF1 * 16u);
+    pass_p1<0, true>(x1, M, comp, m);
+    if constexpr (SYNC1) __syncthreads();
+    uint32_t wb[4], rb[4];
+    p1_bases(wb, h);
+    x_write_p1<0>(x1, lds, wb);
+    pass_p1<8, true>(x1, M, comp, m);
+    __syncthreads();
+    p2_bases(rb, h);
+    x_read_p2<0>(x, lds, rb);
+    __syncthreads();
+    p1_bases(wb, h);
+    x_write_p1<1>(x1, lds, wb);
+    load_mat(M, T.tab, S_F2 + h.w, lo);
+    const uint32_t t3v = h.g * 256u, t3s = (uint32_t)(kTw3f + h.w * 64) * 16u;
+    pass_p2<0>(x, M, T.tab, t3v, t3s, m);
+    __syncthreads();
+    p2_bases(rb, h);
+    x_read_p2<1>(x, lds, rb);
+    pass_p2<8>(x, M, T.tab, t3v, t3s, m);
+    swap_p2p3(x);
+    load_mat(M, T.tab, S_F3B, lo);
+    pass_p3b(x, M, m);
+  }
+  __syncthreads();  // the transpose buffers overlap the exchange region other waves may still read
+  tr_p3p5<true>(x, y, lds, h);
+  tail_ct(y, tw, hi4, mo);
+}
+
+// The product's inverse from y (P5, the block products' Montgomery outputs)
+// to the canonical plane at dst.
+__device__ __forceinline__ void inv_h(uint32_t (&y)[64], Rsrc dst, uint32_t* lds, const Th& h, const Tabs& T, Rsrc itw,
+                                      uint32_t hi4, const Mod<uint32_t>& mo) {
+  tail_gs(y, itw, hi4, mo);
+  uint32_t x[64];
+  tr_p3p5<false>(x, y, lds, h);
+  const Mc& m = T.m;
+  const uint32_t lo = h.lam * 16u;
+  v4i M[4];
+  load_mat(M, T.tab, S_I3B, lo);
+  ipass_p3b(x, M, bld(T.tab, lo, (uint32_t)kCompI3 * 16u), T.tab, h.g * 16u, (uint32_t)(kTw3iB + h.w * 64) * 16u, m);
+  swap_p2p3(x);  // back to P2 (the swap is its own inverse)
+  load_mat(M, T.tab, S_I2 + h.w, lo);
+  uint32_t wb[4], rb[4];
+  uint32_t x1[64];
+  ipass_p2<0, false>(x, M, m);
+  __syncthreads();  // other waves may still use the LDS (their transposes)
+  p2_bases(rb, h);
+  x_write_p2<0, false>(x, lds, rb);
+  ipass_p2<8, false>(x, M, m);
+  __syncthreads();
+  p1_bases(wb, h);
+  x_read_p1<0>(x1, lds, wb);
+  __syncthreads();
+  p2_bases(rb, h);
+  x_write_p2<1, false>(x, lds, rb);
+  load_mat(M, T.tab, S_I1H, lo);
+  ipass_p1<0>(x1, M, m);
+  __syncthreads();
+  p1_bases(wb, h);
+  x_read_p1<1>(x1, lds, wb);
+  ipass_p1<8>(x1, M, m);
+  store_p1(x1, dst, h);
+}
 
 }  // namespace mf
 
 // One workgroup per (poly, limb) plane pair, grid (B, L): c = a * b.
-// a^ goes to a scratch plane (this thread's words, 16 B per chunk) and
-// comes back for the pointwise product.
+// a^ (P5 layout, this thread's 16 blocks of 4 words) goes to a scratch plane
+// and comes back for the degree-3 block products (as rnt_plane.hip's).
 __global__ void __launch_bounds__(mf::kT, 1)
 k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
-         const void* __restrict__ mft, const LimbConst<uint32_t>* __restrict__ lcs, uint64_t ls) {
+         const void* __restrict__ mft, TabPtrs<uint32_t> tp, uint64_t ls) {
   using namespace mf;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   uint32_t* lds = (uint32_t*)smem_raw;
   const Th h(threadIdx.x);
   const uint32_t poly = blockIdx.x, l = blockIdx.y;
   const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * kN;
-  const Tabs T = tabs_of(mft, lcs[l], l);
+  const LimbConst<uint32_t> lc = tp.lc[l];
+  const Tabs T = tabs_of(mft, lc, l);
+  const Mod<uint32_t> mo = mod_of(lc);
   constexpr uint32_t PB = kN * 4u;
-  uint32_t x[64];
+  const Rsrc tw = rsrc(tp.tw + (uint64_t)l * kN, kN * 8u), itw = rsrc(tp.itw + (uint64_t)l * kN, kN * 8u);
+  const uint32_t hi4 = (h.w << 8) | (h.n << 4) | h.g;  // index >> 4 in P5, without the i bits
+  uint32_t y[64];
+  fwd_h<false>(y, rsrc(a + off, PB), lds, h, T, tw, hi4, mo);
   const Rsrc ah = rsrc(scratch + off, PB);
   const uint32_t ao = h.t * 16u;
-  // a^: each tile of the last pass straight to the scratch plane
-  fwd<false>(x, rsrc(a + off, PB), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
-    bst(v4i{r[0], r[1], r[2], r[3]}, ah, ao, (uint32_t)cc * (kT * 16u));
-  });
-  // b^: each tile of the last pass times a^ (Montgomery), packed for the inverse
-  fwd<true>(x, rsrc(b + off, PB), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
-    const v4i v = bld(ah, ao, (uint32_t)cc * (kT * 16u));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) xx[p3(cc, i)] = (uint32_t)mont<true>(v[i], r[i], T.m) ^ K32;
-  });
-  inv<false>(x, rsrc(c + off, PB), lds, h, T, S_I1R);
+  for (int kk = 0; kk < 16; ++kk)
+    bst(v4i{(int)y[16 * (kk >> 2) + 4 * (kk & 3)], (int)y[16 * (kk >> 2) + 4 * (kk & 3) + 1],
+            (int)y[16 * (kk >> 2) + 4 * (kk & 3) + 2], (int)y[16 * (kk >> 2) + 4 * (kk & 3) + 3]},
+        ah, ao, (uint32_t)kk * (kT * 16u));
+  fwd_h<true>(y, rsrc(b + off, PB), lds, h, T, tw, hi4, mo);
+  // degree-3 block products: block (i, bb) of this thread is block index
+  // ((hi4 | i << 2) << 2) | bb, zeta = (-1)^bb psi_rev[N/8 + index / 2]
+#pragma unroll
+  for (int kk = 0; kk < 16; ++kk) {
+    const int i = kk >> 2, bb = kk & 3;
+    const v4i av = bld(ah, ao, (uint32_t)kk * (kT * 16u));
+    const Tw<uint32_t> z = twl(tw, (kN >> 3) + (((hi4 | ((uint32_t)i << 2)) << 1) | (uint32_t)(bb >> 1)));
+    const uint32_t zeta = (bb & 1) ? lc.q - z.w : z.w, zeta_p = (bb & 1) ? ~z.p : z.p;
+    const uint32_t aa[4] = {(uint32_t)av[0], (uint32_t)av[1], (uint32_t)av[2], (uint32_t)av[3]};
+    const uint32_t bv[4] = {y[16 * i + 4 * bb], y[16 * i + 4 * bb + 1], y[16 * i + 4 * bb + 2], y[16 * i + 4 * bb + 3]};
+    uint32_t cc[4];
+    mul_mod_x4(cc, aa, bv, zeta, zeta_p, lc.q, lc.qinv);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[16 * i + 4 * bb + e] = cc[e];
+  }
+  inv_h(y, rsrc(c + off, PB), lds, h, T, itw, hi4, mo);
 }
 
 // Standalone transforms in place (rnt_ntt_fwd / rnt_ntt_inv at N = 2^16).
@@ -794,9 +1106,16 @@ int mf_build(Tables* t, std::string* err) {
     for (int k = 0; k < 16; ++k)
       for (int j = 0; j < 16; ++j) W[k][j] = mulmod(powmod(beta1i, (uint64_t)k, q), Fi[k][j], q);
     expand(W, q, R, false, 0, slot(S_I1));
+    uint64_t Wh[16][16];
+    const uint64_t quarter_r = mulmod(R, invmod(4 % q, q), q);
+    for (int k = 0; k < 16; ++k)
+      for (int j = 0; j < 16; ++j) Wh[k][j] = mulmod(W[k][j], quarter_r, q);
+    expand(Wh, q, R, false, 0, slot(S_I1H));
     for (int k = 0; k < 16; ++k)
       for (int j = 0; j < 16; ++j) W[k][j] = mulmod(W[k][j], R, q);
     expand(W, q, R, false, 0, slot(S_I1R));
+    expand(F, q, R, false, 0, slot(S_F3B));
+    expand(Fi, q, R, false, 0, slot(S_I3B));
     // input-bias compensations: the data digits carry x - 2^30
     const uint64_t bias = mulmod(R, (1ull << 30) % q, q);
     {
@@ -812,10 +1131,12 @@ int mf_build(Tables* t, std::string* err) {
       }
       int32_t* c1 = lt + (size_t)kCompF1 * 4;
       int32_t* c4 = lt + (size_t)kCompI4 * 4;
+      int32_t* c3 = lt + (size_t)kCompI3 * 4;
       for (int lam = 0; lam < 64; ++lam)
         for (int i = 0; i < 4; ++i) {
           c1[lam * 4 + i] = cf[4 * i + (lam >> 4)];
           c4[lam * 4 + i] = ci[lam & 15];
+          c3[lam * 4 + i] = ci[4 * i + (lam >> 4)];  // F^-1 as the A operand (S_I3B, kappa 4i + g)
         }
     }
     // twists (Montgomery form, centred)
@@ -835,6 +1156,14 @@ int mf_build(Tables* t, std::string* err) {
           for (int i = 0; i < 4; ++i) {
             const int U3 = (w << 4) | c;
             t3i[((w * 16 + c) * 4 + g) * 4 + i] = mr(powmod(itw[2048 + 8 * U3], (uint64_t)(4 * g + i), q));
+          }
+    int32_t* t3b = lt + (size_t)kTw3iB * 4;
+    for (int w = 0; w < 16; ++w)
+      for (int c = 0; c < 16; ++c)
+        for (int g = 0; g < 4; ++g)
+          for (int i = 0; i < 4; ++i) {
+            const int U3 = (w << 4) | c;  // P3 positions: k = bits 7..4 = 4i + g
+            t3b[((w * 16 + c) * 4 + g) * 4 + i] = mr(powmod(itw[2048 + 8 * U3], (uint64_t)(4 * i + g), q));
           }
     int32_t* t4f = lt + (size_t)kTw4f * 4;
     int32_t* t4i = lt + (size_t)kTw4i * 4;
@@ -870,7 +1199,7 @@ hipError_t launch_mf_mul(const Launch& k, void* out, const void* a, const void* 
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_mf_mul, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), mf::kLdsBytes, k.s, (uint32_t*)out,
                      (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)scratch, (const void*)k.t->mf,
-                     (const LimbConst<uint32_t>*)k.t->lconst, ls);
+                     tab_ptrs<uint32_t>(k.t), ls);
   return hipGetLastError();
 }
 
