@@ -127,14 +127,12 @@ def test_metric_path_edge_operands(gpu, monkeypatch, plane):
     assert np.array_equal(t.channels(), a.channels())
 
 
-@pytest.mark.parametrize("mode", ["1", "3", "4"])
-def test_plane_product_matches_oracle(gpu, monkeypatch, mode):
-    """rnt_mul through the whole-plane kernels (k_plane_fwd + k_plane_mul,
-    N = 2^16, u32 canonical bases; RNT_PLANE=1 two launches, RNT_PLANE=3
-    both halves in one workgroup, RNT_PLANE=4 its persistent form), bit-exact against
-    the oracle's poly.rs:307-329 product on random, all-(q-1), zero and
-    negacyclic-monomial operands, and in both in-place forms."""
-    monkeypatch.setenv("RNT_PLANE", mode)
+def test_plane_product_matches_oracle(gpu, monkeypatch):
+    """rnt_mul through the whole-plane kernel (k_plane_fused, the default at
+    N = 2^16 on u32 bases), bit-exact against the oracle's poly.rs:307-329
+    product on random, all-(q-1), zero and negacyclic-monomial operands, and
+    in both in-place forms."""
+    monkeypatch.delenv("RNT_PLANE", raising=False)
     rn = gpu
     n, L = 1 << 16, 3
     mod = rn.generate_primes(31, L, n)
@@ -162,15 +160,14 @@ def test_plane_product_matches_oracle(gpu, monkeypatch, mode):
     assert np.array_equal(b2.channels(), got)
 
 
-@pytest.mark.parametrize("plane", [None, "0", "4"])
+@pytest.mark.parametrize("plane", [None, "0"])
 def test_metric_batch_1024_sampled_pairs(gpu, monkeypatch, plane):
     """The metric's own shape and batch (N = 2^16, L = 16 x 31-bit, 1024
     pairs, operands drawn on the device as in bench.py): eight pairs --
     the first, the last, both sides of the 512 midpoint and four random
     ones -- bit-exact against the oracle's poly.rs:307-329 product, and the
     same batch through the in-place form (a *= b, out aliasing a); default
-    path, the four-step kernels (RNT_PLANE=0) and the persistent plane
-    kernel (RNT_PLANE=4: one workgroup per CU walking all 16384 planes)."""
+    path (k_plane_fused) and the four-step kernels (RNT_PLANE=0)."""
     if plane is not None:
         monkeypatch.setenv("RNT_PLANE", plane)
     rn = gpu

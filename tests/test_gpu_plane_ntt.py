@@ -1,7 +1,8 @@
-"""The default N = 2^16 transform path (k_plane_ntt: rnt_ntt_fwd / rnt_ntt_inv
-and every NTT-domain op that runs through them) against the oracle on random
-operands, at the metric's ring (N = 2^16, L = 16 x 31-bit), in the default
-mode (whole-plane kernels) and with RNT_PLANE=0 (four-step kernels).
+"""The default N = 2^16 transform path (k_mf_ntt, the MFMA whole-plane
+transforms: rnt_ntt_fwd / rnt_ntt_inv and every NTT-domain op that runs
+through them) against the oracle on random operands, at the metric's ring
+(N = 2^16, L = 16 x 31-bit), in the default mode and with RNT_PLANE=0
+(four-step kernels).
 
 Reference: to_ntt_domain / to_coeff_domain (poly.rs:136-166), the
 NTT-domain MulAssign branch (poly.rs:297-306), rescale_into from the NTT

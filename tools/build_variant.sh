@@ -12,8 +12,8 @@ mkdir -p $V
 HF="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$C"
 OBJS_REST="$L/rnt_encode.o $L/rnt_sample.o $L/rnt_api.o"
 if [ "${MF_ONLY:-0}" = "1" ]; then
-  # only rnt_mfma.hip with the flags, the rest as built
-  /opt/rocm/bin/hipcc $HF "$@" -c $C/rnt_mfma.hip -o $V/m_$NAME.o
+  # only rnt_mfma.hip with the flags (KSRC=<file>: another version of it), the rest as built
+  /opt/rocm/bin/hipcc $HF "$@" -c ${KSRC:-$C/rnt_mfma.hip} -o $V/m_$NAME.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $L/rnt_kernels.o $L/rnt_plane.o $V/m_$NAME.o $OBJS_REST -o $V/librnsntt_$NAME.so
   echo $V/librnsntt_$NAME.so
   exit 0

@@ -1,7 +1,7 @@
 """Phase timeline of the whole-plane kernels (measurement build).
 
   bash tools/build_variant.sh trace -DRNT_PLANE_TRACE
-  RNSNTT_LIB=toy-heaan-ckks_amd/lib/variants/librnsntt_trace.so RNT_PLANE=1 \
+  RNSNTT_LIB=toy-heaan-ckks_amd/lib/variants/librnsntt_trace.so \
       python tools/plane_trace.py [batch]
 
 Runs the metric's poly-mul (N = 2^16, L = 16, 31-bit) a few times and prints,

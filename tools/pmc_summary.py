@@ -23,21 +23,12 @@ FN = {"k_colt_fwd": "col_fwd", "k_colt_inv": "col_inv", "k_ks_rows": "ks_rows",
 ROW_MODES = {"0": "row_fwd", "1": "row_inv", "2": "row_mul"}
 
 
-PLANE = {"k_plane_fwd": "plane_fwd", "k_plane_mul": "plane_mul", "k_plane_fused": "plane_fused"}
-
-
 def short(kname):
-    m = re.search(r"\bk_mf_ntt<(true|false), 4>", kname)
+    m = re.search(r"\bk_mf_ntt<(true|false)>", kname)
     if m:
         return "mf_ntt_inv" if m.group(1) == "true" else "mf_ntt_fwd"
-    if re.search(r"\bk_mf_mul\(", kname):
-        return "mf_mul"
-    m = re.search(r"\bk_plane_ntt<(true|false)>", kname)
-    if m:
-        return "plane_ntt_inv" if m.group(1) == "true" else "plane_ntt_fwd"
-    m = re.search(r"\b(k_plane_\w+)\(", kname)
-    if m:
-        return PLANE.get(m.group(1))
+    if re.search(r"\bk_plane_fused\(", kname):
+        return "plane_fused"
     m = re.search(r"(k_\w+)<([^>]*)>", kname)
     if not m or not m.group(2).startswith("unsigned int"):
         return None

@@ -95,8 +95,7 @@ thread_local Capture* g_capture = nullptr;
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
-    "sfft", "sample", "copy", "plane_fwd", "plane_mul", "plane_fused", "plane_ntt_fwd", "plane_ntt_inv",
-    "mf_mul", "mf_ntt_fwd", "mf_ntt_inv"};
+    "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -424,21 +423,20 @@ int check_same(const rnt_buf* a, const rnt_buf* b, const char* what) {
   return RNT_OK;
 }
 
-// The MFMA transform path (rnt_mfma.hip) for this context: RNT_PLANE=5 on
-// a basis it supports, its tables built on first use.
+// The MFMA transforms (rnt_mfma.hip) for this context: N = 2^16 on a u32
+// basis (unless RNT_PLANE=0), their tables built on first use.
 bool use_mf(const rnt::Launch& k) {
   rnt::Tables* t = const_cast<rnt::Tables*>(k.t);
-  if (t->plane != 5 || !rnt::mf_supported(t)) return false;
+  if (!rnt::mf_supported(t)) return false;
   std::lock_guard<std::mutex> g(t->mf_mu);
-  if (!t->mf) {
+  if (!t->mf && !t->mf_failed) {
     std::string err;
     if (rnt::mf_build(t, &err) != 0) {
-      fprintf(stderr, "rnsntt: %s; the MFMA path is off for this basis\n", err.c_str());
-      t->plane = 3;
-      return false;
+      fprintf(stderr, "rnsntt: %s; the four-step transforms serve this basis\n", err.c_str());
+      t->mf_failed = true;
     }
   }
-  return true;
+  return t->mf != nullptr;
 }
 
 // Inverse-transform src (NTT domain) into dst (same layout): dst may equal src.
@@ -450,11 +448,7 @@ int to_coeff_into(const rnt_buf* src, void* dst) {
                            hipMemcpyDeviceToDevice, k.s),
             "hipMemcpyAsync");
   if (use_mf(k)) {
-    LAUNCH(k.t, rnt::K_MF_NTT_INV, rnt::launch_mf_ntt(k, 1, dst, ls, 4), "MFMA inverse transform");
-    return RNT_OK;
-  }
-  if (rnt::plane_ok(k.t)) {
-    LAUNCH(k.t, rnt::K_PLANE_NTT_INV, rnt::launch_plane_ntt(k, 1, dst, ls), "plane inverse transform");
+    LAUNCH(k.t, rnt::K_MF_NTT_INV, rnt::launch_mf_ntt(k, 1, dst, ls), "MFMA inverse transform");
     return RNT_OK;
   }
   LAUNCH(k.t, rnt::K_ROW_INV, rnt::launch_row(k, 1, dst, nullptr, ls), "row inverse");
@@ -687,12 +681,9 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     t->wide = wide ? 1 : 0;
     // RNT_LAZY30=0 keeps the canonical product path for 30-bit bases (A/B)
     t->lazy30 = !wide && lazy30 && env_long("RNT_LAZY30", 1) != 0;
-    // RNT_PLANE=1: rnt_mul through the whole-plane kernels (N = 2^16, u32)
-    // the whole-plane product is the default where it applies (plane_ok);
-    // RNT_PLANE=0 keeps the four-step kernels, 1 the two-launch plane path,
-    // 3 the fused kernel (one workgroup per plane), 4 its persistent form
-    t->plane = (int)env_long("RNT_PLANE", 3);
-    t->plane_stagger = (uint32_t)env_long("RNT_PLANE_STAGGER", 0);
+    // the whole-plane product and MFMA transforms are the default where they
+    // apply (N = 2^16, u32); RNT_PLANE=0 keeps the four-step kernels
+    t->plane = env_long("RNT_PLANE", 1) != 0 ? 1 : 0;
     {
       const long jg = env_long("RNT_DEC_JG", 0);  // A/B knob: 0 = auto, else 1..1024
       t->dec_jg = (uint32_t)(jg < 0 ? 0 : jg > 1024 ? 1024 : jg);
@@ -1150,28 +1141,14 @@ extern "C" int rnt_ntt_fwd(rnt_buf* b) {
   rnt::Launch k = launch_for(b);
   const uint64_t ls = limb_stride(b);
   if (use_mf(k)) {
-    LAUNCH(k.t, rnt::K_MF_NTT_FWD, rnt::launch_mf_ntt(k, 0, b->data, ls, 4), "MFMA forward transform");
-  } else if (rnt::plane_ok(k.t)) {
-    // N = 2^16, u32 bases: the whole-plane transform (rnt_plane.hip)
-    LAUNCH(k.t, rnt::K_PLANE_NTT_FWD, rnt::launch_plane_ntt(k, 0, b->data, ls), "plane forward transform");
+    // N = 2^16, u32 bases: the whole-plane MFMA transform (rnt_mfma.hip)
+    LAUNCH(k.t, rnt::K_MF_NTT_FWD, rnt::launch_mf_ntt(k, 0, b->data, ls), "MFMA forward transform");
   } else {
     LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, b->data, b->data, nullptr, nullptr, ls, ls),
            "column forward");
     LAUNCH(k.t, rnt::K_ROW_FWD, rnt::launch_row(k, 0, b->data, nullptr, ls), "row forward");
   }
   b->in_ntt = 1;
-  return RNT_OK;
-}
-
-// Debug (tools/mfma_stage_check.py, not in include/rnsntt.h): the first
-// `stop` (2 or 3) MFMA forward passes in place, each word written canonical
-// at its in-place index; the buffer's domain flag is left as it was.
-extern "C" __attribute__((visibility("default"))) int rnt_debug_mf_stage(rnt_buf* b, int stop) {
-  if (int rc = check_buf(b, "rnt_debug_mf_stage")) return rc;
-  if (int rc = set_device(b->ctx)) return rc;
-  rnt::Launch k = launch_for(b);
-  if (!use_mf(k)) return fail(RNT_ERR_UNSUPPORTED, "the MFMA path is off (RNT_PLANE=5 at N = 2^16, u32)");
-  HIP_TRY(rnt::launch_mf_ntt(k, 0, b->data, limb_stride(b), stop), "MFMA stage");
   return RNT_OK;
 }
 
@@ -1210,21 +1187,9 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   // pointwise product, inverse rows), the inverse column pass.
   const uint64_t ls = limb_stride(out);
   if (int rc = ensure_ws(out, poly_words(out) * word_bytes(k.t))) return rc;
-  if (use_mf(k)) {
-    LAUNCH(k.t, rnt::K_MF_MUL, rnt::launch_mf_mul(k, out->data, a->data, b->data, out->ws, ls), "MFMA product");
-    out->in_ntt = 0;
-    return RNT_OK;
-  }
-  if (rnt::plane_ok(k.t) && k.t->plane >= 3) {
+  if (rnt::plane_ok(k.t)) {
     LAUNCH(k.t, rnt::K_PLANE_FUSED, rnt::launch_plane_fused(k, out->data, a->data, b->data, out->ws, ls),
            "plane fused product");
-    out->in_ntt = 0;
-    return RNT_OK;
-  }
-  if (rnt::plane_ok(k.t)) {
-    // whole-plane product: a^ into the workspace, then b^ (x) a^ -> c
-    LAUNCH(k.t, rnt::K_PLANE_FWD, rnt::launch_plane(k, 0, out->ws, a->data, nullptr, ls), "plane forward");
-    LAUNCH(k.t, rnt::K_PLANE_MUL, rnt::launch_plane(k, 1, out->data, b->data, out->ws, ls), "plane product");
     out->in_ntt = 0;
     return RNT_OK;
   }

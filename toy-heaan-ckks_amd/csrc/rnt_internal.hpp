@@ -81,9 +81,8 @@ struct Tables {
   int device = 0;
   int wide = 0;            // 0: W = u32, 1: W = u64
   bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path
-  int plane = 0;           // rnt_mul through the whole-plane kernels where plane_ok (RNT_PLANE:
-                           // 1 two launches, 3 both halves in one workgroup)
-  uint32_t plane_stagger = 0;  // their first-wave phase shift, 100 MHz ticks (RNT_PLANE_STAGGER)
+  int plane = 0;           // the whole-plane kernels where they apply (plane_ok, mf_ok);
+                           // RNT_PLANE=0: the four-step kernels everywhere
   uint32_t dec_jg = 0;     // key-switch decomposition: target limbs per workgroup (0 = auto)
   size_t ks_ws_bytes = (size_t)4096 << 20;  // key-switch scratch cap per chunk (RNT_KS_WS_MB)
   uint32_t log_n = 0;
@@ -110,9 +109,11 @@ struct Tables {
   void* sfft_tw = nullptr;
   struct Prof* prof = nullptr;  // per-kernel event timing (rnt_profile_*)
   // MFMA transform tables (rnt_mfma.hip: matrix operands, compensations and
-  // twists per limb), built on first use where mf_supported()
+  // twists per limb), built on first use where mf_supported(); mf_failed:
+  // the build failed (reported once; the four-step transforms serve)
   std::mutex mf_mu;
   void* mf = nullptr;
+  bool mf_failed = false;
   ~Tables();
 };
 
@@ -120,8 +121,7 @@ struct Tables {
 enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
-  K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FWD, K_PLANE_MUL, K_PLANE_FUSED, K_PLANE_NTT_FWD, K_PLANE_NTT_INV,
-  K_MF_MUL, K_MF_NTT_FWD, K_MF_NTT_INV, K_COUNT
+  K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FUSED, K_MF_NTT_FWD, K_MF_NTT_INV, K_COUNT
 };
 
 struct Prof {
@@ -196,26 +196,18 @@ hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* ou
 // on x); 2: poly-mul rows: x <- INVrow(FWDrow(x) (.) FWDrow(y) * 2^-w).
 hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls,
                       bool lazy = false);
-// The whole-plane product for u32 canonical bases at N = 2^16 (5 planes of
-// HBM traffic per (poly, limb) instead of the four-step path's 9):
-// which 0: out = a^ (private layout, k.L x k.B planes at limb stride ls) of
-// in; which 1: out = in * a^ (coefficient domain; out may alias in).
+// The whole-plane product for u32 canonical bases at N = 2^16 (rnt_plane.hip;
+// 5 planes of HBM traffic per (poly, limb) instead of the four-step path's
+// 9): out = a * b in the coefficient domain (out may alias a or b; scratch:
+// one word per output word, a^ in a private layout).
 bool plane_ok(const Tables* t);
-hipError_t launch_plane(const Launch& k, int which, void* out, const void* in, const void* ahat,
-                        uint64_t ls);
 hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls);
-// standalone whole-plane transforms in place (N = 2^16, u32; plane_ok)
-hipError_t launch_plane_ntt(const Launch& k, int inverse, void* data, uint64_t ls);
-// The MFMA forms of the same (rnt_mfma.hip): radix-16 passes as i8 matrix
-// products.  mf_supported: u32 bases at N = 2^16 (the tables exist once
-// mf_build ran); mf_build: the per-limb tables into t->mf (0 ok, else err).
-inline bool mf_supported(const Tables* t) { return !t->wide && t->log_n == 16; }
+// The standalone transforms at the same size (rnt_mfma.hip): radix-16 passes
+// as i8 matrix products, in place.  mf_supported: u32 bases at N = 2^16;
+// mf_build: the per-limb tables into t->mf (0 ok, else err).
+inline bool mf_supported(const Tables* t) { return t->plane != 0 && !t->wide && t->log_n == 16; }
 int mf_build(Tables* t, std::string* err);
-// out = a * b (coefficient domain; out may alias a or b; scratch: one word
-// per output word)
-hipError_t launch_mf_mul(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls);
-// in place; stop 4 = the whole transform, 2 / 3 = debug prefixes of the forward
-hipError_t launch_mf_ntt(const Launch& k, int inverse, void* data, uint64_t ls, int stop);
+hipError_t launch_mf_ntt(const Launch& k, int inverse, void* data, uint64_t ls);
 // Whether rnt_mul's row kernel stops its transforms two stages early and
 // multiplies degree-3 residues (u32 canonical bases, row length 2^(4k));
 // its inverse column pass then takes rfold = 2.

@@ -65,7 +65,6 @@
 #include "rnt_hostmath.hpp"
 #include "rnt_modarith.hpp"
 #include "rnt_device.hpp"
-#include "rnt_bfly4.hpp"
 
 namespace rnt {
 namespace mf {
@@ -77,23 +76,18 @@ constexpr uint32_t K32 = 0x80808080u;
 
 // ---- per-limb table (v4i units): MFMA operands, compensations, twists ----
 // Matrix slot s, digit plane a, lane lam: operand bytes of that lane.
-// F1..I1: the standalone transforms (four MFMA passes); F3B, I3B, I1H: the
-// product's pass 2 with the data as B (P3 layout kept) and its inverse, and
-// the product's last inverse matrix (2^32 / 4: the Montgomery block products
-// and the two GS stages' factor 2 each).
-constexpr int S_F1 = 0, S_F2 = 1, S_F3 = 17, S_F4 = 18, S_I4 = 19, S_I3 = 20, S_I2 = 21, S_I1R = 37, S_I1 = 38;
-constexpr int S_F3B = 39, S_I3B = 40, S_I1H = 41;
-constexpr int kSlots = 42;
+// F1..F4: the forward passes (F2: one per U), I4..I1: the inverse's.
+constexpr int S_F1 = 0, S_F2 = 1, S_F3 = 17, S_F4 = 18, S_I4 = 19, S_I3 = 20, S_I2 = 21, S_I1 = 37;
+constexpr int kSlots = 38;
 constexpr int kMat = 0;
 constexpr int kCompF1 = kSlots * 4 * 64;  // [lam]: digit-0 accumulator start of pass 0 (input bias)
 constexpr int kCompI4 = kCompF1 + 64;     // [lam]: the same for the standalone inverse's first pass
-constexpr int kCompI3 = kCompI4 + 64;     // [lam]: the same for the product's inverse pass 2 (S_I3B)
-constexpr int kTw3f = kCompI3 + 64;       // [w][g][c], element i: pass 2 twist, P2 positions
+constexpr int kTw3f = kCompI4 + 64;       // [w][g][c], element i: pass 2 twist, P2 positions
 constexpr int kTw4f = kTw3f + 1024;       // [w][c][lam]: pass 3 twist, P4 positions
 constexpr int kTw4i = kTw4f + 16384;      // [w][c][lam]: inverse pass 3 twist, Q3 positions
 constexpr int kTw3i = kTw4i + 16384;      // [w][c][g]: inverse pass 2 twist, Q3 positions
-constexpr int kTw3iB = kTw3i + 1024;      // [w][c][g]: inverse pass 2 twist, P3 positions (product)
-constexpr int kLimb = kTw3iB + 1024;
+constexpr int kLimb = kTw3i + 1024;
+constexpr size_t kLdsBytes = (size_t)(1u << 15) * 4;  // the P1 <-> P2 exchange: half a plane per round
 
 // Registers of a P3 / P4 / Q3 chunk (c, i) after the P2 -> P3 swap, as
 // physical slots of the P2 numbering 4c + i (see the header).
@@ -194,10 +188,20 @@ __device__ __forceinline__ void load_mat(v4i (&M)[4], Rsrc tab, uint32_t slot, u
   for (int a = 0; a < 4; ++a) M[a] = bld(tab, lo, (uint32_t)(kMat + (slot * 4 + a) * 64) * 16u);
 }
 
+// The thread's coordinates.  Lane-derived values are recomputed at each use
+// from an opaque copy of the thread id: hipcc would otherwise keep every
+// offset derived from them live across the whole kernel (and spill them).
 struct Th {
-  uint32_t t, w, lam, g, n;
-  __device__ explicit Th(uint32_t tt)
-      : t(tt), w(__builtin_amdgcn_readfirstlane(tt >> 6)), lam(tt & 63u), g((tt >> 4) & 3u), n(tt & 15u) {}
+  uint32_t tid0, w;
+  __device__ explicit Th(uint32_t tt) : tid0(tt), w(__builtin_amdgcn_readfirstlane(tt >> 6)) {}
+  __device__ __forceinline__ uint32_t t() const {
+    uint32_t v = tid0;
+    asm volatile("" : "+v"(v));
+    return v;
+  }
+  __device__ __forceinline__ uint32_t lam() const { return t() & 63u; }
+  __device__ __forceinline__ uint32_t g() const { return (t() >> 4) & 3u; }
+  __device__ __forceinline__ uint32_t n() const { return t() & 15u; }
 };
 
 // ---- P1 <-> P2 through LDS ----------------------------------------------------
@@ -209,8 +213,8 @@ struct Th {
 // Per thread: a base per value of the two register bits inside an XOR term,
 // the other register bits as instruction offsets.
 __device__ __forceinline__ void p1_bases(uint32_t (&wb)[4], const Th& h) {
-  const uint32_t n0 = h.n & 1, n1 = (h.n >> 1) & 1, n2 = (h.n >> 2) & 1, n3 = h.n >> 3;
-  const uint32_t g0 = h.g & 1, g1 = h.g >> 1;
+  const uint32_t n0 = h.n() & 1, n1 = (h.n() >> 1) & 1, n2 = (h.n() >> 2) & 1, n3 = h.n() >> 3;
+  const uint32_t g0 = h.g() & 1, g1 = h.g() >> 1;
   const uint32_t w0 = h.w & 1, w1 = (h.w >> 1) & 1, w2 = (h.w >> 2) & 1, w3 = h.w >> 3;
   const uint32_t rest = 4 * n0 + 8 * n1 + 16 * (w1 ^ g0) + 256 * w0 + 512 * w3 + 1024 * n2 + 2048 * n3 +
                         4096 * g0 + 8192 * g1 + 16384 * w2;
@@ -218,8 +222,8 @@ __device__ __forceinline__ void p1_bases(uint32_t (&wb)[4], const Th& h) {
   for (uint32_t e = 0; e < 4; ++e) wb[e] = rest + ((e & 1) ^ n2) + 2 * ((e >> 1) ^ n3);
 }
 __device__ __forceinline__ void p2_bases(uint32_t (&rb)[4], const Th& h) {
-  const uint32_t n0 = h.n & 1, n1 = (h.n >> 1) & 1, n2 = (h.n >> 2) & 1, n3 = h.n >> 3;
-  const uint32_t g0 = h.g & 1, g1 = h.g >> 1;
+  const uint32_t n0 = h.n() & 1, n1 = (h.n() >> 1) & 1, n2 = (h.n() >> 2) & 1, n3 = h.n() >> 3;
+  const uint32_t g0 = h.g() & 1, g1 = h.g() >> 1;
   const uint32_t w0 = h.w & 1, w1 = (h.w >> 1) & 1, w2 = (h.w >> 2) & 1, w3 = h.w >> 3;
   const uint32_t rest = 4 * n2 + 8 * n3 + 16 * (g0 ^ w0) + 64 * w2 + 128 * w3 + 4096 * w0 + 8192 * w1 + 16384 * g1;
 #pragma unroll
@@ -276,12 +280,12 @@ __device__ __forceinline__ void x_read_p2(uint32_t (&x2)[64], const uint32_t* ld
   lds_wait8<32 * H + 24>(x2);
 }
 // the inverse direction: P2 words at q2(c, i) out, P1 words in
-template <int H, bool Q2 = true>
+template <int H>
 __device__ __forceinline__ void x_write_p2(const uint32_t (&x2)[64], uint32_t* lds, const uint32_t (&rb)[4]) {
 #pragma unroll
   for (int c = 8 * H; c < 8 * H + 8; ++c)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) lds[rb[c & 3] + p2_off(c, i)] = x2[(Q2 ? q2(c, i) : 4 * c + i)];
+    for (int i = 0; i < 4; ++i) lds[rb[c & 3] + p2_off(c, i)] = x2[q2(c, i)];
 }
 template <int H, int C, int I>
 __device__ __forceinline__ void x_read_p1_one(uint32_t (&x1)[64], uint32_t lds0, const uint32_t (&wb)[4]) {
@@ -371,30 +375,31 @@ __device__ __forceinline__ void pass_p1(uint32_t (&x1)[64], const v4i (&M)[4], v
   }
 }
 // pass 1 (per-wave matrix) on P2 chunks [C0, C0 + 8), then the pass-2 twist
-// (TW: the table in P2 positions; DBG_NOTW leaves it out: measurement of pass 1).
-template <int C0, bool DBG_NOTW = false>
+// (TW: the table in P2 positions).
+template <int C0>
 __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
                                         const Mc& m) {
   const v4i z = {0, 0, 0, 0};
+  v4i tv = bld(tab, tvo, tso + (uint32_t)C0 * 16u);  // each tile's twists one tile ahead
 #pragma unroll
   for (int c = C0; c < C0 + 8; ++c) {
     v4i b;
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x2[4 * c + i];
-    const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 16u);
+    const v4i tn = c + 1 < C0 + 8 ? bld(tab, tvo, tso + (uint32_t)(c + 1) * 16u) : tv;
     v4i D[4];
     tile<false>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
-      x2[4 * c + i] = DBG_NOTW ? (uint32_t)(r + (int32_t)K32) ^ K32 : (uint32_t)mont<true>(r, tv[i], m) ^ K32;
+      x2[4 * c + i] = (uint32_t)mont<true>(r, tv[i], m) ^ K32;
     }
     pin4(x2[4 * c + 0], x2[4 * c + 1], x2[4 * c + 2], x2[4 * c + 3]);
+    tv = tn;
     tile_fence();
   }
 }
 // pass 2 (F, data as A: P3 -> P4 positions), then the pass-3 twist.
-template <bool DBG_NOTW = false>
 __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
                                         const Mc& m) {
   const v4i z = {0, 0, 0, 0};
@@ -409,7 +414,7 @@ __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rs
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
-      x[p3(c, i)] = DBG_NOTW ? (uint32_t)(r + (int32_t)K32) ^ K32 : (uint32_t)mont<true>(r, tv[i], m) ^ K32;
+      x[p3(c, i)] = (uint32_t)mont<true>(r, tv[i], m) ^ K32;
     }
     pin4(x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
     tile_fence();
@@ -476,25 +481,22 @@ __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], R
     tile_fence();
   }
 }
-// inverse pass 1 (per-wave matrix) on P2 chunks [C0, C0 + 8) at q2 slots; packed output.
-// P2 register of chunk (c, i): after the inverse's Q3 -> P2 swap (Q2) or
-// after a swap back from P3 (the product)
-template <bool Q2>
-__host__ __device__ constexpr int p2r(int c, int i) { return Q2 ? q2(c, i) : 4 * c + i; }
-template <int C0, bool Q2 = true>
+// inverse pass 1 (per-wave matrix) on P2 chunks [C0, C0 + 8) at q2 slots
+// (the registers after the Q3 -> P2 swap); packed output.
+template <int C0>
 __device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], const Mc& m) {
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = C0; c < C0 + 8; ++c) {
     v4i b;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) b[i] = (int)x[p2r<Q2>(c, i)];
+    for (int i = 0; i < 4; ++i) b[i] = (int)x[q2(c, i)];
     v4i D[4];
     tile<false>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      x[p2r<Q2>(c, i)] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
-    pin4(x[p2r<Q2>(c, 0)], x[p2r<Q2>(c, 1)], x[p2r<Q2>(c, 2)], x[p2r<Q2>(c, 3)]);
+      x[q2(c, i)] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
+    pin4(x[q2(c, 0)], x[q2(c, 1)], x[q2(c, 2)], x[q2(c, 3)]);
     tile_fence();
   }
 }
@@ -519,7 +521,7 @@ __device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], 
 // P1 plane byte offsets of load / store (i, hc): 4 consecutive words,
 // chunks c = 4 hc + e, e = 0..3.  Lane part (VGPR), wave part and the
 // register part (SGPR).
-__device__ __forceinline__ uint32_t p1_lane(const Th& h) { return ((h.g << 12) | (h.n << 2)) * 4u; }
+__device__ __forceinline__ uint32_t p1_lane(const Th& h) { return ((h.g() << 12) | (h.n() << 2)) * 4u; }
 __device__ __forceinline__ uint32_t p1_wave(const Th& h) {
   const uint32_t w = h.w;
   return (((w >> 3) << 11) | (((w >> 2) & 1) << 9) | (((w >> 1) & 1) << 8) | ((w & 1) << 6)) * 4u;
@@ -551,7 +553,7 @@ __device__ __forceinline__ void store_p1(const uint32_t (&x1)[64], Rsrc dst, con
     }
 }
 // P4 (NTT-domain device order): chunk c's 4 words are consecutive.
-__device__ __forceinline__ uint32_t p4_lane(const Th& h) { return ((h.n << 4) | (h.g << 2)) * 4u; }
+__device__ __forceinline__ uint32_t p4_lane(const Th& h) { return ((h.n() << 4) | (h.g() << 2)) * 4u; }
 __device__ __forceinline__ uint32_t p4_soff(const Th& h, int c) { return ((h.w << 12) | ((uint32_t)c << 8)) * 4u; }
 
 struct Tabs {
@@ -575,17 +577,18 @@ __device__ __forceinline__ Tabs tabs_of(const void* mf, const LimbConst<uint32_t
 
 // The forward transform: canonical plane at src (P1) -> x2 in P4 positions,
 // centred representatives.  SYNC1: the LDS may still be in use by other waves.
-// STOP (measurement of a prefix, debug only): 1..4 passes.
+// EPI(c, r, x2): the last pass's per-tile epilogue (the standalone forward
+// stores each tile from it).
 struct NoEpi {
   __device__ void operator()(int, const int32_t (&)[4], uint32_t (&)[64]) const {}
 };
-template <bool SYNC1, int STOP = 4, class EPI = NoEpi>
+template <bool SYNC1, class EPI = NoEpi>
 __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds, const Th& h, const Tabs& T,
                                     const EPI& epi = EPI{}) {
   uint32_t x1[64];
   load_p1(x1, src, h);
   const Mc& m = T.m;
-  const uint32_t lo = h.lam * 16u;
+  const uint32_t lo = h.lam() * 16u;
   v4i M[4];
   load_mat(M, T.tab, S_F1, lo);
   const v4i comp = bld(T.tab, lo, (uint32_t)kCompF1 * 16u);
@@ -602,36 +605,31 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   p1_bases(wb, h);
   x_write_p1<1>(x1, lds, wb);
   load_mat(M, T.tab, S_F2 + h.w, lo);
-  const uint32_t t3v = h.g * 256u, t3s = (uint32_t)(kTw3f + h.w * 64) * 16u;
-  pass_p2<0, STOP == 2>(x2, M, T.tab, t3v, t3s, m);
+  const uint32_t t3v = h.g() * 256u, t3s = (uint32_t)(kTw3f + h.w * 64) * 16u;
+  pass_p2<0>(x2, M, T.tab, t3v, t3s, m);
   __syncthreads();
   p2_bases(rb, h);
   x_read_p2<1>(x2, lds, rb);
-  pass_p2<8, STOP == 2>(x2, M, T.tab, t3v, t3s, m);
-  if constexpr (STOP <= 2) return;
+  pass_p2<8>(x2, M, T.tab, t3v, t3s, m);
   swap_p2p3(x2);
   load_mat(M, T.tab, S_F3, lo);
-  pass_p3<STOP == 3>(x2, M, T.tab, lo, (uint32_t)(kTw4f + h.w * 1024) * 16u, m);
-  if constexpr (STOP <= 3) return;
+  pass_p3(x2, M, T.tab, lo, (uint32_t)(kTw4f + h.w * 1024) * 16u, m);
   load_mat(M, T.tab, S_F4, lo);
   pass_p4(x2, M, m, epi);
 }
 
 // The inverse from x2 (packed, P4 positions) to the canonical plane at dst
-// (P1); SLOT1: the last matrix (S_I1R after a product, S_I1 standalone);
-// comp: the first pass's digit-0 start (input bias of a standalone inverse).
-template <bool BIAS>
-__device__ __forceinline__ void inv(uint32_t (&x2)[64], Rsrc dst, uint32_t* lds, const Th& h, const Tabs& T,
-                                    uint32_t slot1) {
+// (P1); the first pass's digit-0 accumulators start at the input bias's
+// compensation (canonical input words travel as x - 2^30).
+__device__ __forceinline__ void inv(uint32_t (&x2)[64], Rsrc dst, uint32_t* lds, const Th& h, const Tabs& T) {
   const Mc& m = T.m;
-  const uint32_t lo = h.lam * 16u;
+  const uint32_t lo = h.lam() * 16u;
   v4i M[4];
   load_mat(M, T.tab, S_I4, lo);
-  const v4i z = {0, 0, 0, 0};
-  ipass_p4(x2, M, BIAS ? bld(T.tab, lo, (uint32_t)kCompI4 * 16u) : z, T.tab, lo, (uint32_t)(kTw4i + h.w * 1024) * 16u,
+  ipass_p4(x2, M, bld(T.tab, lo, (uint32_t)kCompI4 * 16u), T.tab, lo, (uint32_t)(kTw4i + h.w * 1024) * 16u,
            m);
   load_mat(M, T.tab, S_I3, lo);
-  ipass_p3(x2, M, T.tab, h.g * 16u, (uint32_t)(kTw3i + h.w * 64) * 16u, m);
+  ipass_p3(x2, M, T.tab, h.g() * 16u, (uint32_t)(kTw3i + h.w * 64) * 16u, m);
   swap_q3p2(x2);
   load_mat(M, T.tab, S_I2 + h.w, lo);
   uint32_t wb[4], rb[4];
@@ -647,233 +645,7 @@ __device__ __forceinline__ void inv(uint32_t (&x2)[64], Rsrc dst, uint32_t* lds,
   __syncthreads();
   p2_bases(rb, h);
   x_write_p2<1>(x2, lds, rb);
-  load_mat(M, T.tab, slot1, lo);
-  ipass_p1<0>(x1, M, m);
-  __syncthreads();
-  p1_bases(wb, h);
-  x_read_p1<1>(x1, lds, wb);
-  ipass_p1<8>(x1, M, m);
-  store_p1(x1, dst, h);
-}
-
-// ---- the product: MFMA passes 0-2 (index bits 15..4), then the truncated
-// tail as in rnt_plane.hip (CT stages at bits 3, 2; degree-3 block products
-// mod X^4 - zeta; GS stages back) -------------------------------------------
-// P5 layout (the tail): registers y[16 i + d] hold index bits 7,6 (i) and
-// 3..0 (d); lanes: g = (5,4), lane bits 3..0 = index bits 11..8; w = 15..12.
-constexpr int kXS = 17;                         // transpose buffer row stride (words)
-constexpr int kXW = 64 * kXS;                   // one wave's transpose buffer
-constexpr int kTrWords = 16 * 2 * kXW;          // two per wave
-constexpr size_t kLdsBytes = (size_t)((1u << 15) > (uint32_t)kTrWords ? (1u << 15) : (uint32_t)kTrWords) * 4;
-
-// pass 2 with the data as B (P3 layout in place), canonical output for the tail.
-__device__ __forceinline__ void pass_p3b(uint32_t (&x)[64], const v4i (&M)[4], const Mc& m) {
-  const v4i z = {0, 0, 0, 0};
-#pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    v4i b;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) b[i] = (int)x[p3(c, i)];
-    v4i D[4];
-    tile<false>(D, M, b, z);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x[p3(c, i)] = canon(recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m), m.q);
-    pin4(x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
-    tile_fence();
-  }
-}
-// inverse pass 2 (F^-1, data as B in the P3 layout): canonical input (biased,
-// comp undoes it), output twisted and packed.
-__device__ __forceinline__ void ipass_p3b(uint32_t (&x)[64], const v4i (&M)[4], v4i comp, Rsrc tab, uint32_t tvo,
-                                          uint32_t tso, const Mc& m) {
-#pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    v4i b;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) b[i] = (int)pk_canon(x[p3(c, i)]);
-    const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 64u);
-    v4i D[4];
-    tile<false>(D, M, b, comp);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
-      x[p3(c, i)] = (uint32_t)mont<true>(r, tv[i], m) ^ K32;
-    }
-    pin4(x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
-    tile_fence();
-  }
-}
-
-// P3 <-> P5: per register i and lane group g a 16 x 16 transpose of lane
-// bits 3..0 (index bits 3..0 in P3, 11..8 in P5) and chunk bits (11..8 in
-// P3, 3..0 in P5) through the wave's own LDS buffers (4 rounds, 2 buffers;
-// rows of 17 words: conflict-free both ways).  No workgroup barrier: a wave
-// reads only what it wrote (its LDS instructions execute in order).
-template <bool TO_P5>
-__device__ __forceinline__ void tr_p3p5(uint32_t (&x)[64], uint32_t (&y)[64], uint32_t* lds, const Th& h) {
-  uint32_t* base = lds + h.w * (2 * kXW);
-  const uint32_t rowa = h.lam * kXS;                           // + c
-  const uint32_t rowb = (h.g * 16u) * kXS + h.n;               // + d * kXS
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    uint32_t* buf = base + (i & 1) * kXW;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      if constexpr (TO_P5)
-        buf[rowa + c] = x[p3(c, i)];
-      else
-        buf[rowb + c * kXS] = y[16 * i + c];
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      if constexpr (TO_P5)
-        y[16 * i + c] = buf[rowb + c * kXS];
-      else
-        x[p3(c, i)] = buf[rowa + c];
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// Twiddle pairs {w, w'} of the limb's table by heap node (8-byte loads).
-__device__ __forceinline__ Tw<uint32_t> twl(Rsrc t, uint32_t node) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b64(t, node * 8u, 0, 0);
-  return Tw<uint32_t>{(uint32_t)v[0], (uint32_t)v[1]};
-}
-
-// Four CT butterflies (y[A + k], y[A + k + D]), k = 0..3, one twiddle, as
-// interleaved asm (rnt_bfly4.hpp: no s_nop hazard pads); LAZY: outputs in
-// [0, 2q] (both only multiplied next).
-template <int A, int D, bool LAZY>
-__device__ __forceinline__ void ct4(uint32_t (&y)[64], Tw<uint32_t> t, const Mod<uint32_t>& mo) {
-  const uint32_t w[4] = {t.w, t.w, t.w, t.w}, wp[4] = {t.p, t.p, t.p, t.p};
-  uint64_t P[4];
-  b4::shoup_prod4<false>(P, y[A + D], y[A + D + 1], y[A + D + 2], y[A + D + 3], w, wp, mo.nq);
-  uint32_t pl[4] = {(uint32_t)P[0], (uint32_t)P[1], (uint32_t)P[2], (uint32_t)P[3]};
-  if constexpr (LAZY)
-    b4::ct_reduce4_lazy(y[A], y[A + 1], y[A + 2], y[A + 3], y[A + D], y[A + D + 1], y[A + D + 2], y[A + D + 3], pl,
-                        mo.q);
-  else
-    b4::ct_reduce4(y[A], y[A + 1], y[A + 2], y[A + 3], y[A + D], y[A + D + 1], y[A + D + 2], y[A + D + 3], pl, mo.q);
-}
-template <int A, int D>
-__device__ __forceinline__ void gs4(uint32_t (&y)[64], Tw<uint32_t> t, const Mod<uint32_t>& mo) {
-  const uint32_t w[4] = {t.w, t.w, t.w, t.w}, wp[4] = {t.p, t.p, t.p, t.p};
-  uint32_t dd[4];
-  b4::gs_pre4(y[A], y[A + 1], y[A + 2], y[A + 3], y[A + D], y[A + D + 1], y[A + D + 2], y[A + D + 3], dd, mo.q);
-  uint64_t P[4];
-  b4::shoup_prod4<false>(P, dd[0], dd[1], dd[2], dd[3], w, wp, mo.nq);
-  const uint32_t pl[4] = {(uint32_t)P[0], (uint32_t)P[1], (uint32_t)P[2], (uint32_t)P[3]};
-  b4::csub4(y[A + D], y[A + D + 1], y[A + D + 2], y[A + D + 3], pl, mo.q);
-}
-
-// CT stages at index bits 3 and 2 in P5 (hi4 = index >> 4 without the i bits).
-// Bit 3's butterflies with bit 2 set only feed bit 2's multiplicands (lazy).
-template <int I>
-__device__ __forceinline__ void tail_ct_i(uint32_t (&y)[64], Rsrc tw, uint32_t hi4, const Mod<uint32_t>& mo) {
-  const uint32_t h6 = hi4 | ((uint32_t)I << 2);
-  const Tw<uint32_t> t3 = twl(tw, (kN >> 4) + h6);
-  const Tw<uint32_t> t20 = twl(tw, (kN >> 3) + (h6 << 1)), t21 = twl(tw, (kN >> 3) + (h6 << 1) + 1);
-  ct4<16 * I, 8, false>(y, t3, mo);
-  ct4<16 * I + 4, 8, true>(y, t3, mo);
-  ct4<16 * I, 4, false>(y, t20, mo);
-  ct4<16 * I + 8, 4, false>(y, t21, mo);
-}
-__device__ __forceinline__ void tail_ct(uint32_t (&y)[64], Rsrc tw, uint32_t hi4, const Mod<uint32_t>& mo) {
-  tail_ct_i<0>(y, tw, hi4, mo);
-  tail_ct_i<1>(y, tw, hi4, mo);
-  tail_ct_i<2>(y, tw, hi4, mo);
-  tail_ct_i<3>(y, tw, hi4, mo);
-}
-// GS stages at index bits 2 and 3 (the inverse of tail_ct times 4).
-template <int I>
-__device__ __forceinline__ void tail_gs_i(uint32_t (&y)[64], Rsrc itw, uint32_t hi4, const Mod<uint32_t>& mo) {
-  const uint32_t h6 = hi4 | ((uint32_t)I << 2);
-  const Tw<uint32_t> t20 = twl(itw, (kN >> 3) + (h6 << 1)), t21 = twl(itw, (kN >> 3) + (h6 << 1) + 1);
-  const Tw<uint32_t> t3 = twl(itw, (kN >> 4) + h6);
-  gs4<16 * I, 4>(y, t20, mo);
-  gs4<16 * I + 8, 4>(y, t21, mo);
-  gs4<16 * I, 8>(y, t3, mo);
-  gs4<16 * I + 4, 8>(y, t3, mo);
-}
-__device__ __forceinline__ void tail_gs(uint32_t (&y)[64], Rsrc itw, uint32_t hi4, const Mod<uint32_t>& mo) {
-  tail_gs_i<0>(y, itw, hi4, mo);
-  tail_gs_i<1>(y, itw, hi4, mo);
-  tail_gs_i<2>(y, itw, hi4, mo);
-  tail_gs_i<3>(y, itw, hi4, mo);
-}
-
-// The product's forward transform (14 stages): canonical plane at src -> y
-// (P5 layout, canonical, blocks of 4 words at y[16 i + 4 bb ..]).
-template <bool SYNC1>
-__device__ __forceinline__ void fwd_h(uint32_t (&y)[64], Rsrc src, uint32_t* lds, const Th& h, const Tabs& T,
-                                      Rsrc tw, uint32_t hi4, const Mod<uint32_t>& mo) {
-  uint32_t x[64];
-  {
-    uint32_t x1[64];
-    load_p1(x1, src, h);
-    const Mc& m = T.m;
-    const uint32_t lo = h.lam * 16u;
-    v4i M[4];
-    load_mat(M, T.tab, S_F1, lo);
-    const v4i comp = bld(T.tab, lo, (uint32_t)kCompF1 * 16u);
-    pass_p1<0, true>(x1, M, comp, m);
-    if constexpr (SYNC1) __syncthreads();
-    uint32_t wb[4], rb[4];
-    p1_bases(wb, h);
-    x_write_p1<0>(x1, lds, wb);
-    pass_p1<8, true>(x1, M, comp, m);
-    __syncthreads();
-    p2_bases(rb, h);
-    x_read_p2<0>(x, lds, rb);
-    __syncthreads();
-    p1_bases(wb, h);
-    x_write_p1<1>(x1, lds, wb);
-    load_mat(M, T.tab, S_F2 + h.w, lo);
-    const uint32_t t3v = h.g * 256u, t3s = (uint32_t)(kTw3f + h.w * 64) * 16u;
-    pass_p2<0>(x, M, T.tab, t3v, t3s, m);
-    __syncthreads();
-    p2_bases(rb, h);
-    x_read_p2<1>(x, lds, rb);
-    pass_p2<8>(x, M, T.tab, t3v, t3s, m);
-    swap_p2p3(x);
-    load_mat(M, T.tab, S_F3B, lo);
-    pass_p3b(x, M, m);
-  }
-  __syncthreads();  // the transpose buffers overlap the exchange region other waves may still read
-  tr_p3p5<true>(x, y, lds, h);
-  tail_ct(y, tw, hi4, mo);
-}
-
-// The product's inverse from y (P5, the block products' Montgomery outputs)
-// to the canonical plane at dst.
-__device__ __forceinline__ void inv_h(uint32_t (&y)[64], Rsrc dst, uint32_t* lds, const Th& h, const Tabs& T, Rsrc itw,
-                                      uint32_t hi4, const Mod<uint32_t>& mo) {
-  tail_gs(y, itw, hi4, mo);
-  uint32_t x[64];
-  tr_p3p5<false>(x, y, lds, h);
-  const Mc& m = T.m;
-  const uint32_t lo = h.lam * 16u;
-  v4i M[4];
-  load_mat(M, T.tab, S_I3B, lo);
-  ipass_p3b(x, M, bld(T.tab, lo, (uint32_t)kCompI3 * 16u), T.tab, h.g * 16u, (uint32_t)(kTw3iB + h.w * 64) * 16u, m);
-  swap_p2p3(x);  // back to P2 (the swap is its own inverse)
-  load_mat(M, T.tab, S_I2 + h.w, lo);
-  uint32_t wb[4], rb[4];
-  uint32_t x1[64];
-  ipass_p2<0, false>(x, M, m);
-  __syncthreads();  // other waves may still use the LDS (their transposes)
-  p2_bases(rb, h);
-  x_write_p2<0, false>(x, lds, rb);
-  ipass_p2<8, false>(x, M, m);
-  __syncthreads();
-  p1_bases(wb, h);
-  x_read_p1<0>(x1, lds, wb);
-  __syncthreads();
-  p2_bases(rb, h);
-  x_write_p2<1, false>(x, lds, rb);
-  load_mat(M, T.tab, S_I1H, lo);
+  load_mat(M, T.tab, S_I1, lo);
   ipass_p1<0>(x1, M, m);
   __syncthreads();
   p1_bases(wb, h);
@@ -884,56 +656,9 @@ __device__ __forceinline__ void inv_h(uint32_t (&y)[64], Rsrc dst, uint32_t* lds
 
 }  // namespace mf
 
-// One workgroup per (poly, limb) plane pair, grid (B, L): c = a * b.
-// a^ (P5 layout, this thread's 16 blocks of 4 words) goes to a scratch plane
-// and comes back for the degree-3 block products (as rnt_plane.hip's).
-__global__ void __launch_bounds__(mf::kT, 1)
-k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
-         const void* __restrict__ mft, TabPtrs<uint32_t> tp, uint64_t ls) {
-  using namespace mf;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  uint32_t* lds = (uint32_t*)smem_raw;
-  const Th h(threadIdx.x);
-  const uint32_t poly = blockIdx.x, l = blockIdx.y;
-  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * kN;
-  const LimbConst<uint32_t> lc = tp.lc[l];
-  const Tabs T = tabs_of(mft, lc, l);
-  const Mod<uint32_t> mo = mod_of(lc);
-  constexpr uint32_t PB = kN * 4u;
-  const Rsrc tw = rsrc(tp.tw + (uint64_t)l * kN, kN * 8u), itw = rsrc(tp.itw + (uint64_t)l * kN, kN * 8u);
-  const uint32_t hi4 = (h.w << 8) | (h.n << 4) | h.g;  // index >> 4 in P5, without the i bits
-  uint32_t y[64];
-  fwd_h<false>(y, rsrc(a + off, PB), lds, h, T, tw, hi4, mo);
-  const Rsrc ah = rsrc(scratch + off, PB);
-  const uint32_t ao = h.t * 16u;
-#pragma unroll
-  for (int kk = 0; kk < 16; ++kk)
-    bst(v4i{(int)y[16 * (kk >> 2) + 4 * (kk & 3)], (int)y[16 * (kk >> 2) + 4 * (kk & 3) + 1],
-            (int)y[16 * (kk >> 2) + 4 * (kk & 3) + 2], (int)y[16 * (kk >> 2) + 4 * (kk & 3) + 3]},
-        ah, ao, (uint32_t)kk * (kT * 16u));
-  fwd_h<true>(y, rsrc(b + off, PB), lds, h, T, tw, hi4, mo);
-  // degree-3 block products: block (i, bb) of this thread is block index
-  // ((hi4 | i << 2) << 2) | bb, zeta = (-1)^bb psi_rev[N/8 + index / 2]
-#pragma unroll
-  for (int kk = 0; kk < 16; ++kk) {
-    const int i = kk >> 2, bb = kk & 3;
-    const v4i av = bld(ah, ao, (uint32_t)kk * (kT * 16u));
-    const Tw<uint32_t> z = twl(tw, (kN >> 3) + (((hi4 | ((uint32_t)i << 2)) << 1) | (uint32_t)(bb >> 1)));
-    const uint32_t zeta = (bb & 1) ? lc.q - z.w : z.w, zeta_p = (bb & 1) ? ~z.p : z.p;
-    const uint32_t aa[4] = {(uint32_t)av[0], (uint32_t)av[1], (uint32_t)av[2], (uint32_t)av[3]};
-    const uint32_t bv[4] = {y[16 * i + 4 * bb], y[16 * i + 4 * bb + 1], y[16 * i + 4 * bb + 2], y[16 * i + 4 * bb + 3]};
-    uint32_t cc[4];
-    mul_mod_x4(cc, aa, bv, zeta, zeta_p, lc.q, lc.qinv);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) y[16 * i + 4 * bb + e] = cc[e];
-  }
-  inv_h(y, rsrc(c + off, PB), lds, h, T, itw, hi4, mo);
-}
-
-// Standalone transforms in place (rnt_ntt_fwd / rnt_ntt_inv at N = 2^16).
-// STOP < 4 (debug: tools/mfma_stage_check.py): the first STOP forward
-// passes, the words written canonical at their in-place index.
-template <bool INV, int STOP = 4>
+// Standalone transforms in place (rnt_ntt_fwd / rnt_ntt_inv at N = 2^16),
+// grid (B, L): one workgroup per (poly, limb) plane.
+template <bool INV>
 __global__ void __launch_bounds__(mf::kT, 1)
 k_mf_ntt(uint32_t* __restrict__ data, const void* __restrict__ mft, const LimbConst<uint32_t>* __restrict__ lcs,
          uint64_t ls) {
@@ -950,31 +675,10 @@ k_mf_ntt(uint32_t* __restrict__ data, const void* __restrict__ mft, const LimbCo
     // the last pass stores each tile, canonical, in the device order (in
     // place: every wave read its words of the plane before the first
     // exchange's barrier)
-    fwd<false, STOP>(x, pr, lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+    fwd<false>(x, pr, lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
       bst(v4i{(int)canon(r[0], T.m.q), (int)canon(r[1], T.m.q), (int)canon(r[2], T.m.q), (int)canon(r[3], T.m.q)}, pr,
           p4_lane(h), p4_soff(h, cc));
     });
-    if constexpr (STOP == 2) {
-      __syncthreads();
-      // P2 positions, packed (untwisted)
-#pragma unroll
-      for (int cc = 0; cc < 16; ++cc)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int32_t r = (int32_t)((x[4 * cc + i] ^ K32) - K32);
-          p[(h.w << 12) | ((uint32_t)i << 10) | (h.g << 8) | ((uint32_t)cc << 4) | h.n] = canon(r % T.m.q, T.m.q);
-        }
-    } else if constexpr (STOP == 3) {
-      __syncthreads();
-      // P4 positions, packed (untwisted)
-#pragma unroll
-      for (int cc = 0; cc < 16; ++cc)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int32_t r = (int32_t)((x[p3(cc, i)] ^ K32) - K32);
-          p[((h.w << 12) | ((uint32_t)cc << 8) | (h.n << 4) | (h.g << 2)) + (uint32_t)i] = canon(r % T.m.q, T.m.q);
-        }
-    }
   } else {
 #pragma unroll
     for (int cc = 0; cc < 16; ++cc) {
@@ -982,8 +686,9 @@ k_mf_ntt(uint32_t* __restrict__ data, const void* __restrict__ mft, const LimbCo
 #pragma unroll
       for (int i = 0; i < 4; ++i) x[p3(cc, i)] = pk_canon((uint32_t)v[i]);
     }
-    __syncthreads();  // every wave has read its words before any is written back
-    inv<true>(x, pr, lds, h, T, S_I1);
+    // in place: a wave stores only after the exchanges' barriers, which it
+    // passes once it has used (so read) every word it loaded
+    inv(x, pr, lds, h, T);
   }
 }
 
@@ -1106,16 +811,6 @@ int mf_build(Tables* t, std::string* err) {
     for (int k = 0; k < 16; ++k)
       for (int j = 0; j < 16; ++j) W[k][j] = mulmod(powmod(beta1i, (uint64_t)k, q), Fi[k][j], q);
     expand(W, q, R, false, 0, slot(S_I1));
-    uint64_t Wh[16][16];
-    const uint64_t quarter_r = mulmod(R, invmod(4 % q, q), q);
-    for (int k = 0; k < 16; ++k)
-      for (int j = 0; j < 16; ++j) Wh[k][j] = mulmod(W[k][j], quarter_r, q);
-    expand(Wh, q, R, false, 0, slot(S_I1H));
-    for (int k = 0; k < 16; ++k)
-      for (int j = 0; j < 16; ++j) W[k][j] = mulmod(W[k][j], R, q);
-    expand(W, q, R, false, 0, slot(S_I1R));
-    expand(F, q, R, false, 0, slot(S_F3B));
-    expand(Fi, q, R, false, 0, slot(S_I3B));
     // input-bias compensations: the data digits carry x - 2^30
     const uint64_t bias = mulmod(R, (1ull << 30) % q, q);
     {
@@ -1131,12 +826,10 @@ int mf_build(Tables* t, std::string* err) {
       }
       int32_t* c1 = lt + (size_t)kCompF1 * 4;
       int32_t* c4 = lt + (size_t)kCompI4 * 4;
-      int32_t* c3 = lt + (size_t)kCompI3 * 4;
       for (int lam = 0; lam < 64; ++lam)
         for (int i = 0; i < 4; ++i) {
           c1[lam * 4 + i] = cf[4 * i + (lam >> 4)];
           c4[lam * 4 + i] = ci[lam & 15];
-          c3[lam * 4 + i] = ci[4 * i + (lam >> 4)];  // F^-1 as the A operand (S_I3B, kappa 4i + g)
         }
     }
     // twists (Montgomery form, centred)
@@ -1156,14 +849,6 @@ int mf_build(Tables* t, std::string* err) {
           for (int i = 0; i < 4; ++i) {
             const int U3 = (w << 4) | c;
             t3i[((w * 16 + c) * 4 + g) * 4 + i] = mr(powmod(itw[2048 + 8 * U3], (uint64_t)(4 * g + i), q));
-          }
-    int32_t* t3b = lt + (size_t)kTw3iB * 4;
-    for (int w = 0; w < 16; ++w)
-      for (int c = 0; c < 16; ++c)
-        for (int g = 0; g < 4; ++g)
-          for (int i = 0; i < 4; ++i) {
-            const int U3 = (w << 4) | c;  // P3 positions: k = bits 7..4 = 4i + g
-            t3b[((w * 16 + c) * 4 + g) * 4 + i] = mr(powmod(itw[2048 + 8 * U3], (uint64_t)(4 * i + g), q));
           }
     int32_t* t4f = lt + (size_t)kTw4f * 4;
     int32_t* t4i = lt + (size_t)kTw4i * 4;
@@ -1190,39 +875,21 @@ int mf_build(Tables* t, std::string* err) {
   return 0;
 }
 
-bool mf_ok(const Tables* t) { return t->mf != nullptr && t->plane == 5; }
-
-hipError_t launch_mf_mul(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls) {
-  if (k.B == 0 || k.L == 0) return hipSuccess;
-  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
-  hipError_t e = hipFuncSetAttribute((const void*)k_mf_mul, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mf::kLdsBytes);
+static hipError_t launch_ntt_t(const Launch& k, const void* fn, void* data, uint64_t ls) {
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mf::kLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_mf_mul, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), mf::kLdsBytes, k.s, (uint32_t*)out,
-                     (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)scratch, (const void*)k.t->mf,
-                     tab_ptrs<uint32_t>(k.t), ls);
-  return hipGetLastError();
+  uint32_t* d = (uint32_t*)data;
+  const void* mft = k.t->mf;
+  const LimbConst<uint32_t>* lcs = (const LimbConst<uint32_t>*)k.t->lconst;
+  void* args[] = {&d, &mft, &lcs, &ls};
+  return hipLaunchKernel(fn, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), args, mf::kLdsBytes, k.s);
 }
 
-template <bool INV, int STOP>
-static hipError_t launch_ntt_t(const Launch& k, void* data, uint64_t ls) {
-  hipError_t e = hipFuncSetAttribute((const void*)k_mf_ntt<INV, STOP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)mf::kLdsBytes);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_mf_ntt<INV, STOP>), dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), mf::kLdsBytes, k.s,
-                     (uint32_t*)data, (const void*)k.t->mf, (const LimbConst<uint32_t>*)k.t->lconst, ls);
-  return hipGetLastError();
-}
-
-// stop: 4 = the whole transform; 1..3 = the debug prefixes (forward only)
-hipError_t launch_mf_ntt(const Launch& k, int inverse, void* data, uint64_t ls, int stop) {
+hipError_t launch_mf_ntt(const Launch& k, int inverse, void* data, uint64_t ls) {
   if (k.B == 0 || k.L == 0) return hipSuccess;
   if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
-  if (inverse) return launch_ntt_t<true, 4>(k, data, ls);
-  switch (stop) {
-    case 2: return launch_ntt_t<false, 2>(k, data, ls);
-    case 3: return launch_ntt_t<false, 3>(k, data, ls);
-    default: return launch_ntt_t<false, 4>(k, data, ls);
-  }
+  return inverse ? launch_ntt_t(k, (const void*)k_mf_ntt<true>, data, ls)
+                 : launch_ntt_t(k, (const void*)k_mf_ntt<false>, data, ls);
 }
 
 }  // namespace rnt

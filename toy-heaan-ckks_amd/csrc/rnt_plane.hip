@@ -8,7 +8,6 @@
 // same (and the reference's).
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
 #include <type_traits>
 
 #include "rnt_internal.hpp"
@@ -20,15 +19,14 @@ namespace rnt {
 
 // ---- whole-plane product (rnt_mul at N = 2^16, u32 canonical bases) ------
 // 5 planes of HBM traffic per (poly, limb) instead of the four-step path's
-// 9.  The shipped form is one launch, k_plane_fused: a
-// workgroup transforms a, writes a^ to a scratch plane in a private layout,
-// transforms b, reads a^ back (pipelined 4 blocks ahead), forms the degree-3
-// block products and runs the inverse, storing c.  k_plane_fwd + k_plane_mul
-// split the same work over two launches (RNT_PLANE=1), k_plane_fused_p is the
-// persistent form (RNT_PLANE=4).  The butterflies run as 4-way interleaved
-// inline asm (rnt_bfly4.hpp; the kernel is bound by VALU issue), pass C's
-// twiddles are loaded ahead of X2, and X1 runs in its two rounds with pass B
-// (gs B) of one register half between them.
+// 9, in one launch, k_plane_fused: a workgroup transforms
+// a, writes a^ to a scratch plane in a private layout, transforms b, reads a^
+// back (pipelined 4 blocks ahead), forms the degree-3 block products and runs
+// the inverse, storing c.  The butterflies run as 4-way interleaved inline
+// asm (rnt_bfly4.hpp; the kernel is bound by VALU issue), pass C's twiddles
+// are loaded ahead of X2, and X1 runs in its two rounds with pass B (gs B) of
+// one register half between them.  (The standalone transforms at this size
+// are rnt_mfma.hip's.)
 // A workgroup = 1024 threads holds one 2^16-word plane, 64 words a thread.
 // Thread t = (w << 6) | lam (wave w, lane lam); the 16-bit index i is split
 // three ways:
@@ -49,9 +47,6 @@ namespace rnt {
 //      buffer in four rounds, with no workgroup barrier.
 // The physical register of a logical one is a compile-time permutation
 // (slot1, shared by L1 and L2).
-#ifndef RNT_PLANE_EXP
-#define RNT_PLANE_EXP 0
-#endif
 namespace plane {
 constexpr int T = 1024;
 constexpr int XS = 17;                  // X2 buffer row stride (words): conflict-free both ways
@@ -67,60 +62,11 @@ __host__ __device__ constexpr int slot(int r) {
 }
 }  // namespace plane
 
-// Butterflies as interleaved groups of four in inline asm (rnt_bfly4.hpp):
-// 1 (default) or 0 (the C++ butterflies of rnt_modarith.hpp, A/B).
-#ifndef RNT_PLANE_ASM
-#define RNT_PLANE_ASM 1
-#endif
-// Cache policy (buffer aux bits) of the streamed operand loads and the
-// product store: 0 default, 2 non-temporal (A/B knob, -DRNT_PLANE_AUX=2).
-#ifndef RNT_PLANE_AUX
-#define RNT_PLANE_AUX 0
-#endif
-constexpr int kPlaneAux = RNT_PLANE_AUX;
-// plane loads in pass A's first-stage order (1) or register order (0)
-#ifndef RNT_PLANE_LOAD_ORDER
-#define RNT_PLANE_LOAD_ORDER 1
-#endif
-constexpr bool kPlaneLoadOrder = RNT_PLANE_LOAD_ORDER != 0;
-// b's loads issued ahead of a^'s stores (0: none)
-#ifndef RNT_PLANE_BEARLY
-#define RNT_PLANE_BEARLY 0
-#endif
-constexpr int kPlaneBEarly = RNT_PLANE_BEARLY;
-// Twiddles per scalar-load chunk in pass A (64 SGPRs at 32)
-#ifndef RNT_PLANE_CHA
-#define RNT_PLANE_CHA 32
-#endif
-constexpr int kPlaneChA = RNT_PLANE_CHA;
-// a^ blocks in flight ahead of the degree-3 block products (0: loaded at use)
-#ifndef RNT_PLANE_AHD
-#define RNT_PLANE_AHD 4
-#endif
-constexpr int kPlaneAhd = RNT_PLANE_AHD;
-// X1 through 8-byte LDS words (1) or 4-byte ones (0, default: the 8-byte
-// form measured flat, profiles/r03/ab_plane_x1wide_preg.txt)
-#ifndef RNT_PLANE_X1W
-#define RNT_PLANE_X1W 0
-#endif
-constexpr bool kPlaneX1Wide = RNT_PLANE_X1W != 0;
-// X1 in two rounds with pass B (gs B) of one half between them (1, needs
-// the asm butterflies, which can run one half of the L1 registers) or as
-// one exchange (0)
-#ifndef RNT_PLANE_X1SPLIT
-#define RNT_PLANE_X1SPLIT 1
-#endif
-constexpr bool kPlaneX1Split = RNT_PLANE_X1SPLIT != 0 && RNT_PLANE_ASM != 0;
+// Tuning constants (each measured against its alternatives):
+// twiddles per scalar-load chunk in pass A (64 SGPRs) and pass B, per
+// per-lane chunk in pass C; a^ blocks in flight ahead of the block products.
+constexpr int kPlaneChA = 32, kPlaneChB = 16, kPlaneChC = 8, kPlaneAhd = 4;
 
-// Pass C's per-thread twiddles (stages at index bits 5..2: 1, 2, 4 and 8
-// of them), loaded ahead of the X2 exchange so the loads are in flight
-// during it instead of stalling each stage of the pass.
-#ifndef RNT_PLANE_PREC
-#define RNT_PLANE_PREC 3  // forward pass C stages whose twiddles are preloaded (0..4)
-#endif
-#ifndef RNT_PLANE_PREG
-#define RNT_PLANE_PREG 0  // inverse pass C stages preloaded (0..4; 1 measured flat)
-#endif
 // Pass C's per-thread twiddles (stages at index bits 5..2: 1, 2, 4 and 8 of
 // them), the stages in MASK (bit SL - 2) loaded ahead: before the X2
 // exchange in the forward transforms, during the last block products in the
@@ -150,9 +96,10 @@ __device__ __forceinline__ TwPre<MASK> plane_pre(const Tw<uint32_t>* b, uint32_t
   }
   return p;
 }
-// Forward: the first PREC stages (5, 4, ...); inverse: the first PREG (2, 3, ...).
-constexpr int kPreFwd = (0xF0 >> RNT_PLANE_PREC) & 0xF;
-constexpr int kPreInv = (1 << RNT_PLANE_PREG) - 1;
+// Forward: the first three stages (5, 4, 3); inverse: none (preloading its
+// first stage measured flat).
+constexpr int kPreFwd = 0xE;
+constexpr int kPreInv = 0;
 // Twiddle m of a stage chunk at index bit SL (+ BB): from the source, or
 // from the preloaded set.
 template <int SL, class TS>
@@ -265,15 +212,12 @@ __device__ __forceinline__ TwChunk<n> plane_chunk(const TS& tw, uint32_t nb) {
   TwChunk<n> c;
 #pragma unroll
   for (int j = 0; j < n; ++j)
-    c.t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<SLB>(tw, nb, (uint32_t)(M0 + j));
+    c.t[j] = tw_fetch<SLB>(tw, nb, (uint32_t)(M0 + j));
   return c;
 }
-#ifndef RNT_PLANE_TPIPE
-#define RNT_PLANE_TPIPE 1
-#endif
 template <int LY, int SL, int M0, int CH>
 constexpr bool chunk_pipe() {
-  return RNT_PLANE_TPIPE != 0 && LY == 2 && M0 + CH < (32 >> SL);
+  return LY == 2 && M0 + CH < (32 >> SL);
 }
 
 // CT stages on logical register bits SLHI .. SLLO of layout LY (index bits
@@ -295,39 +239,24 @@ __device__ __forceinline__ void plane_ct_chunks(uint32_t (&x)[64], uint32_t nb, 
   } else {
 #pragma unroll
     for (int j = 0; j < n; ++j)
-      t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<BB + SL>(tw, nb, (uint32_t)(M0 + j));
+      t[j] = tw_fetch<BB + SL>(tw, nb, (uint32_t)(M0 + j));
   }
-  if constexpr (RNT_PLANE_ASM != 0) {
-    constexpr bool SW = tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0;
-    constexpr int n2 = (cnt - M0 - CH) < CH ? (cnt - M0 - CH) : CH;
-    TwChunk<(n2 > 0 ? n2 : 1)> nxt;
-    if constexpr (chunk_pipe<LY, SL, M0, CH>()) nxt = plane_chunk<BB + SL, M0 + CH, (n2 > 0 ? n2 : 1)>(tw, nb);
-    if constexpr (SL > SLLO) {
-      plane_ct_groups<LY, SL, M0, d / 2, false, SW, HM>(x, t, mo);
-      plane_ct_groups<LY, SL, M0, d / 2, true, SW, HM>(x, t, mo);
-    } else {
-      plane_ct_groups<LY, SL, M0, d, false, SW, HM>(x, t, mo);
-    }
-    if constexpr (M0 + CH < cnt) {
-      if constexpr (chunk_pipe<LY, SL, M0, CH>())
-        plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH, HM, TS, (n2 > 0 ? n2 : 1)>(x, nb, tw, mo, &nxt);
-      else
-        plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH, HM>(x, nb, tw, mo);
-    }
-    return;
+  constexpr bool SW = tw_uniform<TS>();
+  constexpr int n2 = (cnt - M0 - CH) < CH ? (cnt - M0 - CH) : CH;
+  TwChunk<(n2 > 0 ? n2 : 1)> nxt;
+  if constexpr (chunk_pipe<LY, SL, M0, CH>()) nxt = plane_chunk<BB + SL, M0 + CH, (n2 > 0 ? n2 : 1)>(tw, nb);
+  if constexpr (SL > SLLO) {
+    plane_ct_groups<LY, SL, M0, d / 2, false, SW, HM>(x, t, mo);
+    plane_ct_groups<LY, SL, M0, d / 2, true, SW, HM>(x, t, mo);
+  } else {
+    plane_ct_groups<LY, SL, M0, d, false, SW, HM>(x, t, mo);
   }
-#pragma unroll
-  for (int j = 0; j < n; ++j) {
-#pragma unroll
-    for (int e = 0; e < d; ++e) {
-      const int i = ((M0 + j) << (SL + 1)) | e;
-      if (SL > SLLO && (i & (d >> 1)))
-        ct_bfly_lazy(x[plane::slot<LY>(i)], x[plane::slot<LY>(i | d)], t[j].w, t[j].p, mo);
-      else
-        ct_bfly(x[plane::slot<LY>(i)], x[plane::slot<LY>(i | d)], t[j].w, t[j].p, mo);
-    }
+  if constexpr (M0 + CH < cnt) {
+    if constexpr (chunk_pipe<LY, SL, M0, CH>())
+      plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH, HM, TS, (n2 > 0 ? n2 : 1)>(x, nb, tw, mo, &nxt);
+    else
+      plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH, HM>(x, nb, tw, mo);
   }
-  if constexpr (M0 + CH < cnt) plane_ct_chunks<LY, BB, SL, SLLO, M0 + CH, CH>(x, nb, tw, mo);
 }
 template <int LY, int BB, int SL, int SLLO, int CH, int HM = -1, class TS>
 __device__ __forceinline__ void plane_ct(uint32_t (&x)[64], uint32_t node0, const TS& tw,
@@ -342,7 +271,7 @@ __device__ __forceinline__ void plane_ct(uint32_t (&x)[64], uint32_t node0, cons
 template <int LY, int BB, int SL, int M0, int CH, int HM = -1, class TS, int NP = 1>
 __device__ __forceinline__ void plane_gs_chunks(uint32_t (&x)[64], uint32_t nb, const TS& itw,
                                                 const Mod<uint32_t>& mo, const TwChunk<NP>* pre = nullptr) {
-  constexpr int d = 1 << SL, cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
+  constexpr int cnt = 32 >> SL, n = (cnt - M0) < CH ? (cnt - M0) : CH;
   Tw<uint32_t> t[n];
   if constexpr (NP == n && M0 > 0) {
 #pragma unroll
@@ -350,30 +279,18 @@ __device__ __forceinline__ void plane_gs_chunks(uint32_t (&x)[64], uint32_t nb, 
   } else {
 #pragma unroll
     for (int j = 0; j < n; ++j)
-      t[j] = (RNT_PLANE_EXP & 8) ? Tw<uint32_t>{12345u + (uint32_t)j, 54321u} : tw_fetch<BB + SL>(itw, nb, (uint32_t)(M0 + j));
+      t[j] = tw_fetch<BB + SL>(itw, nb, (uint32_t)(M0 + j));
   }
-  if constexpr (RNT_PLANE_ASM != 0) {
-    constexpr int n2 = (cnt - M0 - CH) < CH ? (cnt - M0 - CH) : CH;
-    TwChunk<(n2 > 0 ? n2 : 1)> nxt;
-    if constexpr (chunk_pipe<LY, SL, M0, CH>()) nxt = plane_chunk<BB + SL, M0 + CH, (n2 > 0 ? n2 : 1)>(itw, nb);
-    plane_gs_groups<LY, SL, M0, tw_uniform<TS>() || (RNT_PLANE_EXP & 8) != 0, HM>(x, t, mo);
-    if constexpr (M0 + CH < cnt) {
-      if constexpr (chunk_pipe<LY, SL, M0, CH>())
-        plane_gs_chunks<LY, BB, SL, M0 + CH, CH, HM, TS, (n2 > 0 ? n2 : 1)>(x, nb, itw, mo, &nxt);
-      else
-        plane_gs_chunks<LY, BB, SL, M0 + CH, CH, HM>(x, nb, itw, mo);
-    }
-    return;
+  constexpr int n2 = (cnt - M0 - CH) < CH ? (cnt - M0 - CH) : CH;
+  TwChunk<(n2 > 0 ? n2 : 1)> nxt;
+  if constexpr (chunk_pipe<LY, SL, M0, CH>()) nxt = plane_chunk<BB + SL, M0 + CH, (n2 > 0 ? n2 : 1)>(itw, nb);
+  plane_gs_groups<LY, SL, M0, tw_uniform<TS>(), HM>(x, t, mo);
+  if constexpr (M0 + CH < cnt) {
+    if constexpr (chunk_pipe<LY, SL, M0, CH>())
+      plane_gs_chunks<LY, BB, SL, M0 + CH, CH, HM, TS, (n2 > 0 ? n2 : 1)>(x, nb, itw, mo, &nxt);
+    else
+      plane_gs_chunks<LY, BB, SL, M0 + CH, CH, HM>(x, nb, itw, mo);
   }
-#pragma unroll
-  for (int j = 0; j < n; ++j) {
-#pragma unroll
-    for (int e = 0; e < d; ++e) {
-      const int i = ((M0 + j) << (SL + 1)) | e;
-      gs_bfly(x[plane::slot<LY>(i)], x[plane::slot<LY>(i | d)], t[j].w, t[j].p, mo);
-    }
-  }
-  if constexpr (M0 + CH < cnt) plane_gs_chunks<LY, BB, SL, M0 + CH, CH>(x, nb, itw, mo);
 }
 template <int LY, int BB, int SL, int SLHI, int CH, bool FOLD, int HM = -1, class TS>
 __device__ __forceinline__ void plane_gs(uint32_t (&x)[64], uint32_t node0, const TS& itw,
@@ -392,76 +309,16 @@ __device__ __forceinline__ void plane_gs(uint32_t (&x)[64], uint32_t node0, cons
   if constexpr (SL < SLHI) plane_gs<LY, BB, SL + 1, SLHI, CH, FOLD, HM>(x, node0, itw, mo, f);
 }
 
-// X1, L0 <-> L1 through LDS.  Round h carries the words with index bit
-// 10 == h: L0 registers 2k + h, L1 logical registers r1 = ((k >> 4) << 5) |
-// (h << 4) | (k & 15), both in physical register 2k + h.  LDS word = the 15
-// other index bits; every access is 64 consecutive words per wave.
-// SYNC_FIRST: other waves may still be reading their X2 buffers.
-template <bool TO_L1, bool SYNC_FIRST>
-__device__ __forceinline__ void plane_x1(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
-  const uint32_t w = t >> 6, lam = t & 63u;
-  if constexpr ((RNT_PLANE_EXP & 16) != 0) return;
-  if constexpr (SYNC_FIRST) __syncthreads();
-  if constexpr (kPlaneX1Wide) {
-    // 8-byte LDS words: pairs differing in index bit 11, a register bit on
-    // both sides (L0 registers 4m + h, 4m + 2 + h; L1 registers 2k + h,
-    // 2k + 32 + h); pair address = the index without bits 10 and 11.
-    // ds_write_b64 / ds_read_b64 move 85 / 256 B per clock against 64 / 128
-    // for the 4-byte forms, and every access stays 16 (32) consecutive pairs
-    // per lane group: conflict-free.
-    uint2* lp = (uint2*)lds;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        if constexpr (TO_L1)
-          lp[((uint32_t)m << 10) | t] = make_uint2(x[4 * m + h], x[4 * m + 2 + h]);
-        else
-          lp[(w << 10) | ((uint32_t)m << 6) | lam] = make_uint2(x[2 * m + h], x[2 * m + 32 + h]);
-      }
-      __syncthreads();
-#pragma unroll
-      for (int m = 0; m < 16; ++m) {
-        if constexpr (TO_L1) {
-          const uint2 v = lp[(w << 10) | ((uint32_t)m << 6) | lam];
-          x[2 * m + h] = v.x;
-          x[2 * m + 32 + h] = v.y;
-        } else {
-          const uint2 v = lp[((uint32_t)m << 10) | t];
-          x[4 * m + h] = v.x;
-          x[4 * m + 2 + h] = v.y;
-        }
-      }
-      __syncthreads();
-    }
-    return;
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const uint32_t j0 = ((uint32_t)k << 10) | t;
-      const uint32_t j1 = ((((w << 1) | ((uint32_t)k >> 4))) << 10) | (((uint32_t)k & 15u) << 6) | lam;
-      lds[TO_L1 ? j0 : j1] = x[2 * k + h];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const uint32_t j0 = ((uint32_t)k << 10) | t;
-      const uint32_t j1 = ((((w << 1) | ((uint32_t)k >> 4))) << 10) | (((uint32_t)k & 15u) << 6) | lam;
-      x[2 * k + h] = lds[TO_L1 ? j1 : j0];
-    }
-    __syncthreads();
-  }
-}
-
-// One round of X1 (4-byte words), as plane_x1: WRITE puts round H's
-// registers into LDS, !WRITE takes them out.  plane_fwd / plane_mul_tail
-// split X1 into these so that pass B (gs B) of the half already delivered
-// (still to be sent) runs while the other round's LDS traffic drains.
+// X1, L0 <-> L1 through LDS, in two rounds: round h carries the words with
+// index bit 10 == h: L0 registers 2k + h, L1 logical registers r1 =
+// ((k >> 4) << 5) | (h << 4) | (k & 15), both in physical register 2k + h.
+// LDS word = the 15 other index bits; every access is 64 consecutive words
+// per wave.  (8-byte LDS words measured flat, profiles/r03/ab_plane_x1wide_preg.txt.)
+// WRITE puts round H's registers into LDS, !WRITE takes them out; plane_fwd
+// / plane_inv_tail run pass B (gs B) of the half already delivered (still to
+// be sent) while the other round's LDS traffic drains.
 template <bool TO_L1, int H, bool WRITE>
 __device__ __forceinline__ void plane_x1_round(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
-  if constexpr ((RNT_PLANE_EXP & 16) != 0) return;
   const uint32_t w = t >> 6, lam = t & 63u;
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
@@ -473,9 +330,7 @@ __device__ __forceinline__ void plane_x1_round(uint32_t (&x)[64], uint32_t* lds,
       x[2 * k + H] = lds[TO_L1 ? j1 : j0];
   }
 }
-__device__ __forceinline__ void plane_sync() {
-  if constexpr ((RNT_PLANE_EXP & 16) == 0) __syncthreads();
-}
+__device__ __forceinline__ void plane_sync() { __syncthreads(); }
 
 // Lane bit 5 <-> L1 register bit 5 and lane bit 4 <-> register bit 4
 // (self-inverse; the two commute).
@@ -507,7 +362,6 @@ __device__ __forceinline__ void plane_swap54(uint32_t (&x)[64]) {
 template <bool TO_L2>
 __device__ __forceinline__ void plane_x2(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
   const uint32_t w = t >> 6, lam = t & 63u;
-  if constexpr ((RNT_PLANE_EXP & 16) != 0) return;
   if constexpr (TO_L2) plane_swap54(x);
   const uint32_t a15 = lam * plane::XS;                          // + (m & 15)
   const uint32_t a2 = (lam & 48u) * plane::XS + (lam & 15u);     // + c * XS
@@ -522,21 +376,6 @@ __device__ __forceinline__ void plane_x2(uint32_t (&x)[64], uint32_t* lds, uint3
     __builtin_amdgcn_wave_barrier();
   }
   if constexpr (!TO_L2) plane_swap54(x);
-}
-
-// One workgroup per CU and equal work per workgroup keep every CU's load,
-// compute and store phases in step across the chip, so the loads of all
-// CUs meet at the HBM together while the VALUs idle, and then the other
-// way round.  Delaying the first workgroup of every other CU by `ticks`
-// of the 100 MHz real-time counter once shifts that CU's phase for the
-// rest of the launch (its next workgroups start when the previous one
-// ends), so half the CUs load while the other half compute.
-__device__ __forceinline__ void plane_stagger(uint32_t ticks) {
-  if (ticks == 0) return;
-  const uint32_t id = blockIdx.x + blockIdx.y * gridDim.x;
-  if (id >= 256u || !((id >> 3) & 1u)) return;  // first wave, every other CU of each XCD
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
 // Phase timeline of the plane kernels (measurement build only:
@@ -562,35 +401,13 @@ __device__ uint64_t g_plane_trace[2 * kTraceWg * 16 * kTraceStamps];
   } while (0)
 #endif
 
-// Measurement builds (tools/build_variant.sh, wrong results by design):
-// RNT_PLANE_EXP bit 0: pass C / inverse pass C twiddles wave-uniform;
-// bit 1: no plane loads (synthetic words); bit 2: no plane stores;
-// bit 3: no twiddle loads in the passes (one constant); bit 4: no X1 / X2;
-// bit 5: no product store; bit 6: no a^ store (the a^ loads stay).
-
-// ... and in pass B (wave-uniform too)
-#ifndef RNT_PLANE_CHB
-#define RNT_PLANE_CHB 16
-#endif
-constexpr int kPlaneChB = RNT_PLANE_CHB;
-// twiddles per chunk in pass C (per-lane twiddles)
-#ifndef RNT_PLANE_CHC
-#define RNT_PLANE_CHC 8
-#endif
-constexpr int kPlaneChC = RNT_PLANE_CHC;
-
 // Register of the q-th plane load.
 __host__ __device__ constexpr int plane_load_reg(int q) {
-  return kPlaneLoadOrder ? (((q >> 3) << 2) | (q & 3)) + ((q & 4) ? 32 : 0) : q;
+  return (((q >> 3) << 2) | (q & 3)) + ((q & 4) ? 32 : 0);
 }
 
 // Load the L0 plane at src (64 coalesced dword loads a thread).
 __device__ __forceinline__ void plane_load(uint32_t (&x)[64], const uint32_t* src, uint32_t t) {
-  if constexpr ((RNT_PLANE_EXP & 2) != 0) {
-#pragma unroll
-    for (int r = 0; r < 64; ++r) x[r] = (t * 2654435761u + (uint32_t)r * 40503u) >> 2;
-    return;
-  }
   const __amdgpu_buffer_rsrc_t g = __builtin_amdgcn_make_buffer_rsrc((void*)src, 0, (int)(4u << 16), 0x00020000);
   // in the order pass A's first stage consumes them (groups of four pairs
   // r, r + 32), so its butterflies start while the rest of the plane is
@@ -598,20 +415,8 @@ __device__ __forceinline__ void plane_load(uint32_t (&x)[64], const uint32_t* sr
 #pragma unroll
   for (int q = 0; q < 64; ++q) {
     const int r = plane_load_reg(q);
-    x[r] = __builtin_amdgcn_raw_buffer_load_b32(g, t * 4u, (uint32_t)r << 12, kPlaneAux);
+    x[r] = __builtin_amdgcn_raw_buffer_load_b32(g, t * 4u, (uint32_t)r << 12, 0);
   }
-}
-
-// The CU this workgroup runs on, as a dense id below kPlaneSlots: XCC_ID
-// (hwreg 20, bits 3:0) and HW_ID's SE_ID (15:13), SH_ID (12), CU_ID (11:8).
-// The plane kernels use 139 KiB of LDS and the whole register file, so a CU
-// runs one of their workgroups at a time: while it runs, the id names a
-// scratch slot no other workgroup of the launch uses.
-constexpr uint32_t kPlaneSlots = 1u << 12;
-__device__ __forceinline__ uint32_t plane_cu_slot() {
-  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
-  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
-  return ((xcc & 15u) << 8) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 15u);
 }
 
 // The truncated forward transform of the plane in x (L0 in, L2 out).
@@ -644,7 +449,7 @@ struct NoHook {
 };
 // AFTER_X1 / AFTER_X2 run right after the exchanges (prefetches of the next
 // operand: issued there, they are in flight during the passes that follow).
-template <int K, bool SYNC1, class H1 = NoHook, class H2 = NoHook, bool FULL = false>
+template <int K, bool SYNC1, class H1 = NoHook, class H2 = NoHook>
 __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint32_t t,
                                           const Tw<uint32_t>* tw, const Mod<uint32_t>& mo, uint32_t trace_id,
                                           const H1& after_x1 = H1{}, const H2& after_x2 = H2{}) {
@@ -657,88 +462,64 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   plane_ct<0, 10, 5, 0, kPlaneChA>(x, N, tws, mo);
   PLANE_STAMP(K, 2);
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
-  if constexpr (kPlaneX1Split) {
-    // X1 in its two rounds, pass B of round 0's half while round 1 drains
-    if constexpr (SYNC1) plane_sync();
-    plane_x1_round<true, 0, true>(x, lds, t);
-    plane_sync();
-    plane_x1_round<true, 0, false>(x, lds, t);
-    plane_sync();
-    plane_x1_round<true, 1, true>(x, lds, t);
-    PLANE_STAMP(K, 3);
-    after_x1();
-    plane_ct<1, 6, 3, 0, kPlaneChB, 0>(x, N + (wu << 12), tws, mo);
-    plane_sync();
-    plane_x1_round<true, 1, false>(x, lds, t);
-    plane_ct<1, 6, 3, 0, kPlaneChB, 1>(x, N + (wu << 12), tws, mo);
-    plane_sync();  // X2's buffers overlap the X1 region
-  } else {
-    plane_x1<true, SYNC1>(x, lds, t);
-    PLANE_STAMP(K, 3);
-    after_x1();
-    plane_ct<1, 6, 3, 0, kPlaneChB>(x, N + (wu << 12), tws, mo);
-  }
+  // X1 in its two rounds, pass B of round 0's half while round 1 drains
+  if constexpr (SYNC1) plane_sync();
+  plane_x1_round<true, 0, true>(x, lds, t);
+  plane_sync();
+  plane_x1_round<true, 0, false>(x, lds, t);
+  plane_sync();
+  plane_x1_round<true, 1, true>(x, lds, t);
+  PLANE_STAMP(K, 3);
+  after_x1();
+  plane_ct<1, 6, 3, 0, kPlaneChB, 0>(x, N + (wu << 12), tws, mo);
+  plane_sync();
+  plane_x1_round<true, 1, false>(x, lds, t);
+  plane_ct<1, 6, 3, 0, kPlaneChB, 1>(x, N + (wu << 12), tws, mo);
+  plane_sync();  // X2's buffers overlap the X1 region
   PLANE_STAMP(K, 4);
   const auto pc = plane_pre<kPreFwd>(tw, N + (t << 6));
   plane_x2<true>(x, lds, t);
   PLANE_STAMP(K, 5);
   after_x2();
-  // pass C: bits 5..2 for the product (bits 1..0 are its truncated
-  // stages), bits 5..0 for a standalone transform (FULL)
-  constexpr int SLLO_C = FULL ? 0 : 2;
-  if constexpr ((RNT_PLANE_EXP & 1) != 0)
-    plane_ct<2, 0, 5, SLLO_C, kPlaneChC>(x, N, tws, mo);
-  else
-    plane_ct<2, 0, 5, SLLO_C, kPlaneChC>(x, N + (t << 6), pc, mo);
+  // pass C: bits 5..2 (bits 1..0 are the product's truncated stages)
+  plane_ct<2, 0, 5, 2, kPlaneChC>(x, N + (t << 6), pc, mo);
   PLANE_STAMP(K, 6);
 }
 
 // The inverse transform from pass C's layout (L2) to the store of c in L0:
-// gs C on bits SLLO_C..5 (2 after a truncated product, 0 for a standalone
-// transform), X2, gs B, X1 (split as the forward one), gs A with the folded
-// last-stage constants F (4/N with the Montgomery factor after a product,
-// 1/N for a standalone transform).
-template <int K, int SLLO_C, class TSC>
+// gs C on bits 2..5, X2, gs B, X1 (split as the forward one), gs A with the
+// folded last-stage constants F (4/N with the Montgomery factor).
+template <int K, class TSC>
 __device__ __forceinline__ void plane_inv_tail(uint32_t (&x)[64], uint32_t* lds, uint32_t t, uint32_t* c,
                                                const Tw<uint32_t>* itw, const TSC& gsrc, const Mod<uint32_t>& mo,
                                                const Fold<uint32_t>& F, uint32_t trace_id) {
   (void)trace_id;
   const uint32_t n0 = 1u << 16;
   const TwScalar<uint32_t> itws{(const RNT_CONST_AS Tw<uint32_t>*)itw};
-  if constexpr ((RNT_PLANE_EXP & 1) != 0)
-    plane_gs<2, 0, SLLO_C, 5, kPlaneChC, false>(x, n0, itws, mo, Fold<uint32_t>{});
-  else
-    plane_gs<2, 0, SLLO_C, 5, kPlaneChC, false>(x, n0 + (t << 6), gsrc, mo, Fold<uint32_t>{});
+  plane_gs<2, 0, 2, 5, kPlaneChC, false>(x, n0 + (t << 6), gsrc, mo, Fold<uint32_t>{});
   PLANE_STAMP(K, 8);
   plane_x2<false>(x, lds, t);
   PLANE_STAMP(K, 9);
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
-  if constexpr (kPlaneX1Split) {
-    // gs B of round 0's half, X1 round 0 written while gs B of the other half runs
-    plane_gs<1, 6, 0, 3, kPlaneChB, false, 0>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
-    plane_sync();  // other waves may still be in their X2
-    plane_x1_round<false, 0, true>(x, lds, t);
-    plane_gs<1, 6, 0, 3, kPlaneChB, false, 1>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
-    PLANE_STAMP(K, 10);
-    plane_sync();
-    plane_x1_round<false, 0, false>(x, lds, t);
-    plane_sync();
-    plane_x1_round<false, 1, true>(x, lds, t);
-    plane_sync();
-    plane_x1_round<false, 1, false>(x, lds, t);
-    plane_sync();
-  } else {
-    plane_gs<1, 6, 0, 3, kPlaneChB, false>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
-    PLANE_STAMP(K, 10);
-    plane_x1<false, true>(x, lds, t);  // other waves may still be in their X2
-  }
+  // gs B of round 0's half, X1 round 0 written while gs B of the other half runs
+  plane_gs<1, 6, 0, 3, kPlaneChB, false, 0>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+  plane_sync();  // other waves may still be in their X2
+  plane_x1_round<false, 0, true>(x, lds, t);
+  plane_gs<1, 6, 0, 3, kPlaneChB, false, 1>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+  PLANE_STAMP(K, 10);
+  plane_sync();
+  plane_x1_round<false, 0, false>(x, lds, t);
+  plane_sync();
+  plane_x1_round<false, 1, true>(x, lds, t);
+  plane_sync();
+  plane_x1_round<false, 1, false>(x, lds, t);
+  plane_sync();
   PLANE_STAMP(K, 11);
   plane_gs<0, 10, 0, 5, kPlaneChA, true>(x, n0, itws, mo, F);
   PLANE_STAMP(K, 12);
-  if ((RNT_PLANE_EXP & (4 | 32)) != 0 && x[0] != 0xffffffffu) return;
   const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc((void*)c, 0, (int)(4u << 16), 0x00020000);
 #pragma unroll
-  for (int r = 0; r < 64; ++r) __builtin_amdgcn_raw_buffer_store_b32(x[r], dst, t * 4u, (uint32_t)r << 12, kPlaneAux);
+  for (int r = 0; r < 64; ++r) __builtin_amdgcn_raw_buffer_store_b32(x[r], dst, t * 4u, (uint32_t)r << 12, 0);
   PLANE_STAMP(K, 13);
 }
 
@@ -758,36 +539,23 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
   // a^ blocks and zeta twiddles are loaded AHD blocks ahead of their use
   // (pinned by scheduling barriers: left to itself hipcc issues each load
   // just before its product, so every block waits out a memory latency)
-  constexpr int D = kPlaneAhd, Z = D > 0 ? (D + 1) / 2 + 1 : 1;  // zeta j serves blocks 2j, 2j + 1
-  uint4 abuf[D > 0 ? D : 1];
+  constexpr int D = kPlaneAhd, Z = (D + 1) / 2 + 1;  // zeta j serves blocks 2j, 2j + 1
+  uint4 abuf[D];
   Tw<uint32_t> zbuf[Z];
   TwPre<kPreInv> gpre;  // the inverse pass C's first stages, loaded during the last products
-  if constexpr (D == 0) gpre = plane_pre<kPreInv>(itw, n0 + (t << 6));
-  if constexpr (D > 0) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) abuf[d] = ah(d);
+  for (int d = 0; d < D; ++d) abuf[d] = ah(d);
 #pragma unroll
-    for (int j = 0; j < Z; ++j) zbuf[j] = tw[zb + j];
-    __builtin_amdgcn_sched_barrier(0);
-  }
+  for (int j = 0; j < Z; ++j) zbuf[j] = tw[zb + j];
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk) {
-    uint4 av;
-    Tw<uint32_t> w;
-    if constexpr ((RNT_PLANE_EXP & 2) != 0) {
-      av = make_uint4(t * 7u + kk, t * 11u, t + 3u * kk, t ^ 0x55u);
-      w = tw[zb + (kk >> 1)];
-    } else if constexpr (D > 0) {
-      av = abuf[kk % D];
-      w = zbuf[(kk >> 1) % Z];
-      if (kk + D < 16) abuf[kk % D] = ah(kk + D);
-      if (kk == 16 - D) gpre = plane_pre<kPreInv>(itw, n0 + (t << 6));
-      if ((kk & 1) && (kk >> 1) + Z < 8) zbuf[(kk >> 1) % Z] = tw[zb + (kk >> 1) + Z];
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-      av = ah(kk);
-      w = tw[zb + (kk >> 1)];
-    }
+    const uint4 av = abuf[kk % D];
+    const Tw<uint32_t> w = zbuf[(kk >> 1) % Z];
+    if (kk + D < 16) abuf[kk % D] = ah(kk + D);
+    if (kk == 16 - D) gpre = plane_pre<kPreInv>(itw, n0 + (t << 6));
+    if ((kk & 1) && (kk >> 1) + Z < 8) zbuf[(kk >> 1) % Z] = tw[zb + (kk >> 1) + Z];
+    __builtin_amdgcn_sched_barrier(0);
     const uint32_t aa[4] = {av.x, av.y, av.z, av.w};
     const uint32_t bb[4] = {x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
                             x[plane::slot2(4 * kk + 3)]};
@@ -799,68 +567,22 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
     for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = cc[e];
   }
   PLANE_STAMP(K, 7);
-  plane_inv_tail<K, 2>(x, lds, t, c, itw, gpre, mo, Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p}, trace_id);
+  plane_inv_tail<K>(x, lds, t, c, itw, gpre, mo, Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p}, trace_id);
 }
 
 // a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
 __device__ __forceinline__ void plane_store_hat(const HatBuf& dst, const uint32_t (&x)[64], uint32_t t) {
-  if ((RNT_PLANE_EXP & (4 | 64)) != 0 && x[0] != 0xffffffffu) return;
 #pragma unroll
   for (int kk = 0; kk < 16; ++kk)
     dst.st(t, kk, x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
            x[plane::slot2(4 * kk + 3)]);
 }
 
-// One workgroup per plane, grid (B, L).
-__global__ void __launch_bounds__(plane::T, 1)
-k_plane_fwd(uint32_t* __restrict__ ahat, const uint32_t* __restrict__ a, TabPtrs<uint32_t> tp, uint64_t ls,
-            uint32_t stagger) {
-  plane_stagger(stagger);
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  uint32_t* lds = (uint32_t*)smem_raw;
-  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
-  const uint32_t trace_id = poly + l * gridDim.x;
-  PLANE_STAMP(0, 0);
-  const uint64_t N = 1ull << 16;
-  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
-  uint32_t x[64];
-  plane_load(x, a + off, t);
-  PLANE_STAMP(0, 1);
-  plane_fwd<0, false>(x, lds, t, tp.tw + (uint64_t)l * N, mod_of(tp.lc[l]), trace_id);
-  plane_store_hat(HatBuf(ahat + off), x, t);
-  PLANE_STAMP(0, 7);
-}
-
-__global__ void __launch_bounds__(plane::T, 1)
-k_plane_mul(uint32_t* __restrict__ c, const uint32_t* __restrict__ b, const uint32_t* __restrict__ ahat,
-            TabPtrs<uint32_t> tp, uint64_t ls, uint32_t stagger) {
-  plane_stagger(stagger);
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  uint32_t* lds = (uint32_t*)smem_raw;
-  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
-  const uint32_t trace_id = poly + l * gridDim.x;
-  PLANE_STAMP(1, 0);
-  const uint64_t N = 1ull << 16;
-  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
-  const LimbConst<uint32_t> lc = tp.lc[l];
-  const Mod<uint32_t> mo = mod_of(lc);
-  const Tw<uint32_t>* tw = tp.tw + (uint64_t)l * N;
-  uint32_t x[64];
-  plane_load(x, b + off, t);
-  PLANE_STAMP(1, 1);
-  plane_fwd<1, false>(x, lds, t, tw, mo, trace_id);
-  const uint4* ah = (const uint4*)(ahat + off);
-  const HatBuf hb(ah);
-  plane_mul_tail<1>(x, lds, t, [hb, t](int kk) { return hb.ld(t, kk); }, c + off, tw, tp.itw + (uint64_t)l * N,
-                    lc, mo, trace_id);
-}
-
-// Both halves in one workgroup (RNT_PLANE=3): a -> a^ through the scratch
-// plane, which the same threads read back ~40 us later (so the read is
-// served by the Infinity Cache or L2 rather than HBM), then b -> c as
-// k_plane_mul.  One launch per batch; the store of a^ and the load of b
+// The product of one (poly, limb) plane pair: a -> a^ through the scratch
+// plane ah, which the same threads read back ~40 us later (so the read is
+// served by the Infinity Cache or L2 rather than HBM), then b -> b^, the
+// block products and the inverse to c.  The store of a^ and the load of b
 // are back to back and overlap.
-// The product of one (poly, limb) plane pair; the body of both fused kernels.
 __device__ __forceinline__ void plane_fused_one(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b,
                                                 uint32_t* ah, const TabPtrs<uint32_t>& tp, uint64_t ls, uint32_t poly,
                                                 uint32_t l, uint32_t* lds, uint32_t t, uint32_t trace_id) {
@@ -874,34 +596,10 @@ __device__ __forceinline__ void plane_fused_one(uint32_t* __restrict__ c, const 
   plane_load(x, a + off, t);
   PLANE_STAMP(0, 1);
   plane_fwd<0, false>(x, lds, t, tw, mo, trace_id);
-  if constexpr (kPlaneBEarly > 0) {
-    // b's first KB loads (in plane_load's order) go out before a^'s stores,
-    // so waiting for them does not wait for the stores (one in-order vmcnt
-    // counter): pass A of b starts on them while the stores drain
-    constexpr int KB = kPlaneBEarly;
-    const uint32_t* bp = b + off;
-    asm volatile("" : "+s"(bp));
-    const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc((void*)bp, 0, (int)(4u << 16), 0x00020000);
-    uint32_t y[KB > 0 ? KB : 1];
-#pragma unroll
-    for (int q = 0; q < KB; ++q) {
-      const int r = plane_load_reg(q);
-      y[q] = __builtin_amdgcn_raw_buffer_load_b32(gb, t * 4u, (uint32_t)r << 12, kPlaneAux);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    plane_store_hat(HatBuf(ah), x, t);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < 64; ++q) {
-      const int r = plane_load_reg(q);
-      x[r] = q < KB ? y[q < KB ? q : 0] : __builtin_amdgcn_raw_buffer_load_b32(gb, t * 4u, (uint32_t)r << 12, kPlaneAux);
-    }
-  } else {
-    plane_store_hat(HatBuf(ah), x, t);
-    PLANE_STAMP(0, 7);
-    PLANE_STAMP(1, 0);
-    plane_load(x, b + off, t);
-  }
+  plane_store_hat(HatBuf(ah), x, t);
+  PLANE_STAMP(0, 7);
+  PLANE_STAMP(1, 0);
+  plane_load(x, b + off, t);
   PLANE_STAMP(1, 1);
   plane_fwd<1, true>(x, lds, t, tw, mo, trace_id);
   // a^ comes back from this thread's own stores above (the descriptor is
@@ -914,93 +612,18 @@ __device__ __forceinline__ void plane_fused_one(uint32_t* __restrict__ c, const 
                     mo, trace_id);
 }
 
-
+// One workgroup per (poly, limb) plane pair, grid (B, L).  The a^ scratch
+// plane of (poly, limb) is at limb stride sls, or (sls = 0) packed [L][B].
+// (The form of this address is register allocation's business: the
+// runtime choice keeps it apart from the operands' offsets, which measured
+// 70 fewer SGPR spills than either form alone.)
 __global__ void __launch_bounds__(plane::T, 1)
 k_plane_fused(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
-              TabPtrs<uint32_t> tp, uint64_t ls, uint32_t cu_slots) {
+              TabPtrs<uint32_t> tp, uint64_t ls, uint64_t sls) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  const uint64_t N = 1ull << 16;
   const uint32_t poly = blockIdx.x, l = blockIdx.y;
-  // a^ goes to a scratch plane: per (poly, limb), or (cu_slots) per CU, so
-  // the launch's scratch footprint is 256 KiB per CU (64 MiB on 256 CUs),
-  // rewritten by the CU's next workgroup while it may still sit in the
-  // Infinity Cache
-  uint32_t* ah = scratch + (cu_slots ? (uint64_t)plane_cu_slot() * N : (uint64_t)l * ls + (uint64_t)poly * N);
+  uint32_t* ah = scratch + (sls ? (uint64_t)l * sls + ((uint64_t)poly << 16) : (uint64_t)(poly + l * gridDim.x) << 16);
   plane_fused_one(c, a, b, ah, tp, ls, poly, l, (uint32_t*)smem_raw, threadIdx.x, poly + l * gridDim.x);
-}
-
-// Persistent form (RNT_PLANE=4): one workgroup per CU walks the planes p =
-// blockIdx.x, + gridDim.x, ... (poly p % B, limb p / B, so the chip works on
-// one limb's twiddles at a time), with its own a^ scratch plane: a plane's
-// product stores and the next plane's loads meet in one wave's queue instead
-// of a workgroup ending and the next one starting.
-__global__ void __launch_bounds__(plane::T, 1)
-k_plane_fused_p(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
-                TabPtrs<uint32_t> tp, uint64_t ls, uint32_t B, uint32_t planes) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  uint32_t* ah = scratch + (uint64_t)blockIdx.x * (1ull << 16);
-  for (uint32_t p = blockIdx.x; p < planes; p += gridDim.x) {
-    const uint32_t l = p / B, poly = p - l * B;
-    // opaque per-iteration copies of the bases: nothing derived from them is
-    // hoisted out of the loop and held (in spilled registers) across a body
-    uint32_t* c1 = c;
-    const uint32_t *a1 = a, *b1 = b;
-    uint32_t* ah1 = ah;
-    TabPtrs<uint32_t> tp1 = tp;
-    asm volatile("" : "+s"(c1), "+s"(a1), "+s"(b1), "+s"(ah1));
-    asm volatile("" : "+s"(tp1.tw), "+s"(tp1.itw), "+s"(tp1.lc));
-    plane_fused_one(c1, a1, b1, ah1, tp1, ls, poly, l, (uint32_t*)smem_raw, threadIdx.x, p);
-  }
-}
-
-// Standalone transforms at N = 2^16, u32 bases (rnt_ntt_fwd / rnt_ntt_inv,
-// to_ntt_domain / to_coeff_domain, poly.rs:136-166): one workgroup per
-// (poly, limb) plane, in place.  Forward: the L0 load, all 16 stages (pass C
-// runs bits 5..0), and the L2 layout stored as it stands -- thread t holds
-// the 64 consecutive device-order words (t << 6) .. (t << 6) + 63, the same
-// bit-reversed order the four-step kernels write.  Inverse: those words in,
-// gs C from bit 0, then as after a product with the plain 1/N fold.  2
-// planes of HBM traffic per transform against the four-step kernels' 4.
-template <bool INV>
-__global__ void __launch_bounds__(plane::T, 1)
-k_plane_ntt(uint32_t* __restrict__ data, TabPtrs<uint32_t> tp, uint64_t ls) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  uint32_t* lds = (uint32_t*)smem_raw;
-  const uint32_t t = threadIdx.x, poly = blockIdx.x, l = blockIdx.y;
-  const uint64_t N = 1ull << 16;
-  const uint64_t off = (uint64_t)l * ls + (uint64_t)poly * N;
-  const LimbConst<uint32_t> lc = tp.lc[l];
-  const Mod<uint32_t> mo = mod_of(lc);
-  uint32_t x[64];
-  if constexpr (!INV) {
-    plane_load(x, data + off, t);
-    plane_fwd<0, false, NoHook, NoHook, true>(x, lds, t, tp.tw + (uint64_t)l * N, mo, poly + l * gridDim.x);
-    uint32_t* dp = data + off;
-    asm volatile("" : "+s"(dp));
-    const __amdgpu_buffer_rsrc_t g = __builtin_amdgcn_make_buffer_rsrc((void*)dp, 0, (int)(4u << 16), 0x00020000);
-    using V4 = decltype(__builtin_amdgcn_raw_buffer_load_b128(g, 0, 0, 0));
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      V4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = x[plane::slot2(4 * kk + e)];
-      __builtin_amdgcn_raw_buffer_store_b128(v, g, t * 256u, (uint32_t)kk * 16u, kPlaneAux);
-    }
-  } else {
-    const __amdgpu_buffer_rsrc_t g =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(data + off), 0, (int)(4u << 16), 0x00020000);
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(g, t * 256u, (uint32_t)kk * 16u, kPlaneAux);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = v[e];
-    }
-    const Tw<uint32_t>* itw = tp.itw + (uint64_t)l * N;
-    TwPre<0> gsrc;
-    gsrc.b = itw;
-    plane_inv_tail<1, 0>(x, lds, t, data + off, itw, gsrc, mo, Fold<uint32_t>{lc.c1, lc.c1_p, lc.c2, lc.c2_p},
-                         poly + l * gridDim.x);
-  }
 }
 
 #ifdef RNT_PLANE_TRACE
@@ -1009,94 +632,22 @@ extern "C" __attribute__((visibility("default"))) int rnt_debug_plane_trace(uint
 }
 #endif
 
-// The whole-plane product (k_plane_fwd + k_plane_mul) serves rnt_mul for
-// u32 canonical bases at N = 2^16 when Tables::plane is set (RNT_PLANE).
-// The whole-plane kernels take every u32 basis at N = 2^16 (their
-// canonical arithmetic holds for any q < 2^31, so 30-bit bases too: 131k
-// against the lazy four-step kernels' 114k products/s).
+// The whole-plane product serves rnt_mul for u32 bases at N = 2^16 unless
+// RNT_PLANE=0 (Tables::plane): its canonical arithmetic holds for any q <
+// 2^31, so 30-bit bases too (131k against the lazy four-step kernels' 114k
+// products/s).
 bool plane_ok(const Tables* t) {
   return t->plane != 0 && !t->wide && t->log_n == 16;
-}
-
-hipError_t launch_plane(const Launch& k, int which, void* out, const void* in, const void* ahat,
-                        uint64_t ls) {
-  if (k.B == 0 || k.L == 0) return hipSuccess;
-  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
-  const size_t lds = (size_t)plane::LDS_WORDS * 4;
-  const dim3 grid((unsigned)k.B, (unsigned)k.L);
-  const uint32_t st = k.t->plane_stagger;
-  if (which == 0) {
-    hipError_t e = allow_lds(k_plane_fwd, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_plane_fwd, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)in,
-                       tab_ptrs<uint32_t>(k.t), ls, st);
-  } else {
-    hipError_t e = allow_lds(k_plane_mul, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_plane_mul, grid, dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)in,
-                       (const uint32_t*)ahat, tab_ptrs<uint32_t>(k.t), ls, st);
-  }
-  return hipGetLastError();
-}
-
-#ifndef RNT_PLANE_SLOTS
-#define RNT_PLANE_SLOTS 0
-#endif
-// Per-CU scratch slots once the batch has at least as many planes as slots
-// (the workspace, one plane per (poly, limb), then holds every slot).
-bool plane_fused_slots(const Launch& k) {
-  return RNT_PLANE_SLOTS && (uint64_t)k.B * k.L >= kPlaneSlots;
-}
-
-hipError_t launch_plane_ntt(const Launch& k, int inverse, void* data, uint64_t ls) {
-  if (k.B == 0 || k.L == 0) return hipSuccess;
-  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
-  const size_t lds = (size_t)plane::LDS_WORDS * 4;
-  const dim3 grid((unsigned)k.B, (unsigned)k.L);
-  if (inverse) {
-    hipError_t e = allow_lds(k_plane_ntt<true>, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_plane_ntt<true>, grid, dim3(plane::T), lds, k.s, (uint32_t*)data, tab_ptrs<uint32_t>(k.t), ls);
-  } else {
-    hipError_t e = allow_lds(k_plane_ntt<false>, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_plane_ntt<false>, grid, dim3(plane::T), lds, k.s, (uint32_t*)data, tab_ptrs<uint32_t>(k.t), ls);
-  }
-  return hipGetLastError();
-}
-
-static int plane_cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-      n = v > 0 ? v : 256;
-    else
-      n = 256;
-  }
-  return n;
 }
 
 hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls) {
   if (k.B == 0 || k.L == 0) return hipSuccess;
   if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
   const size_t lds = (size_t)plane::LDS_WORDS * 4;
-  const uint64_t planes = (uint64_t)k.B * k.L;
-  if (k.t->plane == 4 && planes < 0xffffffffull) {
-    // one workgroup per CU, each with one a^ scratch plane (planes >= grid)
-    const unsigned grid = (unsigned)std::min<uint64_t>(planes, (uint64_t)plane_cu_count());
-    hipError_t e = allow_lds(k_plane_fused_p, lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_plane_fused_p, dim3(grid), dim3(plane::T), lds, k.s, (uint32_t*)out, (const uint32_t*)a,
-                       (const uint32_t*)b, (uint32_t*)scratch, tab_ptrs<uint32_t>(k.t), ls, (uint32_t)k.B,
-                       (uint32_t)planes);
-    return hipGetLastError();
-  }
   hipError_t e = allow_lds(k_plane_fused, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_plane_fused, dim3((unsigned)k.B, (unsigned)k.L), dim3(plane::T), lds, k.s, (uint32_t*)out,
-                     (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)scratch, tab_ptrs<uint32_t>(k.t), ls,
-                     plane_fused_slots(k) ? 1u : 0u);
+                     (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)scratch, tab_ptrs<uint32_t>(k.t), ls, ls);
   return hipGetLastError();
 }
 
