@@ -87,7 +87,9 @@ constexpr int kTw4f = kTw3f + 1024;       // [w][c][lam]: pass 3 twist, P4 posit
 constexpr int kTw4i = kTw4f + 16384;      // [w][c][lam]: inverse pass 3 twist, Q3 positions
 constexpr int kTw3i = kTw4i + 16384;      // [w][c][g]: inverse pass 2 twist, Q3 positions
 constexpr int kLimb = kTw3i + 1024;
-constexpr size_t kLdsBytes = (size_t)(1u << 15) * 4;  // the P1 <-> P2 exchange: half a plane per round
+// LDS: the P1 <-> P2 exchange (128 KiB: half a plane per round) and the
+// inverse's stash (10 KiB a wave); one workgroup per CU either way
+constexpr size_t kLdsBytes = (size_t)160 * 1024;
 
 // Registers of a P3 / P4 / Q3 chunk (c, i) after the P2 -> P3 swap, as
 // physical slots of the P2 numbering 4c + i (see the header).
@@ -380,13 +382,14 @@ template <int C0>
 __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
                                         const Mc& m) {
   const v4i z = {0, 0, 0, 0};
-  v4i tv = bld(tab, tvo, tso + (uint32_t)C0 * 16u);  // each tile's twists one tile ahead
 #pragma unroll
   for (int c = C0; c < C0 + 8; ++c) {
     v4i b;
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x2[4 * c + i];
-    const v4i tn = c + 1 < C0 + 8 ? bld(tab, tvo, tso + (uint32_t)(c + 1) * 16u) : tv;
+    // (the twists of a 16 KiB table: cache hits, loaded at the tile -- a
+    // tile-ahead prefetch measured 4 more spilled registers)
+    const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 16u);
     v4i D[4];
     tile<false>(D, M, b, z);
 #pragma unroll
@@ -395,7 +398,6 @@ __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], R
       x2[4 * c + i] = (uint32_t)mont<true>(r, tv[i], m) ^ K32;
     }
     pin4(x2[4 * c + 0], x2[4 * c + 1], x2[4 * c + 2], x2[4 * c + 3]);
-    tv = tn;
     tile_fence();
   }
 }
@@ -440,15 +442,34 @@ __device__ __forceinline__ void pass_p4(uint32_t (&x)[64], const v4i (&M)[4], co
     tile_fence();
   }
 }
-// inverse pass 3 (F^-1, data as A: P4 -> Q3), then its twist; packed output.
-__device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v4i comp, Rsrc tab, uint32_t tvo,
-                                         uint32_t tso, const Mc& m) {
+// The inverse's first two passes hold the whole plane and two matrices'
+// worth of operands in registers: the outputs of ipass_p4's first kStash
+// tiles wait in a per-wave LDS stash (the LDS is idle until the exchanges)
+// until ipass_p3 takes them, instead of being spilled to scratch memory.
+constexpr int kStash = 10;
+__device__ __forceinline__ uint32_t stash_addr(const uint32_t* lds, const Th& h) {
+  return (uint32_t)(uintptr_t)lds + (h.w * (kStash * 64u) + h.lam()) * 16u;
+}
+__device__ __forceinline__ void stash_put(uint32_t addr, int c, uint32_t a, uint32_t b, uint32_t d, uint32_t e) {
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "v"(v4i{(int)a, (int)b, (int)d, (int)e}), "i"(c * 1024)
+               : "memory");
+}
+__device__ __forceinline__ v4i stash_get(uint32_t addr, int c) {
+  v4i v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr), "i"(c * 1024) : "memory");
+  return v;
+}
+// inverse pass 3 (F^-1, data as A: P4 -> Q3) on the canonical words as
+// loaded (biased here, comp undoes it), then its twist; packed output.
+// tv: tile 0's twists (each tile loads the next one's).
+__device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v4i comp, v4i tv, Rsrc tab,
+                                         uint32_t tvo, uint32_t tso, const Mc& m, uint32_t* lds, const Th& h) {
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
     v4i a;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = (int)x[p3(c, i)];
-    const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 1024u);
+    for (int i = 0; i < 4; ++i) a[i] = (int)pk_canon(x[p3(c, i)]);
+    const v4i tn = c + 1 < 16 ? bld(tab, tvo, tso + (uint32_t)(c + 1) * 1024u) : tv;
     v4i D[4];
     tile<true>(D, M, a, comp);
 #pragma unroll
@@ -456,19 +477,27 @@ __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
       x[p3(c, i)] = (uint32_t)mont<true>(r, tv[i], m) ^ K32;
     }
-    pin4(x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
+    if (c < kStash)
+      stash_put(stash_addr(lds, h), c, x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
+    else
+      pin4(x[p3(c, 0)], x[p3(c, 1)], x[p3(c, 2)], x[p3(c, 3)]);
+    tv = tn;
     tile_fence();
   }
 }
 // inverse pass 2 (F^-1 in Q3), then its twist; packed output.
 __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
-                                         const Mc& m) {
+                                         const Mc& m, uint32_t* lds, const Th& h) {
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
     v4i b;
+    if (c < kStash) {
+      b = stash_get(stash_addr(lds, h), c);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) b[i] = (int)x[p3(c, i)];
+      for (int i = 0; i < 4; ++i) b[i] = (int)x[p3(c, i)];
+    }
     const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 64u);
     v4i D[4];
     tile<false>(D, M, b, z);
@@ -585,13 +614,15 @@ struct NoEpi {
 template <bool SYNC1, class EPI = NoEpi>
 __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds, const Th& h, const Tabs& T,
                                     const EPI& epi = EPI{}) {
-  uint32_t x1[64];
-  load_p1(x1, src, h);
+  // the first pass's operands load ahead of the plane (cache hits, needed
+  // first): its first tile then waits only for its own words
   const Mc& m = T.m;
   const uint32_t lo = h.lam() * 16u;
   v4i M[4];
   load_mat(M, T.tab, S_F1, lo);
   const v4i comp = bld(T.tab, lo, (uint32_t)kCompF1 * 16u);
+  uint32_t x1[64];
+  load_p1(x1, src, h);
   pass_p1<0, true>(x1, M, comp, m);
   if constexpr (SYNC1) __syncthreads();
   uint32_t wb[4], rb[4];
@@ -618,18 +649,31 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   pass_p4(x2, M, m, epi);
 }
 
-// The inverse from x2 (packed, P4 positions) to the canonical plane at dst
-// (P1); the first pass's digit-0 accumulators start at the input bias's
-// compensation (canonical input words travel as x - 2^30).
-__device__ __forceinline__ void inv(uint32_t (&x2)[64], Rsrc dst, uint32_t* lds, const Th& h, const Tabs& T) {
+// The inverse in place: the NTT-domain plane (device order, P4 positions)
+// to the canonical coefficients (P1).  The first pass's digit-0
+// accumulators start at the input bias's compensation (canonical input
+// words travel as x - 2^30).  The first pass's operands load ahead of the
+// plane (cache hits, needed first); its first tile then waits only for
+// its own words.  In place: a wave stores only after the exchanges'
+// barriers, which it passes once it has used (so read) every word it loaded.
+__device__ __forceinline__ void inv(Rsrc pr, uint32_t* lds, const Th& h, const Tabs& T) {
   const Mc& m = T.m;
   const uint32_t lo = h.lam() * 16u;
   v4i M[4];
   load_mat(M, T.tab, S_I4, lo);
-  ipass_p4(x2, M, bld(T.tab, lo, (uint32_t)kCompI4 * 16u), T.tab, lo, (uint32_t)(kTw4i + h.w * 1024) * 16u,
-           m);
+  const v4i comp = bld(T.tab, lo, (uint32_t)kCompI4 * 16u);
+  const uint32_t t4s = (uint32_t)(kTw4i + h.w * 1024) * 16u;
+  const v4i tv0 = bld(T.tab, lo, t4s);
+  uint32_t x2[64];
+#pragma unroll
+  for (int cc = 0; cc < 16; ++cc) {
+    const v4i v = bld(pr, p4_lane(h), p4_soff(h, cc));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x2[p3(cc, i)] = (uint32_t)v[i];
+  }
+  ipass_p4(x2, M, comp, tv0, T.tab, lo, t4s, m, lds, h);
   load_mat(M, T.tab, S_I3, lo);
-  ipass_p3(x2, M, T.tab, h.g() * 16u, (uint32_t)(kTw3i + h.w * 64) * 16u, m);
+  ipass_p3(x2, M, T.tab, h.g() * 16u, (uint32_t)(kTw3i + h.w * 64) * 16u, m, lds, h);
   swap_q3p2(x2);
   load_mat(M, T.tab, S_I2 + h.w, lo);
   uint32_t wb[4], rb[4];
@@ -651,7 +695,7 @@ __device__ __forceinline__ void inv(uint32_t (&x2)[64], Rsrc dst, uint32_t* lds,
   p1_bases(wb, h);
   x_read_p1<1>(x1, lds, wb);
   ipass_p1<8>(x1, M, m);
-  store_p1(x1, dst, h);
+  store_p1(x1, pr, h);
 }
 
 }  // namespace mf
@@ -670,8 +714,8 @@ k_mf_ntt(uint32_t* __restrict__ data, const void* __restrict__ mft, const LimbCo
   uint32_t* p = data + (uint64_t)l * ls + (uint64_t)poly * kN;
   const Tabs T = tabs_of(mft, lcs[l], l);
   const Rsrc pr = rsrc(p, kN * 4u);
-  uint32_t x[64];
   if constexpr (!INV) {
+    uint32_t x[64];
     // the last pass stores each tile, canonical, in the device order (in
     // place: every wave read its words of the plane before the first
     // exchange's barrier)
@@ -680,15 +724,7 @@ k_mf_ntt(uint32_t* __restrict__ data, const void* __restrict__ mft, const LimbCo
           p4_lane(h), p4_soff(h, cc));
     });
   } else {
-#pragma unroll
-    for (int cc = 0; cc < 16; ++cc) {
-      const v4i v = bld(pr, p4_lane(h), p4_soff(h, cc));
-#pragma unroll
-      for (int i = 0; i < 4; ++i) x[p3(cc, i)] = pk_canon((uint32_t)v[i]);
-    }
-    // in place: a wave stores only after the exchanges' barriers, which it
-    // passes once it has used (so read) every word it loaded
-    inv(x, pr, lds, h, T);
+    inv(pr, lds, h, T);
   }
 }
 
