@@ -529,23 +529,11 @@ __device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], c
     tile_fence();
   }
 }
-// inverse pass 0 on P1 chunks [C0, C0 + 8): canonical output.
+// inverse pass 0 on P1 chunks [C0, C0 + 8): canonical output; every four
+// chunks (the words of one 16-byte store per register) go to memory at once.
 template <int C0>
-__device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], const Mc& m) {
-  const v4i z = {0, 0, 0, 0};
-#pragma unroll
-  for (int c = C0; c < C0 + 8; ++c) {
-    v4i b;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) b[i] = (int)x1[4 * c + i];
-    v4i D[4];
-    tile<false>(D, M, b, z);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) x1[4 * c + i] = canon(recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m), m.q);
-    pin4(x1[4 * c + 0], x1[4 * c + 1], x1[4 * c + 2], x1[4 * c + 3]);
-    tile_fence();
-  }
-}
+__device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], const Mc& m, Rsrc dst,
+                                         const Th& h);
 
 // P1 plane byte offsets of load / store (i, hc): 4 consecutive words,
 // chunks c = 4 hc + e, e = 0..3.  Lane part (VGPR), wave part and the
@@ -569,18 +557,36 @@ __device__ __forceinline__ void load_p1(uint32_t (&x1)[64], Rsrc src, const Th& 
       for (int e = 0; e < 4; ++e) x1[4 * (4 * hc + e) + i] = (uint32_t)v[e];
     }
 }
-__device__ __forceinline__ void store_p1(const uint32_t (&x1)[64], Rsrc dst, const Th& h) {
-  const uint32_t lo = p1_lane(h), wo = p1_wave(h);
+template <int C0>
+__device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], const Mc& m, Rsrc dst,
+                                         const Th& h) {
+  const v4i z = {0, 0, 0, 0};
 #pragma unroll
-  for (int hc = 0; hc < 4; ++hc)
+  for (int c = C0; c < C0 + 8; ++c) {
+    v4i b;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v4i v;
+    for (int i = 0; i < 4; ++i) b[i] = (int)x1[4 * c + i];
+    v4i D[4];
+    tile<false>(D, M, b, z);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (int)x1[4 * (4 * hc + e) + i];
-      bst(v, dst, lo, wo + p1_reg(i, hc));
+    for (int i = 0; i < 4; ++i) x1[4 * c + i] = canon(recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m), m.q);
+    if ((c & 3) == 3) {
+      const int hc = c >> 2;
+      const uint32_t lo = p1_lane(h), wo = p1_wave(h);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v4i v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (int)x1[4 * (4 * hc + e) + i];
+        bst(v, dst, lo, wo + p1_reg(i, hc));
+      }
+    } else {
+      pin4(x1[4 * c + 0], x1[4 * c + 1], x1[4 * c + 2], x1[4 * c + 3]);
     }
+    tile_fence();
+  }
 }
+
 // P4 (NTT-domain device order): chunk c's 4 words are consecutive.
 __device__ __forceinline__ uint32_t p4_lane(const Th& h) { return ((h.n() << 4) | (h.g() << 2)) * 4u; }
 __device__ __forceinline__ uint32_t p4_soff(const Th& h, int c) { return ((h.w << 12) | ((uint32_t)c << 8)) * 4u; }
@@ -690,12 +696,11 @@ __device__ __forceinline__ void inv(Rsrc pr, uint32_t* lds, const Th& h, const T
   p2_bases(rb, h);
   x_write_p2<1>(x2, lds, rb);
   load_mat(M, T.tab, S_I1, lo);
-  ipass_p1<0>(x1, M, m);
+  ipass_p1<0>(x1, M, m, pr, h);
   __syncthreads();
   p1_bases(wb, h);
   x_read_p1<1>(x1, lds, wb);
-  ipass_p1<8>(x1, M, m);
-  store_p1(x1, pr, h);
+  ipass_p1<8>(x1, M, m, pr, h);
 }
 
 }  // namespace mf
