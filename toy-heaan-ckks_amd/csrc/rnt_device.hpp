@@ -57,43 +57,12 @@ __device__ __forceinline__ auto mod_for(const LimbConst<W>& lc) {
 // Cache-policy bits (`aux`) of the plane loads and stores: the default
 // policy (non-temporal was within run-to-run spread).
 constexpr int kBufAux = 0;
-// Measurement builds only (tools/build_variant.sh -DRNT_MEAS=...; never the
-// shipped library): 1 = the product kernels (k_colt_fwd, k_row<2>,
-// k_colt_inv) move no plane data through memory (synthetic loads, stores
-// kept behind a never-true compare), 2 = their butterflies are skipped.
-// They time the VALU-only and memory/LDS-only parts of the poly-mul
-// ("ceiling").
-#ifndef RNT_MEAS
-#define RNT_MEAS 0
-#endif
-constexpr int kMeas = RNT_MEAS;
-// 3 and 4 keep every butterfly and move the poly-mul's plane traffic of a
-// lower-traffic design: the intermediate planes named below are replaced
-// by synthetic values (loads) and never-true stores, so the three kernels
-// move 5 planes per (poly, limb) (3: a's column output and the row
-// output are not written, a's column output and the column-inverse input
-// not read) or 7 (4: only the row -> inverse-column plane is skipped) --
-// the energy model's what-ifs measured directly.
-// Sites: 0 k_colt_fwd operand-0 store, 1 k_row<2> load of operand 0,
-// 2 k_row<2> store, 3 k_colt_inv load.
-constexpr bool meas_virtual(int site) {
-  return (kMeas == 3 && site <= 3) || (kMeas == 4 && (site == 2 || site == 3));
-}
-template <class W>
-__device__ __forceinline__ W meas_val(uint32_t v, uint32_t s) {
-  return (W)((v * 2654435761u + s) & 0x3fffffffu);
-}
 template <class W>
 __device__ __forceinline__ W gload(const W* p, uint64_t i) {
-  if constexpr (kMeas == 1) return meas_val<W>((uint32_t)i, 0u);
   return p[i];
 }
 template <class W>
 __device__ __forceinline__ void gstore(W* p, uint64_t i, W x) {
-  if constexpr (kMeas == 1) {
-    if (x == (W)0xffffffffu) p[i] = x;
-    return;
-  }
   p[i] = x;
 }
 
@@ -103,7 +72,6 @@ struct BufView {
   __device__ BufView(const W* base, uint32_t elems)
       : r(__builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(elems * sizeof(W)), 0x00020000)) {}
   __device__ __forceinline__ W ld(uint32_t v, uint32_t s) const {
-    if constexpr (kMeas == 1) return meas_val<W>(v, s);
     if constexpr (sizeof(W) == 4) {
       return __builtin_amdgcn_raw_buffer_load_b32(r, v * 4u, s * 4u, kBufAux);
     } else {
@@ -129,9 +97,6 @@ struct BufView {
     }
   }
   __device__ __forceinline__ void st(W x, uint32_t v, uint32_t s) const {
-    if constexpr (kMeas == 1) {
-      if (x != (W)0xffffffffu) return;
-    }
     if constexpr (sizeof(W) == 4) {
       __builtin_amdgcn_raw_buffer_store_b32(x, r, v * 4u, s * 4u, kBufAux);
     } else {

@@ -294,7 +294,6 @@ struct ColGeo : PassSched<LOG_R> {
 template <class W, int NOPS, int LOGE, int K, int BB, class TS, class MO, int SLMIN = 0>
 __device__ __forceinline__ void pass_ct(W (&x)[NOPS][1 << LOGE], uint32_t node0, const TS& tw,
                                         const MO& mo) {
-  if constexpr (kMeas == 2) return;
   constexpr int E = 1 << LOGE;
 #pragma unroll
   for (int sl = K - 1; sl >= SLMIN; --sl) {
@@ -329,7 +328,6 @@ template <class W, int NOPS, int LOGE, int K, int BB, int LOGX, bool FOLD, class
           int SLMIN = 0>
 __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0, const TS& itw,
                                         const MO& mo, const Fold<W>& f) {
-  if constexpr (kMeas == 2) return;
   const W bias = gs_bias(mo);
   constexpr int E = 1 << LOGE;
 #pragma unroll
@@ -554,12 +552,7 @@ k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t
   }
   xf_fwd<G, W, 1>(x, cp.xp, lds, tw, m);
 #pragma unroll
-  for (int i = 0; i < E; ++i) {
-    if constexpr (meas_virtual(0)) {
-      if (x[0][i] != (W)0xffffffffu) continue;
-    }
-    dst.st(x[0][i], al.v, i * al.s);
-  }
+  for (int i = 0; i < E; ++i) dst.st(x[0][i], al.v, i * al.s);
 }
 
 template <class W, int LOG_R, int LOG_TC, bool LZ = false>
@@ -585,7 +578,7 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
   W x[1][E];
 #pragma unroll
   for (int i = 0; i < E; ++i)
-    x[0][i] = meas_virtual(3) ? meas_val<W>(al.v, (uint32_t)i * al.s) : src.ld(al.v, i * al.s);
+    x[0][i] = src.ld(al.v, i * al.s);
   xf_inv<G, W, 1, true>(x, cp.xp, lds, itw, mod_for<W, LZ>(lc), f);  // canonical out
   a0.refresh();
   if (addend != nullptr) {
@@ -704,8 +697,7 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
     W v[2][E];
 #pragma unroll
     for (int i = 0; i < E; ++i) {
-      v[0][i] = meas_virtual(1) ? meas_val<W>((uint32_t)(base + b0) + (uint32_t)i, 7u)
-                                : gload(xg, base + b0 + ((uint32_t)i << G::BB0));
+      v[0][i] = gload(xg, base + b0 + ((uint32_t)i << G::BB0));
       v[1][i] = gload(yg, base + b0 + ((uint32_t)i << G::BB0));
     }
     const auto mo = mod_for<W, LZ>(lc);
@@ -754,12 +746,7 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
     }
     if (rp.active) {
 #pragma unroll
-      for (int i = 0; i < E; ++i) {
-        if constexpr (meas_virtual(2)) {
-          if (z[0][i] != (W)0xffffffffu) continue;
-        }
-        gstore(xg, base + b0 + ((uint32_t)i << G::BB0), z[0][i]);
-      }
+      for (int i = 0; i < E; ++i) gstore(xg, base + b0 + ((uint32_t)i << G::BB0), z[0][i]);
     }
   } else if constexpr (MODE == 0) {
     W v[1][E];
@@ -793,24 +780,16 @@ __host__ __device__ constexpr int ks_kpad_words(int c) {
 // reads of 16 lanes at 64-byte strides (a row's E = 16 consecutive words per
 // thread) start on 16 distinct 4-bank groups, and 16-byte alignment holds.
 __device__ __forceinline__ uint32_t ks_pad(uint32_t w) { return w + ((w >> 6) << 2); }
-#ifndef RNT_KS_SPRE
-#define RNT_KS_SPRE 0
-#endif
 // LDS plan of k_ks_rows<W, LOG_C, NP>, shared by the kernel and its launcher.
 //  * KEYGLDS: u32 rows of >= 64 words take the key rows global -> LDS
 //    directly (global_load_lds);
 //  * KDOUBLE: two key buffers (the next limb's keys are written while the
 //    last ones may still be read) when they fit beside the exchange region in
-//    a quarter of the LDS, else one buffer and a barrier per limb;
-//  * SPRE: the next source limb's S rows also go global -> LDS, one limb
-//    ahead, into a buffer of RPW rows (row stride C + T words, so the T
-//    lanes of each of a wave's rows read distinct banks), when a wave's
-//    lanes own whole rows (T <= 64), the keys are double-buffered and it all
-//    still fits in a quarter of the LDS (4 workgroups per CU).  Off by
-//    default: it applies to the 2^16 ct-mul grid (NP = 16) and measured
-//    slower there, ks_rows 2.40 against 2.31 ms per 64-ct chunk
-//    (profiles/r03/ab_ks_spre.txt), as register prefetch of the next limb
-//    did before it -- the rows kernel does not wait on the S loads.
+//    a quarter of the LDS, else one buffer and a barrier per limb.
+// (Staging the next source limb's S rows global -> LDS one limb ahead
+// measured slower, ks_rows 2.40 against 2.31 ms per 64-ct chunk,
+// profiles/r03/ab_ks_spre.txt, as register prefetch of the next limb did
+// before it: the rows kernel does not wait on the S loads.)
 template <class W, int LOG_C, int NP>
 struct KsCfg {
   using G = RowGeo<LOG_C>;
@@ -819,12 +798,8 @@ struct KsCfg {
   static constexpr bool KEYGLDS = sizeof(W) == 4 && G::C >= 64 && (NP > 1 || LOG_C >= kKsGldsWideMinLogC);
   static constexpr bool KDOUBLE =
       (size_t)(G::REGION + 4 * KROWS * KPAD) * sizeof(W) <= 40u * 1024u || KROWS == 1;
-  static constexpr int SSTRIDE = G::C + G::S::T;
-  static constexpr int SWORDS = G::RPW * SSTRIDE;
   static constexpr int KWORDS = (KDOUBLE ? 4 : 2) * KROWS * KPAD;
-  static constexpr bool SPRE = RNT_KS_SPRE != 0 && KEYGLDS && KDOUBLE && G::S::T <= 64 &&
-                               (size_t)(G::REGION + KWORDS + SWORDS) * sizeof(W) <= 40u * 1024u;
-  static constexpr size_t LDS_BYTES = (size_t)(G::REGION + KWORDS + (SPRE ? SWORDS : 0)) * sizeof(W);
+  static constexpr size_t LDS_BYTES = (size_t)(G::REGION + KWORDS) * sizeof(W);
 };
 
 // 16 bytes of LDS into registers (p is 16-byte aligned by construction:
@@ -894,13 +869,10 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   constexpr int KPT = (2 * KROWS * C + G::THREADS - 1) / G::THREADS;  // key words per thread per i
   constexpr bool kKeyGlds = K::KEYGLDS;
   constexpr bool KDOUBLE = K::KDOUBLE;
-  constexpr bool SPRE = K::SPRE;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
   // [buffers][key_b rows | key_a rows]
   W* kbuf = lds + G::REGION;
-  // [RPW rows of SSTRIDE]: the S rows of the next source limb (SPRE)
-  W* sbuf = kbuf + K::KWORDS;
   // XCD-aware deal: hardware block b runs on XCD b % 8; consecutive logical
   // blocks (one (j, r), successive poly groups) get the same b % 8
   const uint32_t per_xcd = (nblocks + 7) / 8;
@@ -953,52 +925,6 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     acc[1][e] = init1 ? init1[ibase + pos] : (W)0;
   }
   constexpr uint32_t KW = (uint32_t)(KROWS * C);  // words per key
-  // SPRE: key rows and S rows of source limb i go global -> LDS (no
-  // registers) during limb i - 1's transform and accumulate.  A wave's lanes
-  // own whole rows (T <= 64), so a wave loads exactly the S rows it reads
-  // back; the key rows are shared, published by a barrier.
-  [[maybe_unused]] const uint32_t wave_u = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  [[maybe_unused]] const uint32_t lane_u = threadIdx.x & 63u;
-  auto ks_issue = [&](uint32_t i, W* kb) {
-    if constexpr (SPRE) {
-    constexpr uint32_t SEG = KW / 64;  // segments per key
-    constexpr int WAVES = G::THREADS / 64;
-    const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + (WIDE ? (uint64_t)rbase * G::C : rowoff);
-#pragma unroll
-    for (int m = 0; m < (int)((2 * SEG + WAVES - 1) / WAVES); ++m) {
-      const uint32_t sg = wave_u + (uint32_t)m * WAVES;
-      if (sg < 2 * SEG) {
-        const uint32_t kk = sg >= SEG, rs = kk ? sg - SEG : sg;
-        const W* src = (kk ? key_a : key_b) + kbase + rs * 64u + lane_u;
-        W* dst = kb + kk * (KROWS * KPAD) + (rs / (C / 64)) * KPAD + ks_pad((rs % (C / 64)) * 64u);
-        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
-      }
-    }
-    if constexpr (SPRE) {
-      // the wave's rows: slots wave * 64 / T .. + 64 / T, C / 64 segments each
-      constexpr int SPW = 64 / G::S::T, SSEG = C / 64;
-#pragma unroll
-      for (int m = 0; m < SPW * SSEG; ++m) {
-        const uint32_t slot = wave_u * SPW + (uint32_t)(m / SSEG), sg = (uint32_t)(m % SSEG);
-        uint32_t p, r;
-        if constexpr (WIDE) {
-          r = rbase + slot / NP;
-          p = pg * NP + slot % NP;
-        } else {
-          r = rbase;
-          p = pg * G::RPW + slot;
-        }
-        p = p < B ? p : B - 1;
-        const W* src = S + (((uint64_t)j * L + i) * B + p) * N + (uint64_t)r * G::C + sg * 64u + lane_u;
-        W* dst = sbuf + slot * K::SSTRIDE + sg * 64u;
-        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
-      }
-    }
-    }
-  };
-  if constexpr (SPRE) ks_issue(0u, kbuf);
 #pragma unroll 1
   for (uint32_t i = 0; i < L; ++i) {
     // this limb's key rows (key poly i, limb j, rows rbase ..; limb stride
@@ -1006,29 +932,11 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     const uint64_t sbase = (((uint64_t)j * L + i) * B + rp.p) * N + rowoff;
     const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + (WIDE ? (uint64_t)rbase * G::C : rowoff);
     W x[1][E];
-    if constexpr (SPRE) {
-      // limb i's rows have landed (this wave's loads), and every wave's
-      // (the barrier, which also orders every wave's reads of the key buffer
-      // limb i + 1 overwrites, two limbs ago, before the loads into it)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      const W* sr = sbuf + rp.xp.slot * K::SSTRIDE + b0;
-#pragma unroll
-      for (int e = 0; e < E; ++e) x[0][e] = sr[(uint32_t)e << G::BB0];
-      // the reads complete before the next limb's rows overwrite them
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      if (i + 1 < L) ks_issue(i + 1, kbuf + ((i + 1) & 1u) * 2 * KROWS * KPAD);
-      __builtin_amdgcn_sched_barrier(0);
-    }
     // one key buffer: every thread's reads of the previous limb's keys
     // finish before it is rewritten
     if constexpr (!KDOUBLE) __syncthreads();
     W* kb = KDOUBLE ? kbuf + (i & 1u) * 2 * KROWS * KPAD : kbuf;
-    if constexpr (SPRE) {
-      (void)sbase;
-      (void)kbase;
-    } else if constexpr (kKeyGlds) {
+    if constexpr (kKeyGlds) {
       // u32 rows of >= 64 words: the key rows go global -> LDS directly, one
       // 64-word segment (one ks_pad run) per wave instruction, no registers
       constexpr uint32_t SEG = KW / 64;  // segments per key

@@ -162,11 +162,7 @@ __device__ __forceinline__ int32_t mont(int32_t a, int32_t b, const Mc& m) {
 }
 // The end of one tile's work: hipcc would otherwise hoist later tiles'
 // MFMAs and loads above it and keep their digit sums live (spills).
-__device__ __forceinline__ void tile_fence() {
-#ifndef RNT_MF_NOFENCE
-  __builtin_amdgcn_sched_barrier(0);
-#endif
-}
+__device__ __forceinline__ void tile_fence() { __builtin_amdgcn_sched_barrier(0); }
 // Pins a tile's four outputs as computed at this point: IR-level code motion
 // (sched_barrier orders only the machine scheduler) would otherwise sink the
 // reductions to the words' next use and keep their partial sums live.

@@ -38,16 +38,10 @@ __host__ __device__ __forceinline__ uint64_t mulhi(uint64_t a, uint64_t b) {
 // into VCC / an SGPR pair) + v_cndmask_b32, two full-rate instructions
 // (tools/oprate2.hip: 2.1 cycles each per wave64 on one SIMD), where the
 // min(x, x - q) form costs v_sub (2.2) + v_min_u32 (4.1, half rate).
-#ifndef RNT_CSUB_MIN
-#define RNT_CSUB_MIN 0
-#endif
-#ifndef RNT_SHOUP_MULLO
-#define RNT_SHOUP_MULLO 0
-#endif
 template <class W>
 __host__ __device__ __forceinline__ W csub(W x, W q) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (sizeof(W) == 4 && !RNT_CSUB_MIN) {
+  if constexpr (sizeof(W) == 4) {
     W y;
     const bool borrow = __builtin_sub_overflow(x, q, &y);
     return borrow ? x : y;
@@ -66,7 +60,7 @@ __host__ __device__ __forceinline__ W add_mod(W a, W b, W q) {
 template <class W>
 __host__ __device__ __forceinline__ W sub_mod(W a, W b, W q) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (sizeof(W) == 4 && !RNT_CSUB_MIN) {
+  if constexpr (sizeof(W) == 4) {
     W d;
     const bool borrow = __builtin_sub_overflow(a, b, &d);
     return borrow ? d + q : d;
@@ -118,7 +112,6 @@ __device__ __forceinline__ uint64_t mul64(uint32_t a, uint32_t b) {
 __device__ __forceinline__ uint32_t shoup_lazy(uint32_t x, uint32_t w, uint32_t wp,
                                                const Mod<uint32_t>& m) {
   const uint32_t qh = mulhi(x, wp);
-  if constexpr (RNT_SHOUP_MULLO) return x * w - qh * m.q;
   return (uint32_t)mad64(qh, m.nq, mul64(x, w));  // low word of x*w + qh*(2^32 - q)
 }
 __device__ __forceinline__ uint64_t shoup_lazy(uint64_t x, uint64_t w, uint64_t wp,
