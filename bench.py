@@ -342,7 +342,7 @@ def run_polymul(args, comm, world, rank, local_rank):
     comm.barrier()
     elapsed = comm.max(t1 - t0)
     kernels = {}
-    for k in ("col_fwd", "row_mul", "col_inv", "plane_fused"):
+    for k in ("col_fwd", "row_mul", "col_inv", "plane_fused", "whole_mul"):
         cnt, ms = B.profile_read(k)
         if cnt:
             kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
@@ -397,7 +397,7 @@ def run_polymul(args, comm, world, rank, local_rank):
     op_bytes = 3 * elem * wb
     achieved = op_bytes / (op_ms * 1e-3) / 1e9
     step_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb,
-                  "plane_fused": 3 * elem * wb}
+                  "plane_fused": 3 * elem * wb, "whole_mul": 3 * elem * wb}
     per_gpu = value / world
     pmc = {k: traffic_for(k, "polymul", batch, args.log_n, Lr) if args.prime_bits == 31 else None
            for k in kernels}
@@ -405,7 +405,7 @@ def run_polymul(args, comm, world, rank, local_rank):
     for k, kv in kernels.items():
         kb = step_bytes.get(k)
         ent = {"avg_ms": kv["avg_ms"], "launches": kv["launches"], "alg_bytes_per_launch": kb,
-               "bound": "valu" if k in ("row_mul", "plane_fused") else "hbm",
+               "bound": "valu" if k in ("row_mul", "plane_fused", "whole_mul") else "hbm",
                "pmc_bytes_per_launch": pmc.get(k)}
         if kb:
             ent["hbm_GBs"] = kb / (kv["avg_ms"] * 1e-3) / 1e9
@@ -1050,7 +1050,7 @@ def run_ntt(args, comm, world, rank, local_rank):
     comm.barrier()
     elapsed = comm.max(t1 - t0)
     kernels = {}
-    for k in ("col_fwd", "row_fwd", "row_inv", "col_inv", "mf_ntt_fwd", "mf_ntt_inv"):
+    for k in ("col_fwd", "row_fwd", "row_inv", "col_inv", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd", "whole_inv"):
         cnt, ms = B.profile_read(k)
         if cnt:
             kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}

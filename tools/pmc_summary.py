@@ -29,6 +29,9 @@ def short(kname):
         return "mf_ntt_inv" if m.group(1) == "true" else "mf_ntt_fwd"
     if re.search(r"\bk_plane_fused\(", kname):
         return "plane_fused"
+    m = re.search(r"\bk_row<unsigned (int|long), (\d), \d+, (true|false), true>", kname)
+    if m:
+        return ("whole_fwd", "whole_inv", "whole_mul")[int(m.group(2))]
     m = re.search(r"(k_\w+)<([^>]*)>", kname)
     if not m or not m.group(2).startswith("unsigned int"):
         return None

@@ -95,7 +95,7 @@ thread_local Capture* g_capture = nullptr;
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
-    "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv"};
+    "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd", "whole_inv", "whole_mul"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -449,6 +449,10 @@ int to_coeff_into(const rnt_buf* src, void* dst) {
             "hipMemcpyAsync");
   if (use_mf(k)) {
     LAUNCH(k.t, rnt::K_MF_NTT_INV, rnt::launch_mf_ntt(k, 1, dst, ls), "MFMA inverse transform");
+    return RNT_OK;
+  }
+  if (rnt::whole_ok(k.t, 1)) {
+    LAUNCH(k.t, rnt::K_WHOLE_INV, rnt::launch_whole(k, 1, dst, dst, nullptr, ls), "whole-plane inverse");
     return RNT_OK;
   }
   LAUNCH(k.t, rnt::K_ROW_INV, rnt::launch_row(k, 1, dst, nullptr, ls), "row inverse");
@@ -1143,6 +1147,9 @@ extern "C" int rnt_ntt_fwd(rnt_buf* b) {
   if (use_mf(k)) {
     // N = 2^16, u32 bases: the whole-plane MFMA transform (rnt_mfma.hip)
     LAUNCH(k.t, rnt::K_MF_NTT_FWD, rnt::launch_mf_ntt(k, 0, b->data, ls), "MFMA forward transform");
+  } else if (rnt::whole_ok(k.t, 0)) {
+    // 2^10 <= N <= 2^14: the whole transform in one row launch
+    LAUNCH(k.t, rnt::K_WHOLE_FWD, rnt::launch_whole(k, 0, b->data, b->data, nullptr, ls), "whole-plane forward");
   } else {
     LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, b->data, b->data, nullptr, nullptr, ls, ls),
            "column forward");
@@ -1186,6 +1193,13 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   // workspace), the row kernel (both forward row passes, Montgomery
   // pointwise product, inverse rows), the inverse column pass.
   const uint64_t ls = limb_stride(out);
+  if (rnt::whole_ok(k.t, 2)) {
+    // 2^10 <= N <= 2^14: both transforms, the product and the inverse in
+    // one row launch, 3 planes per (poly, limb)
+    LAUNCH(k.t, rnt::K_WHOLE_MUL, rnt::launch_whole(k, 2, out->data, a->data, b->data, ls), "whole-plane product");
+    out->in_ntt = 0;
+    return RNT_OK;
+  }
   if (int rc = ensure_ws(out, poly_words(out) * word_bytes(k.t))) return rc;
   if (rnt::plane_ok(k.t)) {
     LAUNCH(k.t, rnt::K_PLANE_FUSED, rnt::launch_plane_fused(k, out->data, a->data, b->data, out->ws, ls),

@@ -121,7 +121,8 @@ struct Tables {
 enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
-  K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FUSED, K_MF_NTT_FWD, K_MF_NTT_INV, K_COUNT
+  K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FUSED, K_MF_NTT_FWD, K_MF_NTT_INV, K_WHOLE_FWD, K_WHOLE_INV, K_WHOLE_MUL,
+  K_COUNT
 };
 
 struct Prof {
@@ -212,6 +213,13 @@ hipError_t launch_mf_ntt(const Launch& k, int inverse, void* data, uint64_t ls);
 // multiplies degree-3 residues (u32 canonical bases, row length 2^(4k));
 // its inverse column pass then takes rfold = 2.
 bool mul_truncated(const Tables* t);
+// The whole-plane row path at 2^10 <= N <= 2^14 (u32 and u64; rnt_kernels.hip
+// k_row<..., WHOLE>): one launch per transform or product, every plane one
+// row.  mode 0: forward in place (x); 1: inverse in place (x); 2: out = x * y
+// in the coefficient domain (out may alias x or y).  whole_ok: the path serves
+// this mode on this basis.
+bool whole_ok(const Tables* t, int mode);
+hipError_t launch_whole(const Launch& k, int mode, void* out, void* x, const void* y, uint64_t ls);
 // Inverse column pass with n^-1 folded into the last stage; rfold adds the
 // Montgomery factor 2^w.  addend (optional, coefficient domain, out layout).
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,

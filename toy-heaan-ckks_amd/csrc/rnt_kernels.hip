@@ -366,6 +366,9 @@ __device__ __forceinline__ void pass_gs(W (&x)[NOPS][1 << LOGE], uint32_t node0,
 // Minimum resident waves per SIMD requested for the row kernels (caps their
 // VGPR budget at 512 / kRowMinWaves) and for the key-switch rows.
 constexpr int kRowMinWaves = 6;
+// ... and for the whole-plane u32 rows (two operand planes of 16 registers,
+// no spills at 128 VGPRs; the u64 rows are left unconstrained)
+constexpr int kWholeMinWaves = 4;
 constexpr int kKsMinWaves = 4;
 // Key rows of the key-switch rows kernel go global -> LDS directly
 // (global_load_lds, no registers) for u32 rows of >= 64 words, except in the
@@ -674,11 +677,18 @@ bool mul_truncated(const Tables* t) {
 }
 
 // mode 0: forward rows in place; 1: inverse rows in place;
-// 2: poly-mul rows: x <- INV(FWD(x) (.) FWD(y)) with Montgomery pointwise.
-template <class W, int MODE, int LOG_C, bool LZ = false>
-__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kRowMinWaves : 1)
-k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_n, uint32_t B,
-      uint64_t ls, uint64_t rows_total) {
+// 2: poly-mul rows: out <- INV(FWD(x) (.) FWD(y)) with Montgomery pointwise
+// (out = x in the four-step product).
+// WHOLE (log_n = LOG_C <= 14): a row is the whole plane (R = 1), so the
+// transforms are the whole network and the inverse's top stage applies the
+// folded n^-1 constants (with the Montgomery factor after a product, 4/N
+// after a truncated one) that the inverse column pass applies otherwise:
+// the product is one launch moving 3 planes per (poly, limb), a transform
+// one launch moving 2.
+template <class W, int MODE, int LOG_C, bool LZ = false, bool WHOLE = false>
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? (WHOLE ? kWholeMinWaves : kRowMinWaves) : 1)
+k_row(W* __restrict__ xg, const W* __restrict__ yg, W* __restrict__ outg, TabPtrs<W> tp, uint32_t log_n,
+      uint32_t B, uint64_t ls, uint64_t rows_total) {
   using G = RowGeo<LOG_C>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -701,7 +711,9 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
       v[1][i] = gload(yg, base + b0 + ((uint32_t)i << G::BB0));
     }
     const auto mo = mod_for<W, LZ>(lc);
-    W z[1][E];
+    // the product overwrites operand 0's registers (z aliases v[0]): the
+    // inverse then holds one plane, not three
+    W (&z)[1][E] = *reinterpret_cast<W(*)[1][E]>(&v[0]);
     if constexpr (trunc_mul<W, LOG_C, LZ>()) {
       // every pass but the last in full, the last without its two stages
       if constexpr (G::P > 1) fwd_pass<G, W, 2, 0>(v, rp.xp, lds, tw, mo);
@@ -722,10 +734,11 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
 #pragma unroll
         for (int k = 0; k < 4; ++k) z[0][4 * t + k] = c[k];
       }
-      inv_pass<G, W, 1, G::P - 1, false, 2>(z, rp.xp, lds, itw, mo, Fold<W>{});
-      if constexpr (G::P > 3) inv_pass<G, W, 1, 2, false>(z, rp.xp, lds, itw, mo, Fold<W>{});
-      if constexpr (G::P > 2) inv_pass<G, W, 1, 1, false>(z, rp.xp, lds, itw, mo, Fold<W>{});
-      if constexpr (G::P > 1) inv_pass<G, W, 1, 0, false>(z, rp.xp, lds, itw, mo, Fold<W>{});
+      const Fold<W> ft = WHOLE ? Fold<W>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p} : Fold<W>{};
+      inv_pass<G, W, 1, G::P - 1, WHOLE, 2>(z, rp.xp, lds, itw, mo, ft);
+      if constexpr (G::P > 3) inv_pass<G, W, 1, 2, WHOLE>(z, rp.xp, lds, itw, mo, ft);
+      if constexpr (G::P > 2) inv_pass<G, W, 1, 1, WHOLE>(z, rp.xp, lds, itw, mo, ft);
+      if constexpr (G::P > 1) inv_pass<G, W, 1, 0, WHOLE>(z, rp.xp, lds, itw, mo, ft);
     } else {
     xf_fwd<G, W, 2>(v, rp.xp, lds, tw, mo);
     if constexpr (LZ) {
@@ -742,11 +755,12 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
 #pragma unroll
       for (int i = 0; i < E; ++i) z[0][i] = mont_mul<W>(v[0][i], v[1][i], lc.q, lc.qinv);
     }
-    xf_inv<G, W, 1>(z, rp.xp, lds, itw, mo);
+    xf_inv<G, W, 1, WHOLE>(z, rp.xp, lds, itw, mo,
+                           WHOLE ? Fold<W>{lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p} : Fold<W>{});
     }
     if (rp.active) {
 #pragma unroll
-      for (int i = 0; i < E; ++i) gstore(xg, base + b0 + ((uint32_t)i << G::BB0), z[0][i]);
+      for (int i = 0; i < E; ++i) gstore(outg, base + b0 + ((uint32_t)i << G::BB0), z[0][i]);
     }
   } else if constexpr (MODE == 0) {
     W v[1][E];
@@ -761,7 +775,8 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, TabPtrs<W> tp, uint32_t log_
     W v[1][E];
 #pragma unroll
     for (int i = 0; i < E; ++i) v[0][i] = xg[base + bl + ((uint32_t)i << G::BBL)];
-    xf_inv<G, W, 1>(v, rp.xp, lds, itw, mod_of(lc));
+    xf_inv<G, W, 1, WHOLE>(v, rp.xp, lds, itw, mod_of(lc),
+                           WHOLE ? Fold<W>{lc.c1, lc.c1_p, lc.c2, lc.c2_p} : Fold<W>{});
     if (rp.active) {
 #pragma unroll
       for (int i = 0; i < E; ++i) xg[base + b0 + ((uint32_t)i << G::BB0)] = v[0][i];
@@ -1447,19 +1462,55 @@ static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const v
   return hipGetLastError();
 }
 
-template <class W, int MODE, int LOG_C, bool LZ = false>
-static hipError_t row_launch(const Launch& k, void* x, const void* y, uint64_t ls) {
+template <class W, int MODE, int LOG_C, bool LZ = false, bool WHOLE = false>
+static hipError_t row_launch(const Launch& k, void* x, const void* y, uint64_t ls, void* out = nullptr) {
   using G = RowGeo<LOG_C>;
   const Geom g = geom_for(k.t->log_n);
-  const uint64_t rows = (uint64_t)k.L * k.B * g.r;
+  const uint64_t rows = (uint64_t)k.L * k.B * (WHOLE ? 1 : g.r);
   if (rows == 0) return hipSuccess;
-  const unsigned blocks = (unsigned)((rows + G::RPW - 1) / G::RPW);
+  const uint64_t blocks = (rows + G::RPW - 1) / G::RPW;
+  if (blocks > 0x7fffffffull) return hipErrorInvalidConfiguration;
   const size_t lds = row_lds<W, LOG_C>(MODE == 2 ? 2 : 1);
-  hipError_t e = allow_lds(k_row<W, MODE, LOG_C, LZ>, lds);
+  hipError_t e = allow_lds(k_row<W, MODE, LOG_C, LZ, WHOLE>, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_row<W, MODE, LOG_C, LZ>), dim3(blocks), dim3(G::THREADS), lds, k.s, (W*)x,
-                     (const W*)y, tab_ptrs<W>(k.t), g.log_n, (uint32_t)k.B, ls, rows);
+  hipLaunchKernelGGL((k_row<W, MODE, LOG_C, LZ, WHOLE>), dim3((unsigned)blocks), dim3(G::THREADS), lds, k.s,
+                     (W*)x, (const W*)y, (W*)(out ? out : x), tab_ptrs<W>(k.t), WHOLE ? (uint32_t)LOG_C : g.log_n,
+                     (uint32_t)k.B, ls, rows);
   return hipGetLastError();
+}
+
+// The whole-plane row path (k_row<..., WHOLE>): every (poly, limb) plane is
+// one row.  u32 and u64 words at 2^10 <= N <= 2^14 (a row of 2^14 words is
+// 1024 threads x 16 registers); RNT_PLANE=0 keeps the four-step kernels.
+// The u64 product stays on the four-step kernels above 2^12: its rows need
+// ~150 VGPRs, so a CU holds one 512- or 1024-thread workgroup of them (two
+// waves per SIMD) and measured slower (N = 2^13 x 7 x 61-bit: 0.67M against
+// 0.76M poly-muls/s; capped at 128 VGPRs it spills 76 bytes a lane).
+bool whole_ok(const Tables* t, int mode) {
+  if (t->plane == 0 || t->log_n < 10 || t->log_n > 14) return false;
+  return !(t->wide && mode == 2 && t->log_n > 12);
+}
+
+template <class W>
+static hipError_t whole_t(const Launch& k, int mode, void* out, void* x, const void* y, uint64_t ls, bool lz) {
+#define RNT_W(C)                                                                                      \
+  case C:                                                                                             \
+    if (mode == 0) return row_launch<W, 0, C, false, true>(k, x, nullptr, ls);                        \
+    if (mode == 1) return row_launch<W, 1, C, false, true>(k, x, nullptr, ls);                        \
+    if constexpr (sizeof(W) == 4) {                                                                   \
+      if (lz) return row_launch<W, 2, C, true, true>(k, x, y, ls, out);                               \
+    }                                                                                                 \
+    if constexpr (sizeof(W) == 8 && C > 12) return hipErrorInvalidValue; /* whole_ok */              \
+    else return row_launch<W, 2, C, false, true>(k, x, y, ls, out);
+  switch (k.t->log_n) {
+    RNT_W(10)
+    RNT_W(11)
+    RNT_W(12)
+    RNT_W(13)
+    RNT_W(14)
+    default: return hipErrorInvalidValue;
+  }
+#undef RNT_W
 }
 
 template <class W>
@@ -1827,6 +1878,11 @@ hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* ou
 hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls, bool lazy) {
   const bool lz = lazy && lazy30_ok(k.t);
   RNT_WIDE(row_t<uint32_t>(k, mode, x, y, ls, lz), row_t<uint64_t>(k, mode, x, y, ls, false));
+}
+hipError_t launch_whole(const Launch& k, int mode, void* out, void* x, const void* y, uint64_t ls) {
+  // the Harvey-lazy arithmetic where every modulus < 2^30 (as rnt_mul's four-step path)
+  const bool lz = !k.t->wide && k.t->lazy30;
+  RNT_WIDE(whole_t<uint32_t>(k, mode, out, x, y, ls, lz), whole_t<uint64_t>(k, mode, out, x, y, ls, false));
 }
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
                           uint64_t in_ls, int rfold, const void* addend, bool lazy) {
