@@ -42,7 +42,7 @@ def _run_ranks(comm, body):
             results[r] = body(r)
         except BaseException as e:  # surface thread failures in the test
             errors.append(e)
-            comm._bar.abort()
+            comm.abort()
 
     ths = [threading.Thread(target=main, args=(r,)) for r in range(world)]
     for t in ths:

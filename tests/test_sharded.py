@@ -130,6 +130,77 @@ def test_limb_sharded_gloo_matches_unsharded(world, L, B, chunk):
         assert np.array_equal(g.astype(np.uint64), w)
 
 
+@pytest.mark.parametrize("world,L,B,chunk", [(2, 4, 3, 1), (3, 7, 5, 2)])
+def test_limb_sharded_thread_ranks_async_joins(world, L, B, chunk):
+    """ThreadComm's joins run on helper threads and wait() blocks until the
+    join is done.  The joins are held at a gate until every rank has issued
+    the relin all-gather of EVERY chunk (which it can only do if starting a
+    join does not wait for it: the chunks' tensor products run while the
+    earlier chunks' joins are in flight); then the pipeline finishes and the
+    assembled limbs must equal the unsharded oracle pipeline."""
+    import threading
+    import time
+
+    from rns_ntt.sharded import LimbShardedPipeline, ThreadComm
+    from shard_oracle_backend import OracleBackend
+
+    n, seed = 32, 9
+    mods = orc.generate_primes(31, L, n)
+    cts, key_a, key_b = _inputs(mods, n, B, seed)
+    comm = ThreadComm(world)
+    gate, lock, calls = threading.Event(), threading.Lock(), []
+    real_join = comm._join
+
+    class Gated:
+        def __init__(self, bar):
+            self._b = bar
+
+        def wait(self):
+            gate.wait()
+            return self._b.wait()
+
+        def abort(self):
+            self._b.abort()
+
+    def recording_join(seq):
+        j = real_join(seq)
+        with lock:
+            calls.append(seq)
+            if not isinstance(j.bar, Gated):
+                j.bar = Gated(j.bar)
+        return j
+
+    comm._join = recording_join
+    results, errors = [None] * world, []
+
+    def rank_main(r):
+        try:
+            pipe = LimbShardedPipeline(mods, n, comm.rank_view(r), OracleBackend(), chunk=chunk)
+            relin, resc = _run_rank(pipe, cts, key_a, key_b)
+            results[r] = (r, (pipe.limbs.start, pipe.limbs.stop), relin, resc)
+        except BaseException as e:  # surface thread failures in the test
+            errors.append(e)
+            comm.abort()
+
+    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    chunks = -(-B // chunk)
+    t0 = time.time()
+    while len(calls) < world * chunks and time.time() - t0 < 60:
+        time.sleep(0.01)
+    issued = len(calls)
+    gate.set()
+    for t in threads:
+        t.join(timeout=120)
+    assert issued == world * chunks, (issued, world * chunks)
+    assert not errors, errors
+    got = _assemble(results)
+    want = _oracle_reference(mods, n, cts, key_a, key_b)
+    for g, w in zip(got, want):
+        assert np.array_equal(g.astype(np.uint64), w)
+
+
 ROT_K = (1, -3, 0)  # slot offsets; negative = rotate_slots(k < 0), 0 = identity
 
 
@@ -248,7 +319,7 @@ def test_limb_sharded_gpu_threads_match_unsharded(gpu, world, shared):
             results[r] = (r, (pipe.limbs.start, pipe.limbs.stop), relin, resc)
         except BaseException as e:  # surface thread failures in the test
             errors.append(e)
-            comm._bar.abort()
+            comm.abort()
 
     threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
     for t in threads:
@@ -294,7 +365,7 @@ def test_limb_sharded_rotation_gpu_threads_match_unsharded(gpu, world):
             results[r] = _run_rank_rotate(pipe, c0, c1, key_a, key_b)
         except BaseException as e:  # surface thread failures in the test
             errors.append(e)
-            comm._bar.abort()
+            comm.abort()
 
     threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
     for t in threads:

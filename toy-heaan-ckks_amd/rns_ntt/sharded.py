@@ -125,15 +125,87 @@ class SingleComm:
 
 
 class ThreadComm:
-    """`world` simulated ranks as threads of one process (one GPU)."""
+    """`world` simulated ranks as threads of one process (one GPU).
+
+    The async joins are real: each starts a helper thread that waits for the
+    producing rank's stream, meets the other ranks' helpers of the same join
+    (the k-th join of every rank: the ranks issue their joins in the same
+    order) at that join's own barrier, and builds the result; wait() blocks
+    until the helper is done.  So the pipeline's overlap and ordering -- the
+    joins of chunk k in flight while chunk k+1's tensor product runs, each
+    consumer waiting only for its own join -- are exercised as on RCCL."""
 
     def __init__(self, world: int):
         self.world = world
         self._bar = threading.Barrier(world)
-        self._slots: list[Any] = [None] * world
+        self._lock = threading.Lock()
+        self._joins: dict[int, "_ThreadJoin"] = {}
+        self._aborted = False
 
     def rank_view(self, rank: int) -> "_ThreadRank":
         return _ThreadRank(self, rank)
+
+    def _join(self, seq: int) -> "_ThreadJoin":
+        with self._lock:
+            j = self._joins.get(seq)
+            if j is None:
+                j = self._joins[seq] = _ThreadJoin(self.world)
+                if self._aborted:
+                    j.bar.abort()
+            return j
+
+    def _done(self, seq: int, j: "_ThreadJoin"):
+        with self._lock:
+            j.finished += 1
+            if j.finished == self.world:
+                self._joins.pop(seq, None)
+
+    def abort(self):
+        """Break every barrier (a failing rank must not leave the others
+        waiting in a join)."""
+        self._bar.abort()
+        with self._lock:
+            for j in self._joins.values():
+                j.bar.abort()
+            self._aborted = True
+
+
+class _ThreadJoin:
+    def __init__(self, world: int):
+        self.bar = threading.Barrier(world)
+        self.slots: list[Any] = [None] * world
+        self.finished = 0
+
+
+class _ThreadPending:
+    """A join running on a helper thread; wait() blocks until it is done and
+    returns its result (re-raising the helper's exception).  On a GPU the
+    result is also marked as used by the waiter's current stream, so the
+    caching allocator keeps it until that stream's queued work is done."""
+
+    def __init__(self, fn):
+        self._res: list[Any] = []
+        self._err: list[BaseException] = []
+
+        def run():
+            try:
+                self._res.append(fn())
+            except BaseException as e:  # surfaced by wait()
+                self._err.append(e)
+
+        self._t = threading.Thread(target=run, daemon=True)
+        self._t.start()
+
+    def wait(self):
+        self._t.join()
+        if self._err:
+            raise self._err[0]
+        out = self._res[0]
+        if getattr(out, "is_cuda", False):
+            import torch
+
+            out.record_stream(torch.cuda.current_stream(out.device))
+        return out
 
 
 class _ThreadRank:
@@ -141,44 +213,78 @@ class _ThreadRank:
         self._c = comm
         self.rank = rank
         self.world = comm.world
+        self._seq = 0
+
+    def _next(self) -> tuple[int, "_ThreadJoin"]:
+        seq = self._seq
+        self._seq += 1
+        return seq, self._c._join(seq)
 
     def all_gather_limbs(self, local, counts: Sequence[int]):
-        import torch
-
-        c = self._c
-        c._slots[self.rank] = local
-        _stream_done(local)  # ranks read each other's tensors from their own streams
-        c._bar.wait()
-        out = torch.cat([s for s in c._slots], 0)
-        _stream_done(out)
-        c._bar.wait()
-        return out
+        return self.all_gather_limbs_async(local, counts).wait()
 
     def all_gather_limbs_async(self, local, counts: Sequence[int]):
-        return _Done(self.all_gather_limbs(local, counts))
+        seq, j = self._next()
+        producer = _current_stream(local)  # the rank's stream that wrote `local`
+
+        def run():
+            import torch
+
+            _device_of(local)
+            _stream_sync(producer)
+            j.slots[self.rank] = local
+            j.bar.wait()
+            out = torch.cat(list(j.slots), 0)
+            _stream_sync(_current_stream(out))
+            j.bar.wait()  # every rank has its copy before the slots go
+            self._c._done(seq, j)
+            return out
+
+        return _ThreadPending(run)
 
     def broadcast(self, t, src: int):
-        c = self._c
-        if self.rank == src:
-            c._slots[src] = t
-            _stream_done(t)
-        c._bar.wait()
-        if self.rank != src:
-            t.copy_(c._slots[src])
-            _stream_done(t)
-        c._bar.wait()
-        return t
+        return self.broadcast_async(t, src).wait()
 
     def broadcast_async(self, t, src: int):
-        return _Done(self.broadcast(t, src))
+        seq, j = self._next()
+        producer = _current_stream(t)
+
+        def run():
+            _device_of(t)
+            _stream_sync(producer)
+            if self.rank == src:
+                j.slots[src] = t
+            j.bar.wait()
+            if self.rank != src:
+                t.copy_(j.slots[src])
+                _stream_sync(_current_stream(t))
+            j.bar.wait()
+            self._c._done(seq, j)
+            return t
+
+        return _ThreadPending(run)
 
 
-def _stream_done(t):
-    """Wait for this thread's current stream when `t` lives on a GPU."""
+def _current_stream(t):
+    """The calling thread's current stream on `t`'s device (None on the CPU)."""
     if getattr(t, "is_cuda", False):
         import torch
 
-        torch.cuda.current_stream(t.device).synchronize()
+        return torch.cuda.current_stream(t.device)
+    return None
+
+
+def _stream_sync(stream):
+    if stream is not None:
+        stream.synchronize()
+
+
+def _device_of(t):
+    """Make `t`'s device current in a helper thread."""
+    if getattr(t, "is_cuda", False):
+        import torch
+
+        torch.cuda.set_device(t.device)
 
 
 # ---------------------------------------------------------------------------
