@@ -805,15 +805,25 @@ __device__ __forceinline__ uint32_t ks_pad(uint32_t w) { return w + ((w >> 6) <<
 // measured slower, ks_rows 2.40 against 2.31 ms per 64-ct chunk,
 // profiles/r03/ab_ks_spre.txt, as register prefetch of the next limb did
 // before it: the rows kernel does not wait on the S loads.)
+//  * KSPLIT: when even one {key_b, key_a} buffer would push the workgroup
+//    past a quarter of the LDS (the one-poly grid, NP = 1: 8 or 16 rows of
+//    both keys beside the exchange region, 52 KiB), key_a's rows go into
+//    the exchange region once the transform's last exchange is done, so
+//    four workgroups fit a CU (three left a 1024-workgroup grid 1.33
+//    rounds long).
 template <class W, int LOG_C, int NP>
 struct KsCfg {
   using G = RowGeo<LOG_C>;
   static constexpr int KROWS = G::RPW / NP;
   static constexpr int KPAD = ks_kpad_words<W>(G::C);
-  static constexpr bool KEYGLDS = sizeof(W) == 4 && G::C >= 64 && (NP > 1 || LOG_C >= kKsGldsWideMinLogC);
   static constexpr bool KDOUBLE =
       (size_t)(G::REGION + 4 * KROWS * KPAD) * sizeof(W) <= 40u * 1024u || KROWS == 1;
-  static constexpr int KWORDS = (KDOUBLE ? 4 : 2) * KROWS * KPAD;
+  static constexpr bool KSPLIT = sizeof(W) == 4 && G::C >= 64 && !KDOUBLE && G::P >= 2 &&
+                                 (size_t)(G::REGION + 2 * KROWS * KPAD) * sizeof(W) > 40u * 1024u &&
+                                 KROWS * KPAD <= G::REGION;
+  static constexpr bool KEYGLDS =
+      sizeof(W) == 4 && G::C >= 64 && (NP > 1 || LOG_C >= kKsGldsWideMinLogC || KSPLIT);
+  static constexpr int KWORDS = (KDOUBLE ? 4 : KSPLIT ? 1 : 2) * KROWS * KPAD;
   static constexpr size_t LDS_BYTES = (size_t)(G::REGION + KWORDS) * sizeof(W);
 };
 
@@ -884,6 +894,7 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   constexpr int KPT = (2 * KROWS * C + G::THREADS - 1) / G::THREADS;  // key words per thread per i
   constexpr bool kKeyGlds = K::KEYGLDS;
   constexpr bool KDOUBLE = K::KDOUBLE;
+  constexpr bool KSPLIT = K::KSPLIT;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
   // [buffers][key_b rows | key_a rows]
@@ -958,10 +969,11 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
       constexpr int WAVES = G::THREADS / 64;
       const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
       const uint32_t lane = threadIdx.x & 63u;
+      constexpr uint32_t NK = KSPLIT ? 1 : 2;  // keys loaded here (KSPLIT: key_a after the transform)
 #pragma unroll
-      for (int m = 0; m < (int)((2 * SEG + WAVES - 1) / WAVES); ++m) {
+      for (int m = 0; m < (int)((NK * SEG + WAVES - 1) / WAVES); ++m) {
         const uint32_t sg = wave + (uint32_t)m * WAVES;
-        if (sg < 2 * SEG) {
+        if (sg < NK * SEG) {
           const uint32_t kk = sg >= SEG, rs = kk ? sg - SEG : sg;  // key, segment within it
           const W* src = (kk ? key_a : key_b) + kbase + rs * 64u + lane;
           W* dst = kb + kk * (KROWS * KPAD) + (rs / (C / 64)) * KPAD + ks_pad((rs % (C / 64)) * 64u);
@@ -1004,13 +1016,38 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     if constexpr (G::P < 2) __syncthreads();
     xf_fwd<G, W, 1>(x, rp.xp, lds, tw, mod_of(lc));
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (KSPLIT) {
+      // the transform's last exchange has ended in a barrier: the exchange
+      // region takes key_a's rows while acc0 takes key_b's
+      constexpr uint32_t SEG = KW / 64;
+      constexpr int WAVES = G::THREADS / 64;
+      const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+      const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+      for (int m = 0; m < (int)((SEG + WAVES - 1) / WAVES); ++m) {
+        const uint32_t rs = wave + (uint32_t)m * WAVES;
+        if (rs < SEG) {
+          const W* src = key_a + kbase + rs * 64u + lane;
+          W* dst = lds + (rs / (C / 64)) * KPAD + ks_pad((rs % (C / 64)) * 64u);
+          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
     // the last pass leaves a thread's E values at consecutive positions
     // (G::BBL == 0): the keys come back 16 bytes at a time, one key after
     // the other
     static_assert(G::BBL == 0, "last row pass distribution");
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
-      const W* kk = kb + o * KROWS * KPAD + (WIDE ? (rp.xp.slot / NP) * KPAD : 0u) + ks_pad(bl);
+      if (KSPLIT && o == 1) {
+        // every wave's key_a rows have landed and are visible
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      const W* kk = (KSPLIT && o == 1 ? lds : kb + o * KROWS * KPAD) + (WIDE ? (rp.xp.slot / NP) * KPAD : 0u) +
+                    ks_pad(bl);
       constexpr int V = 16 / sizeof(W);
 #pragma unroll
       for (int e0 = 0; e0 < E; e0 += V) {
@@ -1033,6 +1070,9 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  // (KSPLIT: every thread's reads of the last key_a rows end before the
+  // inverse's exchanges write that region)
+  if constexpr (KSPLIT) __syncthreads();
   // the two accumulators' inverse rows one after the other (half the live
   // registers of a two-operand pass).  The thread coordinates pass through
   // an opaque copy, so the inverse passes' twiddle and store addresses are
