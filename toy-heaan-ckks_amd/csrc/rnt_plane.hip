@@ -50,9 +50,14 @@ namespace rnt {
 namespace plane {
 constexpr int T = 1024;
 constexpr int XS = 17;                  // X2 buffer row stride (words): conflict-free both ways
-constexpr int XW = 64 * XS;             // words of one X2 buffer
-constexpr int LDS_WORDS = 16 * 2 * XW;  // two X2 buffers per wave; >= 2^15 (an X1 round)
-static_assert(LDS_WORDS >= (1 << 15), "X1 round");
+constexpr int XW = 64 * XS;             // words of one X2 buffer (one per wave)
+constexpr int X1_WORDS = 1 << 15;       // an X1 round; the X2 buffers share it
+static_assert(16 * XW <= X1_WORDS, "X2 buffers inside the X1 region");
+// The first HAT_LDS blocks of a^ (of 16 per thread) stay in the LDS beside
+// the exchange region instead of going to the scratch plane and back.
+constexpr int HAT_LDS = 2;
+constexpr int LDS_WORDS = X1_WORDS + HAT_LDS * T * 4;
+static_assert(LDS_WORDS * 4 <= 160 * 1024, "LDS of a CU");
 __host__ __device__ constexpr int slot0(int r) { return r; }
 __host__ __device__ constexpr int slot1(int r) { return 2 * (((r >> 5) << 4) | (r & 15)) + ((r >> 4) & 1); }
 __host__ __device__ constexpr int slot2(int r) { return slot1(r); }
@@ -358,7 +363,8 @@ __device__ __forceinline__ void plane_swap54(uint32_t (&x)[64]) {
 // (lane, m & 15) at lane * 17 + (m & 15), read back by lane' as register
 // (g << 4) | c from lane (lane' & 48) | c, column lane' & 15 (both
 // directions 64 distinct banks).  LDS instructions of one wave execute in
-// order, so the reads see the same wave's writes; two buffers alternate.
+// order, so the reads see the same wave's writes (and the next round's
+// writes come after them): one buffer per wave.
 template <bool TO_L2>
 __device__ __forceinline__ void plane_x2(uint32_t (&x)[64], uint32_t* lds, uint32_t t) {
   const uint32_t w = t >> 6, lam = t & 63u;
@@ -367,7 +373,7 @@ __device__ __forceinline__ void plane_x2(uint32_t (&x)[64], uint32_t* lds, uint3
   const uint32_t a2 = (lam & 48u) * plane::XS + (lam & 15u);     // + c * XS
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    uint32_t* buf = lds + (w * 2u + (uint32_t)(g & 1)) * plane::XW;
+    uint32_t* buf = lds + w * plane::XW;
 #pragma unroll
     for (int j = 0; j < 16; ++j) buf[TO_L2 ? a15 + j : a2 + j * plane::XS] = x[plane::slot1((g << 4) | j)];
     __builtin_amdgcn_wave_barrier();
@@ -571,11 +577,20 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
 }
 
 // a^ in the private layout: block kk (4 words) of thread t at (kk * 1024 + t) * 4
-__device__ __forceinline__ void plane_store_hat(const HatBuf& dst, const uint32_t (&x)[64], uint32_t t) {
+// of the scratch plane, the first HAT_LDS blocks at the same place in the
+// LDS past the exchange region (each thread reads back only its own).
+__device__ __forceinline__ uint4* hat_lds(uint32_t* lds) { return (uint4*)(lds + plane::X1_WORDS); }
+__device__ __forceinline__ void plane_store_hat(const HatBuf& dst, const uint32_t (&x)[64], uint32_t t,
+                                                uint32_t* lds) {
 #pragma unroll
-  for (int kk = 0; kk < 16; ++kk)
-    dst.st(t, kk, x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
-           x[plane::slot2(4 * kk + 3)]);
+  for (int kk = 0; kk < 16; ++kk) {
+    if (kk < plane::HAT_LDS)
+      hat_lds(lds)[kk * plane::T + t] = make_uint4(x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)],
+                                                   x[plane::slot2(4 * kk + 2)], x[plane::slot2(4 * kk + 3)]);
+    else
+      dst.st(t, kk, x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
+             x[plane::slot2(4 * kk + 3)]);
+  }
 }
 
 // The product of one (poly, limb) plane pair: a -> a^ through the scratch
@@ -596,7 +611,7 @@ __device__ __forceinline__ void plane_fused_one(uint32_t* __restrict__ c, const 
   plane_load(x, a + off, t);
   PLANE_STAMP(0, 1);
   plane_fwd<0, false>(x, lds, t, tw, mo, trace_id);
-  plane_store_hat(HatBuf(ah), x, t);
+  plane_store_hat(HatBuf(ah), x, t, lds);
   PLANE_STAMP(0, 7);
   PLANE_STAMP(1, 0);
   plane_load(x, b + off, t);
@@ -608,7 +623,9 @@ __device__ __forceinline__ void plane_fused_one(uint32_t* __restrict__ c, const 
   uint32_t* ah2 = ah;
   asm volatile("" : "+s"(ah2));
   const HatBuf hb(ah2);
-  plane_mul_tail<1>(x, lds, t, [hb, t](int kk) { return hb.ld(t, kk); }, c + off, tw, tp.itw + (uint64_t)l * N, lc,
+  plane_mul_tail<1>(x, lds, t,
+                    [hb, t, lds](int kk) { return kk < plane::HAT_LDS ? hat_lds(lds)[kk * plane::T + t] : hb.ld(t, kk); },
+                    c + off, tw, tp.itw + (uint64_t)l * N, lc,
                     mo, trace_id);
 }
 
