@@ -142,7 +142,11 @@ __device__ __forceinline__ int32_t recomb(int32_t c0, int32_t c1, int32_t c2, in
   const int32_t lo = c0 + (int32_t)((uint32_t)c1 << 8);
   const int32_t hi = c2 + (int32_t)((uint32_t)c3 << 8);
   int64_t t;
-  t = (int64_t)lo * m.one + (WK ? m.K : m.K0);
+  if constexpr (WK) {
+    t = (int64_t)lo * m.one + m.K;  // the digit bias rides in the addend's high word
+  } else {
+    t = (int64_t)lo;  // sign extension: one shift instead of a 64-bit multiply-add
+  }
   t = (int64_t)hi * m.s16 + t;
   const uint32_t mm = (uint32_t)t * m.nqinv;
   const int64_t v = (int64_t)(int32_t)mm * m.q + t;
