@@ -569,7 +569,8 @@ def run_ctmul_graph(args, comm, world, rank, local_rank):
 
     g, elapsed, kms, kernels = _graph_step_timing(
         Bs, step, args.steps, args.warmup, comm,
-        ("col_fwd", "tensor_rows", "col_inv", "ks_decompose", "ks_rows", "rescale", "elementwise"))
+        ("col_fwd", "tensor_rows", "col_inv", "ks_decompose", "ks_rows", "rescale", "elementwise", "tensor_whole",
+         "ks_whole"))
     ms_per_step = elapsed / args.steps * 1e3
     value = B * args.steps * world / elapsed
     parity_ok = None
@@ -589,6 +590,13 @@ def run_ctmul_graph(args, comm, world, rank, local_rank):
         bfly = B * (L * L + 2 * L) * (n // 2) * log_c
         ach = bfly / (kernels["ks_rows"]["total_ms"] * 1e-3)
         roof.update(achieved=ach, frac=ach / VALU_PEAK_BFLY, bfly_per_launch=bfly / kernels["ks_rows"]["launches"])
+    elif "ks_whole" in kernels:
+        # k_ks_whole: whole forward transforms of every (source, target) pair
+        # and whole inverses of both accumulators
+        bfly = B * args.steps * (L * L + 2 * L) * (n // 2) * args.log_n
+        ach = bfly / (kernels["ks_whole"]["total_ms"] * 1e-3)
+        roof.update(kernel="ks_whole", achieved=ach, frac=ach / VALU_PEAK_BFLY,
+                    bfly_per_launch=bfly / kernels["ks_whole"]["launches"])
     return {
         "metric": CT_METRIC,
         "value": value,
@@ -684,7 +692,8 @@ def run_ctmul(args, comm, world, rank, local_rank):
     elapsed = comm.max(t1 - t0)
     value = B_global * args.steps / elapsed
     kernels = {}
-    for k in ("col_fwd", "tensor_rows", "col_inv", "ks_decompose", "ks_rows", "rescale", "elementwise"):
+    for k in ("col_fwd", "tensor_rows", "col_inv", "ks_decompose", "ks_rows", "rescale", "elementwise",
+              "tensor_whole", "ks_whole"):
         cnt, ms = prof_basis.profile_read(k)
         if cnt:
             kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
@@ -749,6 +758,11 @@ def run_ctmul(args, comm, world, rank, local_rank):
         roof.update(achieved=ach, frac=ach / VALU_PEAK_BFLY,
                     bfly_per_launch=bfly / kernels["ks_rows"]["launches"],
                     traffic=traffic_for("ks_rows", "ctmul", args.ct_batch, args.log_n, L))
+    elif "ks_whole" in kernels:
+        bfly = B * args.steps * (L * Lr + 2 * Lr) * (n // 2) * args.log_n
+        ach = bfly / (kernels["ks_whole"]["total_ms"] * 1e-3)
+        roof.update(kernel="ks_whole", achieved=ach, frac=ach / VALU_PEAK_BFLY,
+                    bfly_per_launch=bfly / kernels["ks_whole"]["launches"])
     return {
         "metric": CT_METRIC,
         "value": value,
@@ -832,7 +846,7 @@ def run_rotate(args, comm, world, rank, local_rank):
             rn.check(lib.rnt_ct_rotate(out0.handle, out1.handle, c0.handle, c1.handle, k,
                                        key.a.handle, key.b.handle))
 
-    rot_kernels = ("ks_decompose", "ks_rows", "col_inv", "automorphism", "col_fwd", "row_fwd")
+    rot_kernels = ("ks_decompose", "ks_rows", "col_inv", "automorphism", "col_fwd", "row_fwd", "ks_whole")
     graph_info = None
     if args.graph:
         # the reference's call shape replayed: the whole sweep step recorded
@@ -880,6 +894,11 @@ def run_rotate(args, comm, world, rank, local_rank):
         roof.update(achieved=ach, frac=ach / VALU_PEAK_BFLY,
                     bfly_per_launch=bfly_rows / kernels["ks_rows"]["launches"],
                     traffic=traffic_for("ks_rows", "rotate", B, log_n, L))
+    elif "ks_whole" in kernels:
+        bfly = B * len(offsets) * args.steps * (L * L + 2 * L) * (n // 2) * log_n
+        ach = bfly / (kernels["ks_whole"]["total_ms"] * 1e-3)
+        roof.update(kernel="ks_whole", achieved=ach, frac=ach / VALU_PEAK_BFLY,
+                    bfly_per_launch=bfly / kernels["ks_whole"]["launches"])
 
     parity_ok = None
     cpu = None

@@ -95,7 +95,7 @@ thread_local Capture* g_capture = nullptr;
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
-    "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd", "whole_inv", "whole_mul"};
+    "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd", "whole_inv", "whole_mul", "ks_whole", "tensor_whole"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -109,8 +109,23 @@ hipEvent_t prof_event(rnt::Prof* p) {
 }
 
 // Bracket one launch with events when profiling is on.
+// A launcher reports hipGetLastError() after its launch, so an error an
+// earlier unchecked call left in the thread's last-error slot (a cleanup
+// path's hipFree / hipEventDestroy) would be blamed on it: the slot is read
+// and cleared first (RNT_TRACE_STALE=1 names what it held).
+inline void clear_stale_error(int id) {
+  const hipError_t pre = hipGetLastError();
+  static const bool trace = [] {
+    const char* v = std::getenv("RNT_TRACE_STALE");
+    return v && *v && *v != '0';
+  }();
+  if (pre != hipSuccess && trace)
+    std::fprintf(stderr, "rnsntt: stale HIP error before %s: %s\n", kKernelNames[id], hipGetErrorString(pre));
+}
+
 template <class F>
 hipError_t prof_launch(const rnt::Tables* t, hipStream_t s, int id, F&& f) {
+  clear_stale_error(id);
   rnt::Prof* p = t->prof;
   if (p == nullptr || !p->on || g_capture != nullptr) return f();
   std::lock_guard<std::mutex> g(p->mu);
@@ -1718,11 +1733,19 @@ int check_key(const rnt_buf* d, const rnt_buf* key_a, const rnt_buf* key_b) {
 // row_pos_pfast), so bigger chunks cut key traffic per ciphertext; 4 GiB is
 // a small slice of the 288 GB.
 size_t ks_chunk(const rnt::Tables* t, size_t L, size_t B) {
-  const size_t per = L * L * t->n * (t->wide ? 8 : 4);
+  // (the whole-plane key-switch has no S: its chunk is bounded by the
+  // ct-mul's seven chunk-local planes per limb instead)
+  const size_t per = (rnt::ks_whole_ok(t) ? 7 * L : L * L) * t->n * (t->wide ? 8 : 4);
   size_t c = t->ks_ws_bytes;
   c = per ? c / per : B;
   if (c < 1) c = 1;
   return std::min(c, B);
+}
+
+// Key-switch scratch of a chunk of bc polys (words): S | U0 | U1, or none
+// for the whole-plane key-switch.
+size_t ks_scratch_words(const rnt::Tables* t, size_t L, size_t bc) {
+  return rnt::ks_whole_ok(t) ? 0 : (L * L + 2 * L) * bc * t->n;
 }
 
 // Decomposition + key-switch rows of one chunk (k.B polys, k.L target limbs,
@@ -1749,6 +1772,18 @@ int ks_chunk_run(rnt::Launch k, void* ws, const rnt_buf* d, size_t p0, size_t bc
                  const void* add0, int with_init) {
   const size_t n = k.t->n, L = k.L, wb = k.t->wide ? 8 : 4;
   k.B = bc;
+  if (rnt::ks_whole_ok(k.t)) {
+    // 2^10 <= N <= 2^14: one launch, no S (ws unused)
+    const char* i0 = with_init && init0 ? (const char*)init0 + p0 * n * wb : nullptr;
+    const char* i1 = with_init && init1 ? (const char*)init1 + p0 * n * wb : nullptr;
+    const char* a0 = add0 ? (const char*)add0 + p0 * n * wb : nullptr;
+    LAUNCH(k.t, rnt::K_KS_WHOLE,
+           rnt::launch_ks_whole(k, (char*)out0 + p0 * n * wb, (char*)out1 + p0 * n * wb, out_ls,
+                                (const char*)d->data + p0 * n * wb, limb_stride(d), key_a->data, key_b->data,
+                                limb_stride(key_a), i0, i1, init_ls, a0),
+           "whole-plane key-switch");
+    return RNT_OK;
+  }
   char* S = (char*)ws;
   char* U0 = S + L * L * bc * n * wb;
   char* U1 = U0 + L * bc * n * wb;
@@ -1780,10 +1815,10 @@ extern "C" int rnt_keyswitch(rnt_buf* acc0, rnt_buf* acc1, const rnt_buf* d, con
     return fail(RNT_ERR_BAD_ARGUMENT, "rnt_keyswitch: outputs must not alias each other or d");
   if (int rc = set_device(d->ctx)) return rc;
   rnt::Launch k = launch_for(d);
-  const size_t L = k.L, n = k.t->n, wb = word_bytes(k.t);
+  const size_t L = k.L, wb = word_bytes(k.t);
   const size_t bc = ks_chunk(k.t, L, d->n_polys);
   CallWs ws(acc0);
-  if (int rc = ws.get((L * L + 2 * L) * bc * n * wb)) return rc;
+  if (int rc = ws.get(std::max<size_t>(ks_scratch_words(k.t, L, bc) * wb, 16))) return rc;
   for (size_t p0 = 0; p0 < d->n_polys; p0 += bc) {
     const size_t c = std::min(bc, d->n_polys - p0);
     if (int rc = ks_chunk_run(k, ws.p, d, p0, c, key_a, key_b, acc0->data, acc1->data,
@@ -1822,12 +1857,24 @@ extern "C" int rnt_keyswitch_ext(rnt_buf* acc0, rnt_buf* acc1, const void* src, 
   if (int rc = set_device(acc0->ctx)) return rc;
   rnt::Launch k = launch_for(acc0);
   const size_t Lt = k.L, Ls = src_limbs, n = k.t->n, wb = word_bytes(k.t), B = acc0->n_polys;
+  const uint64_t src_ls = (uint64_t)B * n, full_ls = limb_stride(acc0);
+  if (rnt::ks_whole_ok(k.t)) {
+    // 2^10 <= N <= 2^14: the whole batch in one launch, no S
+    rnt::Launch kw = k;
+    kw.Ls = Ls;
+    LAUNCH(kw.t, rnt::K_KS_WHOLE,
+           rnt::launch_ks_whole(kw, acc0->data, acc1->data, full_ls, src, src_ls, key_a->data, key_b->data,
+                                limb_stride(key_a), init0 ? init0->data : nullptr, init1 ? init1->data : nullptr,
+                                full_ls, nullptr),
+           "whole-plane key-switch");
+    acc0->in_ntt = acc1->in_ntt = 0;
+    return RNT_OK;
+  }
   // polys per chunk: S is [Lt][Ls][Bc][N]
   size_t bc = std::max<size_t>(1, k.t->ks_ws_bytes / std::max<size_t>(1, Lt * Ls * n * wb));
   bc = std::min(bc, B);
   CallWs ws(acc0);
   if (int rc = ws.get((Lt * Ls + 2 * Lt) * bc * n * wb)) return rc;
-  const uint64_t src_ls = (uint64_t)B * n, full_ls = limb_stride(acc0);
   for (size_t p0 = 0; p0 < B; p0 += bc) {
     rnt::Launch kc = k;
     kc.B = std::min(bc, B - p0);
@@ -1867,11 +1914,19 @@ extern "C" int rnt_ct_tensor(rnt_buf* d0, rnt_buf* d1, rnt_buf* d2, const rnt_bu
   if (int rc = set_device(c0->ctx)) return rc;
   rnt::Launch k = launch_for(c0);
   const size_t L = k.L, n = k.t->n, wb = word_bytes(k.t);
+  const uint64_t ls = limb_stride(c0);
+  if (rnt::tensor_whole_ok(k.t)) {
+    LAUNCH(k.t, rnt::K_TENSOR_WHOLE,
+           rnt::launch_tensor_whole(k, d0->data, d1->data, d2->data, ls, c0->data, c1->data, c0p->data, c1p->data, ls),
+           "tensor whole");
+    d0->in_ntt = d1->in_ntt = 1;
+    d2->in_ntt = 0;
+    return RNT_OK;
+  }
   CallWs ws(d0);
   if (int rc = ws.get(4 * L * c0->n_polys * n * wb)) return rc;
   char* T[4];
   for (int i = 0; i < 4; ++i) T[i] = (char*)ws.p + i * L * c0->n_polys * n * wb;
-  const uint64_t ls = limb_stride(c0);
   LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, T[0], c0->data, T[1], c1->data, ls, ls), "tensor column");
   LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, T[2], c0p->data, T[3], c1p->data, ls, ls), "tensor column");
   LAUNCH(k.t, rnt::K_TENSOR_ROWS,
@@ -1898,15 +1953,18 @@ extern "C" int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
   rnt::Launch k = launch_for(c0);
   const size_t L = k.L, n = k.t->n, wb = word_bytes(k.t), B = c0->n_polys;
   const size_t bc = ks_chunk(k.t, L, B);
-  // ws: T0..T3 (column outputs, chunk-local) | D0 | D1 | D2 | key-switch (S|U0|U1)
+  // ws: [T0..T3 (column outputs, chunk-local)] | D0 | D1 | D2 | key-switch (S|U0|U1)
+  // (the whole-plane tensor reads the ciphertexts directly: no T)
+  const bool whole = rnt::tensor_whole_ok(k.t);
   const size_t chunk_words = L * bc * n;
-  const size_t need = (7 * chunk_words + (L * L + 2 * L) * bc * n) * wb;
+  const size_t nt = whole ? 0 : 4;
+  const size_t need = ((nt + 3) * chunk_words + ks_scratch_words(k.t, L, bc)) * wb;
   CallWs cws(out0);
   if (int rc = cws.get(need)) return rc;
   char* ws = (char*)cws.p;
   char* T[4];
   for (int i = 0; i < 4; ++i) T[i] = ws + i * chunk_words * wb;
-  char* D0 = ws + 4 * chunk_words * wb;
+  char* D0 = ws + nt * chunk_words * wb;
   char* D1 = D0 + chunk_words * wb;
   char* D2 = D1 + chunk_words * wb;
   char* KS = D2 + chunk_words * wb;
@@ -1917,11 +1975,19 @@ extern "C" int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
     kc.B = c;
     const uint64_t cls = (uint64_t)c * n;
     auto off = [&](const rnt_buf* b) { return (const char*)b->data + p0 * n * wb; };
+    if (whole) {
+      // d0^, d1^ NTT-resident and d2 in coefficient domain (engine.rs:486-493), one
+      // launch reading the ciphertexts in place (full limb stride) into D0..D2 (chunk's)
+      LAUNCH(kc.t, rnt::K_TENSOR_WHOLE,
+             rnt::launch_tensor_whole(kc, D0, D1, D2, cls, off(c0), off(c1), off(c0p), off(c1p), full_ls),
+             "tensor whole");
+    } else {
     LAUNCH(kc.t, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, T[0], off(c0), T[1], off(c1), full_ls, cls), "tensor column");
     LAUNCH(kc.t, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, T[2], off(c0p), T[3], off(c1p), full_ls, cls), "tensor column");
     LAUNCH(kc.t, rnt::K_TENSOR_ROWS, rnt::launch_tensor_rows(kc, D0, D1, D2, T[0], T[1], T[2], T[3], cls), "tensor rows");
     // d2 -> coefficient domain (engine.rs:493), in place in D2
     LAUNCH(kc.t, rnt::K_COL_INV, rnt::launch_col_inv(kc, D2, cls, D2, cls, 1, nullptr), "d2 inverse");
+    }
     // gadget sum with d0hat / d1hat as accumulator seeds (engine.rs:530-531)
     // d2 lives in a chunk-local buffer: present it as a full "buffer".
     rnt_buf d2view;
@@ -1956,7 +2022,7 @@ extern "C" int rnt_ct_rotate(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, co
   const bool any_ntt = c0->in_ntt || c1->in_ntt;
   const size_t tmp_words = any_ntt ? words : 0;
   CallWs ws(out0);
-  if (int rc = ws.get((2 * words + tmp_words + (L * L + 2 * L) * bc * n) * wb)) return rc;
+  if (int rc = ws.get((2 * words + tmp_words + ks_scratch_words(k.t, L, bc)) * wb)) return rc;
   char* sig0 = (char*)ws.p;
   char* sig1 = sig0 + words * wb;
   char* tmp = sig1 + words * wb;

@@ -122,7 +122,7 @@ enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
   K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FUSED, K_MF_NTT_FWD, K_MF_NTT_INV, K_WHOLE_FWD, K_WHOLE_INV, K_WHOLE_MUL,
-  K_COUNT
+  K_KS_WHOLE, K_TENSOR_WHOLE, K_COUNT
 };
 
 struct Prof {
@@ -258,9 +258,25 @@ hipError_t launch_ks_decompose(const Launch& k, void* S, const void* d, uint64_t
 hipError_t launch_ks_rows(const Launch& k, void* u0, void* u1, uint64_t u_ls, const void* S,
                           const void* key_a, const void* key_b, uint64_t key_ls,
                           const void* init0, const void* init1, uint64_t init_ls);
+// The whole-plane key-switch at 2^10 <= N <= 2^13 (k_ks_whole, one launch,
+// no S): out0 = INV(sum_i NTT(src_i mod q_j) (.) key_b[i][j] + init0) (+ add0),
+// out1 likewise with key_a; src is [k.src_limbs()][k.B][N] coefficient-domain
+// at limb stride src_ls, out0/out1/add0 at out_ls, init0/init1 (NTT domain,
+// Montgomery-scaled, may be null) at init_ls.  ks_whole_ok: it serves this basis.
+bool ks_whole_ok(const Tables* t);
+hipError_t launch_ks_whole(const Launch& k, void* out0, void* out1, uint64_t out_ls, const void* src,
+                           uint64_t src_ls, const void* key_a, const void* key_b, uint64_t key_ls,
+                           const void* init0, const void* init1, uint64_t init_ls, const void* add0);
 // Tensor rows for ct x ct: inputs are column-transformed c0,c1,c0p,c1p.
 // Writes d0hat, d1hat (NTT rows, Montgomery-scaled) and the inverse-row
 // output of d2 into d2row.  All arrays share limb stride ls.
+// The whole-plane tensor (k_tensor_rows<..., WHOLE>, 2^10 <= N <= 2^13;
+// u64 bases N <= 2^12): coefficient-domain c0, c1, c0', c1' -> NTT-domain
+// d0^, d1^ and coefficient-domain d2 in one launch.
+bool tensor_whole_ok(const Tables* t);
+hipError_t launch_tensor_whole(const Launch& k, void* d0hat, void* d1hat, void* d2, uint64_t ls,
+                               const void* c0, const void* c1, const void* c0p, const void* c1p,
+                               uint64_t in_ls);
 hipError_t launch_tensor_rows(const Launch& k, void* d0hat, void* d1hat, void* d2row,
                               const void* c0, const void* c1, const void* c0p,
                               const void* c1p, uint64_t ls);

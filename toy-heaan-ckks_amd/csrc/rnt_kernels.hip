@@ -1096,22 +1096,140 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
   }
 }
 
+// Whole-plane key-switch (2^10 <= N <= 2^13): a workgroup owns target
+// limb j of RPW polys, each plane one row (RowGeo<log N>, as k_row's WHOLE
+// form).  For every source limb i it reduces the coefficient-domain plane
+// d_i mod q_j, runs the whole forward transform and multiply-accumulates
+// with the NTT-resident keys (each thread's 16 consecutive words of both,
+// straight from memory: at one poly per row no key row is shared), then
+// runs the whole inverse of both accumulators with the folded n^-1 2^w of
+// the Montgomery sums and stores the coefficient-domain result (+ the
+// addend on the first).  No S intermediate and no column launches: per poly
+// and target limb the source planes and the key planes in, two planes out,
+// in one launch (the four-step path writes and reads S, L planes per target
+// limb, and runs three more launches).
+template <class W, int LOG_N>
+__global__ void __launch_bounds__(RowGeo<LOG_N>::THREADS, sizeof(W) == 4 ? kKsMinWaves : 1)
+k_ks_whole(W* __restrict__ out0, W* __restrict__ out1, uint64_t out_ls, const W* __restrict__ src,
+           uint64_t src_ls, const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
+           const W* __restrict__ init0, const W* __restrict__ init1, uint64_t init_ls,
+           const W* __restrict__ add0, TabPtrs<W> tp, uint32_t L, uint32_t B) {
+  using G = RowGeo<LOG_N>;
+  constexpr int E = G::E;
+  static_assert(G::BBL == 0 && E == 16, "last pass: 16 consecutive words a thread");
+  constexpr uint64_t N = 1ull << LOG_N;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  W* lds = (W*)smem_raw;
+  XPos xp;
+  xp.slot = G::slot_of(threadIdx.x);
+  xp.tau = G::tau_of(threadIdx.x);
+  xp.heap = 1u << LOG_N;
+  const uint32_t j = blockIdx.y;
+  const uint32_t pp = blockIdx.x * G::RPW + xp.slot;
+  const bool active = pp < B;
+  const uint32_t p = active ? pp : B - 1;  // inactive slots read a valid plane, store nothing
+  const LimbConst<W> lc = tp.lc[j];
+  const Tw<W>* tw = tp.tw + (uint64_t)j * N;
+  const Tw<W>* itw = tp.itw + (uint64_t)j * N;
+  const uint32_t b0 = G::base(xp.tau, G::BB0);
+  const uint32_t bl = G::base(xp.tau, G::BBL);
+  constexpr bool kLazy = sizeof(W) == 4;
+  W nqinv = (W)0 - lc.qinv;
+  asm volatile("" : "+s"(nqinv));
+  const W q2 = lc.q + lc.q;
+  W acc[2][E];
+  const uint64_t ibase = (uint64_t)j * init_ls + (uint64_t)p * N + bl;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    acc[0][e] = init0 ? init0[ibase + e] : (W)0;
+    acc[1][e] = init1 ? init1[ibase + e] : (W)0;
+  }
+  auto ld16 = [](W (&o)[E], const W* q) {
+    constexpr int V = 16 / (int)sizeof(W);
+#pragma unroll
+    for (int e0 = 0; e0 < E; e0 += V) {
+      const uint4 v = *(const uint4*)(q + e0);
+      if constexpr (sizeof(W) == 4) {
+        o[e0] = v.x; o[e0 + 1] = v.y; o[e0 + 2] = v.z; o[e0 + 3] = v.w;
+      } else {
+        o[e0] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+        o[e0 + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+      }
+    }
+  };
+  auto mac = [&](W (&a)[E], const W (&x)[E], const W (&k)[E]) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if constexpr (kLazy)
+        a[e] = mac_lazy(a[e], x[e], k[e], lc.q, q2, nqinv);
+      else
+        a[e] = add_mod<W>(a[e], mont_mul<W>(x[e], k[e], lc.q, lc.qinv), lc.q);
+    }
+  };
+#pragma unroll 1
+  for (uint32_t i = 0; i < L; ++i) {
+    const W* kb = key_b + (uint64_t)j * key_ls + (uint64_t)i * N + bl;
+    const W* ka = key_a + (uint64_t)j * key_ls + (uint64_t)i * N + bl;
+    W x[1][E];
+    const W* sp = src + (uint64_t)i * src_ls + (uint64_t)p * N + b0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[0][e] = shoup_mul<W>(sp[(uint32_t)e << G::BB0], (W)1, lc.one_p, lc.q);  // d_i mod q_j
+    xf_fwd<G, W, 1>(x, xp, lds, tw, mod_of(lc));
+    W kv[E];
+    ld16(kv, kb);
+    mac(acc[0], x[0], kv);
+    ld16(kv, ka);
+    mac(acc[1], x[0], kv);
+  }
+  // the thread coordinates pass through an opaque copy, so the inverse's
+  // addresses are derived here rather than held (spilled) across the loop
+  XPos xq = xp;
+  uint32_t pq = p;
+  asm volatile("" : "+v"(xq.tau), "+v"(pq));
+  const uint64_t obase = (uint64_t)j * out_ls + (uint64_t)pq * N + G::base(xq.tau, G::BB0);
+  // the two accumulators' inverses one after the other (written out twice:
+  // a loop over them is not unrolled, and acc would be indexed at run time)
+  auto finish = [&](W (&a)[E], W* dst, const W* add) {
+    W v[1][E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) v[0][e] = kLazy ? csub<W>(a[e], lc.q) : a[e];
+    xf_inv<G, W, 1, true>(v, xq, lds, itw, mod_of(lc), Fold<W>{lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p});
+    if (active) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const uint64_t pos = obase + ((uint32_t)e << G::BB0);
+        dst[pos] = add ? add_mod<W>(v[0][e], add[pos], lc.q) : v[0][e];
+      }
+    }
+  };
+  finish(acc[0], out0, add0);
+  finish(acc[1], out1, nullptr);
+}
+
 // 4 waves per SIMD (<= 128 VGPRs; unconstrained it takes 134-154 and runs
 // at 3): tensor_rows 1.74 -> 1.64 ms per 64 cts (profiles/r02_ab_tensor_waves.txt)
 constexpr int kTensorMinWaves = 4;
-template <class W, int LOG_C>
+// WHOLE (2^10 <= N = 2^LOG_C <= 2^13): a row is the whole plane, as in k_row's
+// WHOLE form, so the four operands come in coefficient domain, d0^ and d1^
+// go out NTT-resident and d2 in coefficient domain (its inverse's top stage
+// applies the folded n^-1 2^32 of the Montgomery product): the tensor step
+// of a ct-mul is this one launch, 4 planes in and 3 out, without the two
+// column launches before it and d2's column inverse after it.
+template <class W, int LOG_C, bool WHOLE = false>
 __global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kTensorMinWaves : 1)
 k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2row,
               const W* __restrict__ c0, const W* __restrict__ c1, const W* __restrict__ c0p,
               const W* __restrict__ c1p, TabPtrs<W> tp, uint32_t log_n, uint32_t B, uint64_t ls,
-              uint64_t rows_total) {
+              uint64_t rows_total, uint64_t in_ls) {
   using G = RowGeo<LOG_C>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   W* lds = (W*)smem_raw;
   const RowPos rp = row_pos_pfast<G>(log_n, B, rows_total);  // shared twiddles, as in k_row
   const uint64_t N = 1ull << log_n;
-  const uint64_t base = (uint64_t)rp.l * ls + (uint64_t)rp.p * N + (uint64_t)rp.r * G::C;
+  const uint64_t pr = (uint64_t)rp.p * N + (uint64_t)rp.r * G::C;
+  const uint64_t base = (uint64_t)rp.l * ls + pr;      // outputs
+  const uint64_t ibase = (uint64_t)rp.l * in_ls + pr;  // operands
   const LimbConst<W> lc = tp.lc[rp.l];
   const Tw<W>* tw = tp.tw + (uint64_t)rp.l * N;
   const Tw<W>* itw = tp.itw + (uint64_t)rp.l * N;
@@ -1121,15 +1239,15 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const uint32_t e = b0 + ((uint32_t)i << G::BB0);
-    a[0][i] = c0[base + e];
-    a[1][i] = c1[base + e];
+    a[0][i] = c0[ibase + e];
+    a[1][i] = c1[ibase + e];
   }
   xf_fwd<G, W, 2>(a, rp.xp, lds, tw, mod_of(lc));
 #pragma unroll
   for (int i = 0; i < E; ++i) {
     const uint32_t e = b0 + ((uint32_t)i << G::BB0);
-    b[0][i] = c0p[base + e];
-    b[1][i] = c1p[base + e];
+    b[0][i] = c0p[ibase + e];
+    b[1][i] = c1p[ibase + e];
   }
   xf_fwd<G, W, 2>(b, rp.xp, lds, tw, mod_of(lc));
   W d2[1][E];
@@ -1158,7 +1276,8 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
       d1hat[base + pos] = d1;
     }
   }
-  xf_inv<G, W, 1>(d2, rp.xp, lds, itw, mod_of(lc));
+  xf_inv<G, W, 1, WHOLE>(d2, rp.xp, lds, itw, mod_of(lc),
+                         WHOLE ? Fold<W>{lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p} : Fold<W>{});
   if (rp.active) {
 #pragma unroll
     for (int i = 0; i < E; ++i) d2row[base + b0 + ((uint32_t)i << G::BB0)] = d2[0][i];
@@ -1547,8 +1666,7 @@ static hipError_t whole_t(const Launch& k, int mode, void* out, void* x, const v
     RNT_W(11)
     RNT_W(12)
     RNT_W(13)
-    RNT_W(14)
-    default: return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;  // ks_whole_ok
   }
 #undef RNT_W
 }
@@ -1872,22 +1990,22 @@ static hipError_t ks_rows_t(const Launch& k, void* u0, void* u1, uint64_t ls, co
   return hipErrorInvalidValue;
 }
 
-template <class W, int LOG_C>
+template <class W, int LOG_C, bool WHOLE = false>
 static hipError_t tensor_rows_launch(const Launch& k, void* d0hat, void* d1hat, void* d2row,
                                      const void* c0, const void* c1, const void* c0p,
-                                     const void* c1p, uint64_t ls) {
+                                     const void* c1p, uint64_t ls, uint64_t in_ls) {
   using G = RowGeo<LOG_C>;
   const Geom g = geom_for(k.t->log_n);
-  const uint64_t rows = (uint64_t)k.L * k.B * g.r;
+  const uint64_t rows = (uint64_t)k.L * k.B * (WHOLE ? 1 : g.r);
   if (rows == 0) return hipSuccess;
   const unsigned blocks = (unsigned)((rows + G::RPW - 1) / G::RPW);
   const size_t lds = row_lds<W, LOG_C>(2);
-  hipError_t e = allow_lds(k_tensor_rows<W, LOG_C>, lds);
+  hipError_t e = allow_lds(k_tensor_rows<W, LOG_C, WHOLE>, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_tensor_rows<W, LOG_C>), dim3(blocks), dim3(G::THREADS), lds, k.s,
+  hipLaunchKernelGGL((k_tensor_rows<W, LOG_C, WHOLE>), dim3(blocks), dim3(G::THREADS), lds, k.s,
                      (W*)d0hat, (W*)d1hat, (W*)d2row, (const W*)c0, (const W*)c1,
-                     (const W*)c0p, (const W*)c1p, tab_ptrs<W>(k.t), g.log_n, (uint32_t)k.B, ls,
-                     rows);
+                     (const W*)c0p, (const W*)c1p, tab_ptrs<W>(k.t),
+                     WHOLE ? (uint32_t)LOG_C : g.log_n, (uint32_t)k.B, ls, rows, in_ls);
   return hipGetLastError();
 }
 
@@ -1896,7 +2014,7 @@ static hipError_t tensor_rows_t(const Launch& k, void* d0hat, void* d1hat, void*
                                 const void* c0, const void* c1, const void* c0p,
                                 const void* c1p, uint64_t ls) {
   const Geom g = geom_for(k.t->log_n);
-#define RNT_L(C) return tensor_rows_launch<W, C>(k, d0hat, d1hat, d2row, c0, c1, c0p, c1p, ls)
+#define RNT_L(C) return tensor_rows_launch<W, C>(k, d0hat, d1hat, d2row, c0, c1, c0p, c1p, ls, ls)
   RNT_DISPATCH_LOGC(g.log_c, RNT_L)
 #undef RNT_L
   return hipErrorInvalidValue;
@@ -2115,6 +2233,74 @@ hipError_t launch_ks_rows(const Launch& k, void* u0, void* u1, uint64_t u_ls, co
                           const void* init0, const void* init1, uint64_t init_ls) {
   RNT_WIDE(ks_rows_t<uint32_t>(k, u0, u1, u_ls, S, key_a, key_b, key_ls, init0, init1, init_ls),
            ks_rows_t<uint64_t>(k, u0, u1, u_ls, S, key_a, key_b, key_ls, init0, init1, init_ls));
+}
+template <class W>
+static hipError_t ks_whole_t(const Launch& k, void* out0, void* out1, uint64_t out_ls, const void* src,
+                             uint64_t src_ls, const void* key_a, const void* key_b, uint64_t key_ls,
+                             const void* init0, const void* init1, uint64_t init_ls, const void* add0) {
+  if (k.L == 0 || k.B == 0) return hipSuccess;
+  if (k.L > 65535) return hipErrorInvalidConfiguration;
+#define RNT_W(C)                                                                                        \
+  case C: {                                                                                             \
+    using G = RowGeo<C>;                                                                                \
+    const size_t lds = row_lds<W, C>(1);                                                                \
+    hipError_t e = allow_lds(k_ks_whole<W, C>, lds);                                                    \
+    if (e != hipSuccess) return e;                                                                      \
+    const dim3 grid((unsigned)((k.B + G::RPW - 1) / G::RPW), (unsigned)k.L);                           \
+    hipLaunchKernelGGL((k_ks_whole<W, C>), grid, dim3(G::THREADS), lds, k.s, (W*)out0, (W*)out1, out_ls,   \
+                       (const W*)src, src_ls, (const W*)key_a, (const W*)key_b, key_ls, (const W*)init0,  \
+                       (const W*)init1, init_ls, (const W*)add0, tab_ptrs<W>(k.t), (uint32_t)k.src_limbs(), \
+                       (uint32_t)k.B);                                                                  \
+    return hipGetLastError();                                                                           \
+  }
+  switch (k.t->log_n) {
+    RNT_W(10)
+    RNT_W(11)
+    RNT_W(12)
+    RNT_W(13)
+    default: return hipErrorInvalidValue;  // ks_whole_ok
+  }
+#undef RNT_W
+}
+// u32 bases only: the u64 form needs 256 VGPRs (one wave per SIMD).
+// N <= 2^13: at 2^14 (one 1024-thread workgroup per plane, one per CU)
+// the whole-plane tensor and key-switch measured slower than the four-step
+// kernels at every batch but 32 (ct-mul 2^14 x 8: 97.1k vs 99.1k/s at 1024
+// cts, 3.3k vs 4.5k/s at one), faster at every batch at 2^10..2^13
+// (profiles/r04/ab_ks_whole.txt)
+constexpr uint32_t kKsWholeMaxLogN = 13;
+bool ks_whole_ok(const Tables* t) {
+  return t->plane != 0 && !t->wide && t->log_n >= 10 && t->log_n <= kKsWholeMaxLogN;
+}
+hipError_t launch_ks_whole(const Launch& k, void* out0, void* out1, uint64_t out_ls, const void* src,
+                           uint64_t src_ls, const void* key_a, const void* key_b, uint64_t key_ls,
+                           const void* init0, const void* init1, uint64_t init_ls, const void* add0) {
+  if (k.t->wide) return hipErrorInvalidValue;  // ks_whole_ok
+  return ks_whole_t<uint32_t>(k, out0, out1, out_ls, src, src_ls, key_a, key_b, key_ls, init0, init1, init_ls, add0);
+}
+template <class W>
+static hipError_t tensor_whole_t(const Launch& k, void* d0hat, void* d1hat, void* d2, uint64_t ls,
+                                 const void* c0, const void* c1, const void* c0p, const void* c1p,
+                                 uint64_t in_ls) {
+#define RNT_W(C)                                                                                     \
+  case C:                                                                                            \
+    if constexpr (sizeof(W) == 8 && C > 12) return hipErrorInvalidValue; /* tensor_whole_ok */      \
+    else return tensor_rows_launch<W, C, true>(k, d0hat, d1hat, d2, c0, c1, c0p, c1p, ls, in_ls);
+  switch (k.t->log_n) {
+    RNT_W(10)
+    RNT_W(11)
+    RNT_W(12)
+    RNT_W(13)
+  }
+#undef RNT_W
+  return hipErrorInvalidValue;  // tensor_whole_ok
+}
+bool tensor_whole_ok(const Tables* t) { return whole_ok(t, 2) && t->log_n <= kKsWholeMaxLogN; }
+hipError_t launch_tensor_whole(const Launch& k, void* d0hat, void* d1hat, void* d2, uint64_t ls,
+                               const void* c0, const void* c1, const void* c0p, const void* c1p,
+                               uint64_t in_ls) {
+  RNT_WIDE(tensor_whole_t<uint32_t>(k, d0hat, d1hat, d2, ls, c0, c1, c0p, c1p, in_ls),
+           tensor_whole_t<uint64_t>(k, d0hat, d1hat, d2, ls, c0, c1, c0p, c1p, in_ls));
 }
 hipError_t launch_tensor_rows(const Launch& k, void* d0hat, void* d1hat, void* d2row,
                               const void* c0, const void* c1, const void* c0p, const void* c1p,
