@@ -111,8 +111,8 @@ hipEvent_t prof_event(rnt::Prof* p) {
 // Bracket one launch with events when profiling is on.
 // A launcher reports hipGetLastError() after its launch, so an error an
 // earlier unchecked call left in the thread's last-error slot (a cleanup
-// path's hipFree / hipEventDestroy) would be blamed on it: the slot is read
-// and cleared first (RNT_TRACE_STALE=1 names what it held).
+// path's (void)hipFree / hipEventDestroy) would be blamed on it: the slot
+// is read and cleared first (RNT_TRACE_STALE=1 names what it held).
 inline void clear_stale_error(int id) {
   const hipError_t pre = hipGetLastError();
   static const bool trace = [] {
@@ -1215,13 +1215,15 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
     out->in_ntt = 0;
     return RNT_OK;
   }
-  if (int rc = ensure_ws(out, poly_words(out) * word_bytes(k.t))) return rc;
   if (rnt::plane_ok(k.t)) {
+    const uint64_t planes = rnt::plane_scratch_planes((uint64_t)k.B * k.L);
+    if (int rc = ensure_ws(out, planes * k.t->n * 4)) return rc;
     LAUNCH(k.t, rnt::K_PLANE_FUSED, rnt::launch_plane_fused(k, out->data, a->data, b->data, out->ws, ls),
            "plane fused product");
     out->in_ntt = 0;
     return RNT_OK;
   }
+  if (int rc = ensure_ws(out, poly_words(out) * word_bytes(k.t))) return rc;
   // lazy: the Harvey 30-bit variant when every q < 2^30 (Tables::lazy30)
   LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, out->data, a->data, out->ws, b->data, ls, ls, true),
          "column forward");

@@ -203,6 +203,8 @@ hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_
 // one word per output word, a^ in a private layout).
 bool plane_ok(const Tables* t);
 hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls);
+// scratch planes (of N words) launch_plane_fused needs for B L pairs
+uint64_t plane_scratch_planes(uint64_t planes);
 // The standalone transforms at the same size (rnt_mfma.hip): radix-16 passes
 // as i8 matrix products, in place.  mf_supported: u32 bases at N = 2^16;
 // mf_build: the per-limb tables into t->mf (0 ok, else err).

@@ -1666,7 +1666,8 @@ static hipError_t whole_t(const Launch& k, int mode, void* out, void* x, const v
     RNT_W(11)
     RNT_W(12)
     RNT_W(13)
-    default: return hipErrorInvalidValue;  // ks_whole_ok
+    RNT_W(14)
+    default: return hipErrorInvalidValue;
   }
 #undef RNT_W
 }

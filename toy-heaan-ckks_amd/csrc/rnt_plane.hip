@@ -643,11 +643,40 @@ k_plane_fused(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, ui
   plane_fused_one(c, a, b, ah, tp, ls, poly, l, (uint32_t*)smem_raw, threadIdx.x, poly + l * gridDim.x);
 }
 
+// The same product with the a^ scratch indexed by the CU the workgroup runs
+// on instead of by its plane.  A workgroup takes the whole LDS (160 KiB), so
+// a CU runs one at a time and no two resident workgroups share a slot; the
+// slot's lines are rewritten by every plane the CU takes (256 slots in use,
+// 64 MiB, instead of B L planes of scratch) and can stay in the Infinity
+// Cache instead of being written back to HBM.  Slot = XCC_ID (4 bits) and
+// HW_ID bits 15..8 (SE, SH, CU), kPlaneSlots in all; the caller's scratch
+// holds at least that many planes (plane_scratch_planes).  sls is 0: the
+// select keeps k_plane_fused's address form (its SGPR allocation).
+// Same-box A/B at the metric: 140.1k against 138.6k poly-muls/s, every word
+// of the 1024 x 16 output equal (profiles/r04/ab_plane_slots.txt).
+constexpr uint32_t kPlaneSlots = 1u << 11;
+static_assert(plane::LDS_WORDS * 4 > 80 * 1024, "one workgroup per CU");
+__global__ void __launch_bounds__(plane::T, 1)
+k_plane_fused_slots(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
+                    TabPtrs<uint32_t> tp, uint64_t ls, uint64_t sls) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const uint32_t poly = blockIdx.x, l = blockIdx.y;
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;   // hwreg(HW_REG_XCC_ID)
+  const uint32_t cu = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8) & 0xffu;  // hwreg(HW_REG_HW_ID)[15:8]
+  uint32_t* ah = scratch + (sls ? 0 : ((uint64_t)((xcc << 8) | cu) << 16));
+  plane_fused_one(c, a, b, ah, tp, ls, poly, l, (uint32_t*)smem_raw, threadIdx.x, poly + l * gridDim.x);
+}
+
 #ifdef RNT_PLANE_TRACE
 extern "C" __attribute__((visibility("default"))) int rnt_debug_plane_trace(uint64_t* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_plane_trace), sizeof(g_plane_trace));
 }
 #endif
+
+// Planes of a^ scratch a launch over `planes` (poly, limb) pairs needs: one
+// per pair, or one per CU slot from kPlaneSlots pairs on (512 MiB at most,
+// against 4 GiB of per-pair scratch at the metric's 1024 x 16).
+uint64_t plane_scratch_planes(uint64_t planes) { return planes < kPlaneSlots ? planes : kPlaneSlots; }
 
 // The whole-plane product serves rnt_mul for u32 bases at N = 2^16 unless
 // RNT_PLANE=0 (Tables::plane): its canonical arithmetic holds for any q <
@@ -661,6 +690,14 @@ hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const v
   if (k.B == 0 || k.L == 0) return hipSuccess;
   if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
   const size_t lds = (size_t)plane::LDS_WORDS * 4;
+  if (k.B * k.L >= kPlaneSlots) {  // plane_scratch_planes: the scratch holds every slot
+    hipError_t e = allow_lds(k_plane_fused_slots, lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_plane_fused_slots, dim3((unsigned)k.B, (unsigned)k.L), dim3(plane::T), lds, k.s,
+                       (uint32_t*)out, (const uint32_t*)a, (const uint32_t*)b, (uint32_t*)scratch,
+                       tab_ptrs<uint32_t>(k.t), ls, (uint64_t)0);
+    return hipGetLastError();
+  }
   hipError_t e = allow_lds(k_plane_fused, lds);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_plane_fused, dim3((unsigned)k.B, (unsigned)k.L), dim3(plane::T), lds, k.s, (uint32_t*)out,
