@@ -570,7 +570,7 @@ def run_ctmul_graph(args, comm, world, rank, local_rank):
     g, elapsed, kms, kernels = _graph_step_timing(
         Bs, step, args.steps, args.warmup, comm,
         ("col_fwd", "tensor_rows", "col_inv", "ks_decompose", "ks_rows", "rescale", "elementwise", "tensor_whole",
-         "ks_whole"))
+         "ks_whole", "mf_tensor"))
     ms_per_step = elapsed / args.steps * 1e3
     value = B * args.steps * world / elapsed
     parity_ok = None
@@ -693,7 +693,7 @@ def run_ctmul(args, comm, world, rank, local_rank):
     value = B_global * args.steps / elapsed
     kernels = {}
     for k in ("col_fwd", "tensor_rows", "col_inv", "ks_decompose", "ks_rows", "rescale", "elementwise",
-              "tensor_whole", "ks_whole"):
+              "tensor_whole", "ks_whole", "mf_tensor"):
         cnt, ms = prof_basis.profile_read(k)
         if cnt:
             kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}

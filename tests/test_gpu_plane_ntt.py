@@ -127,3 +127,55 @@ def test_cross_path_forward_inverse(ring, monkeypatch):
         u = rn.RnsPoly.from_channels(nt, dst, in_ntt_domain=True)
         u.to_coeff_domain()
         assert np.array_equal(u.channels(), a_h)
+
+
+def test_mf_tensor_matches_four_step_and_oracle(ring, monkeypatch):
+    """The matrix-core tensor (k_mf_tensor, engine.rs:480-493) at the
+    metric's ring: d2 = c1 c1' (coefficient domain) against the oracle for
+    every poly of the batch, and the NTT-resident key-switch seeds d0^, d1^
+    word for word equal to the four-step tensor's (RNT_PLANE=0), including an
+    all-(q-1) ciphertext."""
+    rn, mod, Bo, a_h, b_h, x_h, y_h, _ = ring
+    q = np.array(mod, dtype=np.uint64)[:, None]
+    c = [a_h.copy(), b_h.copy(), x_h.copy(), y_h.copy()]
+    c[1][B - 1] = np.broadcast_to(q - 1, (L, N))
+    c[3][B - 1] = np.broadcast_to(q - 1, (L, N))
+    outs = {}
+    for plane in (None, "0"):
+        Bd = _basis(rn, mod, monkeypatch, plane)
+        d = rn.ct_tensor(*(rn.RnsPoly.from_channels(x, Bd) for x in c))
+        outs[plane] = [x.channels() for x in d]
+    for p in range(B):
+        assert np.array_equal(outs[None][2][p], orc.mul(Bo, c[1][p], c[3][p])), p
+    for i in range(3):
+        assert np.array_equal(outs[None][i], outs["0"][i]), i
+
+
+def _seeds_want(Bo, mod, c0, c1, c0p, c1p):
+    """Oracle d0^, d1^ (NTT domain, times 2^-32 as the device's seeds) and d2."""
+    q = np.array(mod, dtype=object)[:, None]
+    rinv = np.array([pow(2, -32, int(x)) for x in mod], dtype=object)[:, None]
+    d0 = orc.to_ntt(Bo, orc.mul(Bo, c0, c0p))
+    d1 = orc.to_ntt(Bo, orc.add(Bo, orc.mul(Bo, c0, c1p), orc.mul(Bo, c1, c0p)))
+    scale = lambda x: ((x.astype(object) * rinv) % q).astype(np.uint64)  # noqa: E731
+    return scale(d0), scale(d1), orc.mul(Bo, c1, c1p)
+
+
+def test_mf_tensor_slot_scratch_batch(ring, monkeypatch):
+    """128 ciphertexts x 16 limbs = 2048 (poly, limb) pairs: the tensor's c1^
+    temporary goes to the CU-indexed scratch slots (kPlaneSlots).  Sampled
+    ciphertexts' d0^, d1^ (Montgomery-scaled NTT-domain seeds) and d2 against
+    the oracle, on both paths."""
+    rn, mod, Bo, *_ = ring
+    Bc = 128
+    picks = (0, 1, 63, 64, 127)
+    for plane in (None, "0"):
+        Bd = _basis(rn, mod, monkeypatch, plane)
+        drng = rn.DeviceRng(128)
+        c = [rn.RnsPoly.sample_uniform(Bd, drng, Bc) for _ in range(4)]
+        d = rn.ct_tensor(*c)
+        for p in picks:
+            ch = [x.channels_of(p)[0] for x in c]
+            want = _seeds_want(Bo, mod, *ch)
+            for i in range(3):
+                assert np.array_equal(d[i].channels_of(p)[0], want[i]), (plane, i, p)

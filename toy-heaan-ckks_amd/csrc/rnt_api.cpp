@@ -95,7 +95,7 @@ thread_local Capture* g_capture = nullptr;
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
-    "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd", "whole_inv", "whole_mul", "ks_whole", "tensor_whole"};
+    "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd", "whole_inv", "whole_mul", "ks_whole", "tensor_whole", "mf_tensor"};
 
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
@@ -1926,6 +1926,16 @@ extern "C" int rnt_ct_tensor(rnt_buf* d0, rnt_buf* d1, rnt_buf* d2, const rnt_bu
     return RNT_OK;
   }
   CallWs ws(d0);
+  if (use_mf(k)) {  // N = 2^16, u32: the matrix-core tensor, one launch
+    if (int rc = ws.get(rnt::plane_scratch_planes((uint64_t)L * c0->n_polys) * n * wb)) return rc;
+    LAUNCH(k.t, rnt::K_MF_TENSOR,
+           rnt::launch_mf_tensor(k, d0->data, d1->data, d2->data, ls, c0->data, c1->data, c0p->data, c1p->data,
+                                 ls, ws.p),
+           "MFMA tensor");
+    d0->in_ntt = d1->in_ntt = 1;
+    d2->in_ntt = 0;
+    return RNT_OK;
+  }
   if (int rc = ws.get(4 * L * c0->n_polys * n * wb)) return rc;
   char* T[4];
   for (int i = 0; i < 4; ++i) T[i] = (char*)ws.p + i * L * c0->n_polys * n * wb;
@@ -1958,8 +1968,10 @@ extern "C" int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
   // ws: [T0..T3 (column outputs, chunk-local)] | D0 | D1 | D2 | key-switch (S|U0|U1)
   // (the whole-plane tensor reads the ciphertexts directly: no T)
   const bool whole = rnt::tensor_whole_ok(k.t);
+  const bool mf = !whole && use_mf(k);
   const size_t chunk_words = L * bc * n;
-  const size_t nt = whole ? 0 : 4;
+  // (the matrix-core tensor's scratch: plane_scratch_planes(L bc) <= L bc planes)
+  const size_t nt = whole ? 0 : mf ? 1 : 4;
   const size_t need = ((nt + 3) * chunk_words + ks_scratch_words(k.t, L, bc)) * wb;
   CallWs cws(out0);
   if (int rc = cws.get(need)) return rc;
@@ -1983,6 +1995,11 @@ extern "C" int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
       LAUNCH(kc.t, rnt::K_TENSOR_WHOLE,
              rnt::launch_tensor_whole(kc, D0, D1, D2, cls, off(c0), off(c1), off(c0p), off(c1p), full_ls),
              "tensor whole");
+    } else if (mf) {
+      // the same on the matrix-core transforms (N = 2^16), T0.. as its scratch
+      LAUNCH(kc.t, rnt::K_MF_TENSOR,
+             rnt::launch_mf_tensor(kc, D0, D1, D2, cls, off(c0), off(c1), off(c0p), off(c1p), full_ls, T[0]),
+             "MFMA tensor");
     } else {
     LAUNCH(kc.t, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, T[0], off(c0), T[1], off(c1), full_ls, cls), "tensor column");
     LAUNCH(kc.t, rnt::K_COL_FWD, rnt::launch_col_fwd(kc, T[2], off(c0p), T[3], off(c1p), full_ls, cls), "tensor column");

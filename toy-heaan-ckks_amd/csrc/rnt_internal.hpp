@@ -122,7 +122,7 @@ enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
   K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FUSED, K_MF_NTT_FWD, K_MF_NTT_INV, K_WHOLE_FWD, K_WHOLE_INV, K_WHOLE_MUL,
-  K_KS_WHOLE, K_TENSOR_WHOLE, K_COUNT
+  K_KS_WHOLE, K_TENSOR_WHOLE, K_MF_TENSOR, K_COUNT
 };
 
 struct Prof {
@@ -203,6 +203,10 @@ hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_
 // one word per output word, a^ in a private layout).
 bool plane_ok(const Tables* t);
 hipError_t launch_plane_fused(const Launch& k, void* out, const void* a, const void* b, void* scratch, uint64_t ls);
+// Scratch slots indexed by the CU a 160-KiB-LDS workgroup runs on (XCC_ID
+// and HW_ID bits 15..8): k_plane_fused_slots, k_mf_tensor from this many
+// (poly, limb) pairs on.
+constexpr uint32_t kPlaneSlots = 1u << 11;
 // scratch planes (of N words) launch_plane_fused needs for B L pairs
 uint64_t plane_scratch_planes(uint64_t planes);
 // The standalone transforms at the same size (rnt_mfma.hip): radix-16 passes
@@ -211,6 +215,13 @@ uint64_t plane_scratch_planes(uint64_t planes);
 inline bool mf_supported(const Tables* t) { return t->plane != 0 && !t->wide && t->log_n == 16; }
 int mf_build(Tables* t, std::string* err);
 hipError_t launch_mf_ntt(const Launch& k, int inverse, void* data, uint64_t ls);
+// The ciphertext tensor product at N = 2^16 on the matrix-core transforms
+// (k_mf_tensor, mf_supported bases): coefficient-domain c0, c1, c0', c1' at
+// limb stride ils -> NTT-domain d0^, d1^ (Montgomery-scaled key-switch seeds)
+// and coefficient-domain d2 at limb stride ols; scratch: plane_scratch_planes(B L)
+// planes of N words.
+hipError_t launch_mf_tensor(const Launch& k, void* d0, void* d1, void* d2, uint64_t ols, const void* c0,
+                            const void* c1, const void* c0p, const void* c1p, uint64_t ils, void* scratch);
 // Whether rnt_mul's row kernel stops its transforms two stages early and
 // multiplies degree-3 residues (u32 canonical bases, row length 2^(4k));
 // its inverse column pass then takes rfold = 2.

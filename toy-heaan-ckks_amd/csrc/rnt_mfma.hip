@@ -178,11 +178,25 @@ __device__ __forceinline__ uint32_t canon(int32_t r, int32_t q) { return (uint32
 
 // One MFMA tile: the four digit planes of a 16 x 16 x 64 product.
 // DA: the data is the A operand (the matrix the B operand).
-template <bool DA>
+template <bool DA, bool W16 = false>
 __device__ __forceinline__ void tile(v4i (&D)[4], const v4i (&M)[4], v4i dat, v4i c0) {
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int a = 0; a < 4; ++a) D[a] = DA ? mfma(dat, M[a], a == 0 ? c0 : z) : mfma(M[a], dat, a == 0 ? c0 : z);
+  // W16: 16 more wait states than the compiler counts before anything
+  // touches the tile's registers.  k_mf_tensor needs them: without, the
+  // first result register of lanes 12..15 of a pass's last tile came out
+  // wrong now and then (16-300 words per 2^26 on the full-output stress,
+  // tools/tensor_stress2.py), where its register allocation lets an MFMA's
+  // destination partly overlap its B operand and the next VALU write lands
+  // on that operand after the compiler's 6 wait states.  The standalone
+  // transforms measured clean without them (tools/ntt_stress.py, 12288
+  // planes) and keep their speed.
+  if constexpr (W16) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7");
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
 // the table of one limb; lo = lam * 16 (the lane's 16 bytes of an operand row)
 __device__ __forceinline__ void load_mat(v4i (&M)[4], Rsrc tab, uint32_t slot, uint32_t lo) {
@@ -360,7 +374,7 @@ __device__ __forceinline__ void swap_q3p2(uint32_t (&x)[64]) {
 // ---- the passes -------------------------------------------------------------
 // pass 0 on P1 chunks [C0, C0 + 8): input canonical (BIAS: packed with the
 // -2^30 shift its compensation undoes) or packed; output packed.
-template <int C0, bool BIAS>
+template <int C0, bool BIAS, bool W16>
 __device__ __forceinline__ void pass_p1(uint32_t (&x1)[64], const v4i (&M)[4], v4i comp, const Mc& m) {
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
@@ -369,7 +383,7 @@ __device__ __forceinline__ void pass_p1(uint32_t (&x1)[64], const v4i (&M)[4], v
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)(BIAS ? pk_canon(x1[4 * c + i]) : x1[4 * c + i]);
     v4i D[4];
-    tile<false>(D, M, b, BIAS ? comp : z);
+    tile<false, W16>(D, M, b, BIAS ? comp : z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) x1[4 * c + i] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
     pin4(x1[4 * c + 0], x1[4 * c + 1], x1[4 * c + 2], x1[4 * c + 3]);
@@ -378,7 +392,7 @@ __device__ __forceinline__ void pass_p1(uint32_t (&x1)[64], const v4i (&M)[4], v
 }
 // pass 1 (per-wave matrix) on P2 chunks [C0, C0 + 8), then the pass-2 twist
 // (TW: the table in P2 positions).
-template <int C0>
+template <int C0, bool W16>
 __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
                                         const Mc& m) {
   const v4i z = {0, 0, 0, 0};
@@ -391,7 +405,7 @@ __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], R
     // tile-ahead prefetch measured 4 more spilled registers)
     const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 16u);
     v4i D[4];
-    tile<false>(D, M, b, z);
+    tile<false, W16>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -402,6 +416,7 @@ __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], R
   }
 }
 // pass 2 (F, data as A: P3 -> P4 positions), then the pass-3 twist.
+template <bool W16>
 __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
                                         const Mc& m) {
   const v4i z = {0, 0, 0, 0};
@@ -412,7 +427,7 @@ __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rs
     for (int i = 0; i < 4; ++i) a[i] = (int)x[p3(c, i)];
     const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 1024u);
     v4i D[4];
-    tile<true>(D, M, a, z);
+    tile<true, W16>(D, M, a, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -425,7 +440,7 @@ __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rs
 // pass 3 (F, P4 in place): each tile's centred outputs go to EPI(c, r, x)
 // at once (stored, or multiplied into the product), so no 64-bit reduction
 // result stays live beyond its tile.
-template <class EPI>
+template <bool W16, class EPI>
 __device__ __forceinline__ void pass_p4(uint32_t (&x)[64], const v4i (&M)[4], const Mc& m, const EPI& epi) {
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
@@ -434,7 +449,7 @@ __device__ __forceinline__ void pass_p4(uint32_t (&x)[64], const v4i (&M)[4], co
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x[p3(c, i)];
     v4i D[4];
-    tile<false>(D, M, b, z);
+    tile<false, W16>(D, M, b, z);
     int32_t r[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -462,6 +477,7 @@ __device__ __forceinline__ v4i stash_get(uint32_t addr, int c) {
 // inverse pass 3 (F^-1, data as A: P4 -> Q3) on the canonical words as
 // loaded (biased here, comp undoes it), then its twist; packed output.
 // tv: tile 0's twists (each tile loads the next one's).
+template <bool W16>
 __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v4i comp, v4i tv, Rsrc tab,
                                          uint32_t tvo, uint32_t tso, const Mc& m, uint32_t* lds, const Th& h) {
 #pragma unroll
@@ -471,7 +487,7 @@ __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v
     for (int i = 0; i < 4; ++i) a[i] = (int)pk_canon(x[p3(c, i)]);
     const v4i tn = c + 1 < 16 ? bld(tab, tvo, tso + (uint32_t)(c + 1) * 1024u) : tv;
     v4i D[4];
-    tile<true>(D, M, a, comp);
+    tile<true, W16>(D, M, a, comp);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -486,6 +502,7 @@ __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v
   }
 }
 // inverse pass 2 (F^-1 in Q3), then its twist; packed output.
+template <bool W16>
 __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
                                          const Mc& m, uint32_t* lds, const Th& h) {
   const v4i z = {0, 0, 0, 0};
@@ -500,7 +517,7 @@ __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], R
     }
     const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 64u);
     v4i D[4];
-    tile<false>(D, M, b, z);
+    tile<false, W16>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -512,7 +529,7 @@ __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], R
 }
 // inverse pass 1 (per-wave matrix) on P2 chunks [C0, C0 + 8) at q2 slots
 // (the registers after the Q3 -> P2 swap); packed output.
-template <int C0>
+template <int C0, bool W16>
 __device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], const Mc& m) {
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
@@ -521,7 +538,7 @@ __device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], c
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x[q2(c, i)];
     v4i D[4];
-    tile<false>(D, M, b, z);
+    tile<false, W16>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       x[q2(c, i)] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
@@ -531,7 +548,7 @@ __device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], c
 }
 // inverse pass 0 on P1 chunks [C0, C0 + 8): canonical output; every four
 // chunks (the words of one 16-byte store per register) go to memory at once.
-template <int C0>
+template <int C0, bool W16>
 __device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], const Mc& m, Rsrc dst,
                                          const Th& h);
 
@@ -557,7 +574,7 @@ __device__ __forceinline__ void load_p1(uint32_t (&x1)[64], Rsrc src, const Th& 
       for (int e = 0; e < 4; ++e) x1[4 * (4 * hc + e) + i] = (uint32_t)v[e];
     }
 }
-template <int C0>
+template <int C0, bool W16>
 __device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], const Mc& m, Rsrc dst,
                                          const Th& h) {
   const v4i z = {0, 0, 0, 0};
@@ -567,7 +584,7 @@ __device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], 
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x1[4 * c + i];
     v4i D[4];
-    tile<false>(D, M, b, z);
+    tile<false, W16>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) x1[4 * c + i] = canon(recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m), m.q);
     if ((c & 3) == 3) {
@@ -617,7 +634,7 @@ __device__ __forceinline__ Tabs tabs_of(const void* mf, const LimbConst<uint32_t
 struct NoEpi {
   __device__ void operator()(int, const int32_t (&)[4], uint32_t (&)[64]) const {}
 };
-template <bool SYNC1, class EPI = NoEpi>
+template <bool SYNC1, bool W16 = false, class EPI = NoEpi>
 __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds, const Th& h, const Tabs& T,
                                     const EPI& epi = EPI{}) {
   // the first pass's operands load ahead of the plane (cache hits, needed
@@ -629,12 +646,12 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   const v4i comp = bld(T.tab, lo, (uint32_t)kCompF1 * 16u);
   uint32_t x1[64];
   load_p1(x1, src, h);
-  pass_p1<0, true>(x1, M, comp, m);
+  pass_p1<0, true, W16>(x1, M, comp, m);
   if constexpr (SYNC1) __syncthreads();
   uint32_t wb[4], rb[4];
   p1_bases(wb, h);
   x_write_p1<0>(x1, lds, wb);
-  pass_p1<8, true>(x1, M, comp, m);
+  pass_p1<8, true, W16>(x1, M, comp, m);
   __syncthreads();
   p2_bases(rb, h);
   x_read_p2<0>(x2, lds, rb);
@@ -643,16 +660,16 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   x_write_p1<1>(x1, lds, wb);
   load_mat(M, T.tab, S_F2 + h.w, lo);
   const uint32_t t3v = h.g() * 256u, t3s = (uint32_t)(kTw3f + h.w * 64) * 16u;
-  pass_p2<0>(x2, M, T.tab, t3v, t3s, m);
+  pass_p2<0, W16>(x2, M, T.tab, t3v, t3s, m);
   __syncthreads();
   p2_bases(rb, h);
   x_read_p2<1>(x2, lds, rb);
-  pass_p2<8>(x2, M, T.tab, t3v, t3s, m);
+  pass_p2<8, W16>(x2, M, T.tab, t3v, t3s, m);
   swap_p2p3(x2);
   load_mat(M, T.tab, S_F3, lo);
-  pass_p3(x2, M, T.tab, lo, (uint32_t)(kTw4f + h.w * 1024) * 16u, m);
+  pass_p3<W16>(x2, M, T.tab, lo, (uint32_t)(kTw4f + h.w * 1024) * 16u, m);
   load_mat(M, T.tab, S_F4, lo);
-  pass_p4(x2, M, m, epi);
+  pass_p4<W16>(x2, M, m, epi);
 }
 
 // The inverse in place: the NTT-domain plane (device order, P4 positions)
@@ -662,7 +679,10 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
 // plane (cache hits, needed first); its first tile then waits only for
 // its own words.  In place: a wave stores only after the exchanges'
 // barriers, which it passes once it has used (so read) every word it loaded.
-__device__ __forceinline__ void inv(Rsrc pr, uint32_t* lds, const Th& h, const Tabs& T) {
+// LOAD = false: the plane is already in x2 (P4 positions, canonical), as a
+// forward pass's epilogue left it; the LDS may still be read by other waves.
+template <bool LOAD, bool W16 = false>
+__device__ __forceinline__ void inv_x(uint32_t (&x2)[64], Rsrc pr, uint32_t* lds, const Th& h, const Tabs& T) {
   const Mc& m = T.m;
   const uint32_t lo = h.lam() * 16u;
   v4i M[4];
@@ -670,25 +690,28 @@ __device__ __forceinline__ void inv(Rsrc pr, uint32_t* lds, const Th& h, const T
   const v4i comp = bld(T.tab, lo, (uint32_t)kCompI4 * 16u);
   const uint32_t t4s = (uint32_t)(kTw4i + h.w * 1024) * 16u;
   const v4i tv0 = bld(T.tab, lo, t4s);
-  uint32_t x2[64];
+  if constexpr (LOAD) {
 #pragma unroll
-  for (int cc = 0; cc < 16; ++cc) {
-    const v4i v = bld(pr, p4_lane(h), p4_soff(h, cc));
+    for (int cc = 0; cc < 16; ++cc) {
+      const v4i v = bld(pr, p4_lane(h), p4_soff(h, cc));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) x2[p3(cc, i)] = (uint32_t)v[i];
+      for (int i = 0; i < 4; ++i) x2[p3(cc, i)] = (uint32_t)v[i];
+    }
+  } else {
+    __syncthreads();  // ipass_p4's stash reuses the LDS of the last exchange
   }
-  ipass_p4(x2, M, comp, tv0, T.tab, lo, t4s, m, lds, h);
+  ipass_p4<W16>(x2, M, comp, tv0, T.tab, lo, t4s, m, lds, h);
   load_mat(M, T.tab, S_I3, lo);
-  ipass_p3(x2, M, T.tab, h.g() * 16u, (uint32_t)(kTw3i + h.w * 64) * 16u, m, lds, h);
+  ipass_p3<W16>(x2, M, T.tab, h.g() * 16u, (uint32_t)(kTw3i + h.w * 64) * 16u, m, lds, h);
   swap_q3p2(x2);
   load_mat(M, T.tab, S_I2 + h.w, lo);
   uint32_t wb[4], rb[4];
   uint32_t x1[64];
-  ipass_p2<0>(x2, M, m);
+  ipass_p2<0, W16>(x2, M, m);
   __syncthreads();  // other waves may still read the LDS (the last forward exchange)
   p2_bases(rb, h);
   x_write_p2<0>(x2, lds, rb);
-  ipass_p2<8>(x2, M, m);
+  ipass_p2<8, W16>(x2, M, m);
   __syncthreads();
   p1_bases(wb, h);
   x_read_p1<0>(x1, lds, wb);
@@ -696,11 +719,15 @@ __device__ __forceinline__ void inv(Rsrc pr, uint32_t* lds, const Th& h, const T
   p2_bases(rb, h);
   x_write_p2<1>(x2, lds, rb);
   load_mat(M, T.tab, S_I1, lo);
-  ipass_p1<0>(x1, M, m, pr, h);
+  ipass_p1<0, W16>(x1, M, m, pr, h);
   __syncthreads();
   p1_bases(wb, h);
   x_read_p1<1>(x1, lds, wb);
-  ipass_p1<8>(x1, M, m, pr, h);
+  ipass_p1<8, W16>(x1, M, m, pr, h);
+}
+__device__ __forceinline__ void inv(Rsrc pr, uint32_t* lds, const Th& h, const Tabs& T) {
+  uint32_t x2[64];
+  inv_x<true>(x2, pr, lds, h, T);
 }
 
 }  // namespace mf
@@ -731,6 +758,100 @@ k_mf_ntt(uint32_t* __restrict__ data, const void* __restrict__ mft, const LimbCo
   } else {
     inv(pr, lds, h, T);
   }
+}
+
+// The ciphertext tensor product at N = 2^16 (rnt_ct_tensor and the
+// relinearised ct-mul, engine.rs:480-493) on the matrix-core transforms, one
+// workgroup per (poly, limb): the four forward transforms run one after the
+// other, each last pass's epilogue combining tile by tile with what the
+// earlier ones left in memory at the same device-order positions (written
+// and read back by the same thread):
+//   fwd c0  -> c0^ into d1's plane (a temporary);  fwd c1 -> c1^ into the
+//   CU's scratch slot (k_plane_fused_slots' indexing, or the pair's own
+//   plane below kPlaneSlots pairs);  fwd c0' -> d0 = c0^ c0'^ (final) and
+//   t = c1^ c0'^ into d2's plane;  fwd c1' -> d1 = t + c0^ c1'^ (final) and
+//   d2 = c1^ c1'^ 2^32 in registers, inverse-transformed from there into
+//   d2's plane (coefficient domain).
+// d0, d1 carry the Montgomery factor 2^-32 as k_tensor_rows' do (key-switch
+// seeds); the same words.  HBM: the 4 operand planes in, 3 planes out (the
+// temporaries are rewritten within the workgroup's life and the slot is
+// the CU's), against 17 planes through the column and row kernels.
+__global__ void __launch_bounds__(mf::kT, 1)
+k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __restrict__ d2, uint64_t ols,
+            const uint32_t* __restrict__ c0, const uint32_t* __restrict__ c1, const uint32_t* __restrict__ c0p,
+            const uint32_t* __restrict__ c1p, uint64_t ils, uint32_t* __restrict__ scratch, uint32_t slots,
+            const void* __restrict__ mft, const LimbConst<uint32_t>* __restrict__ lcs) {
+  using namespace mf;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const Th h(threadIdx.x);
+  const uint32_t poly = blockIdx.x, l = blockIdx.y;
+  const uint64_t oo = (uint64_t)l * ols + (uint64_t)poly * kN, io = (uint64_t)l * ils + (uint64_t)poly * kN;
+  const LimbConst<uint32_t> lc = lcs[l];
+  const Tabs T = tabs_of(mft, lc, l);
+  const uint32_t q = lc.q, nqi = T.m.nqinv;
+  uint64_t so;
+  if (slots) {
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;          // hwreg(HW_REG_XCC_ID)
+    const uint32_t cu = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8) & 0xffu;  // hwreg(HW_REG_HW_ID)[15:8]
+    so = (uint64_t)((xcc << 8) | cu) << 16;
+  } else {
+    so = (uint64_t)(poly + l * gridDim.x) << 16;
+  }
+  const Rsrc R0 = rsrc(d0 + oo, kN * 4u), R1 = rsrc(d1 + oo, kN * 4u), R2 = rsrc(d2 + oo, kN * 4u);
+  const Rsrc RS = rsrc(scratch + so, kN * 4u);
+  // Every transform runs with W16 (tile): the extra MFMA wait states this
+  // kernel's register allocation needs.  The lane offset is computed once
+  // per kernel, and the epilogues' products are plain C++.
+  const uint32_t pl = p4_lane(h);
+  auto canon4 = [q](const int32_t (&r)[4]) {
+    return v4i{(int)canon(r[0], (int32_t)q), (int)canon(r[1], (int32_t)q), (int)canon(r[2], (int32_t)q),
+               (int)canon(r[3], (int32_t)q)};
+  };
+  auto mmul = [q, nqi](uint32_t a, uint32_t b) {  // a b 2^-32 mod q, canonical
+    const uint64_t t = (uint64_t)a * b;
+    const uint32_t mm = (uint32_t)t * nqi;
+    const uint32_t r = (uint32_t)((t + (uint64_t)mm * q) >> 32);
+    return r >= q ? r - q : r;
+  };
+  const uint32_t rm = lc.rmod, rmp = lc.rmod_p;
+  uint32_t x[64];
+  fwd<false, true>(x, rsrc(c0 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+    bst(canon4(r), R1, pl, p4_soff(h, cc));
+  });
+  fwd<true, true>(x, rsrc(c1 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+    bst(canon4(r), RS, pl, p4_soff(h, cc));
+  });
+  fwd<true, true>(x, rsrc(c0p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+    const v4i a0 = bld(R1, pl, p4_soff(h, cc)), a1 = bld(RS, pl, p4_soff(h, cc));
+    const v4i b = canon4(r);
+    v4i o0, t;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o0[i] = (int)mmul((uint32_t)a0[i], (uint32_t)b[i]);
+      t[i] = (int)mmul((uint32_t)a1[i], (uint32_t)b[i]);
+    }
+    bst(o0, R0, pl, p4_soff(h, cc));
+    bst(t, R2, pl, p4_soff(h, cc));
+  });
+  fwd<true, true>(x, rsrc(c1p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
+    const v4i a0 = bld(R1, pl, p4_soff(h, cc)), a1 = bld(RS, pl, p4_soff(h, cc));
+    const v4i t = bld(R2, pl, p4_soff(h, cc));
+    const v4i b = canon4(r);
+    v4i o1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t s = (uint32_t)t[i] + mmul((uint32_t)a0[i], (uint32_t)b[i]);
+      o1[i] = (int)(s >= q ? s - q : s);
+      // c1^ c1'^ 2^-32, times 2^32 (Shoup by 2^32 mod q): the exact product
+      const uint32_t m = mmul((uint32_t)a1[i], (uint32_t)b[i]);
+      const uint32_t qh = (uint32_t)(((uint64_t)m * rmp) >> 32);
+      const uint32_t v = m * rm - qh * q;
+      xx[p3(cc, i)] = v >= q ? v - q : v;
+    }
+    bst(o1, R1, pl, p4_soff(h, cc));
+  });
+  inv_x<false, true>(x, R2, lds, h, T);
 }
 
 // ---------------------------------------------------------------------------
@@ -923,6 +1044,20 @@ static hipError_t launch_ntt_t(const Launch& k, const void* fn, void* data, uint
   const void* mft = k.t->mf;
   const LimbConst<uint32_t>* lcs = (const LimbConst<uint32_t>*)k.t->lconst;
   void* args[] = {&d, &mft, &lcs, &ls};
+  return hipLaunchKernel(fn, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), args, mf::kLdsBytes, k.s);
+}
+
+hipError_t launch_mf_tensor(const Launch& k, void* d0, void* d1, void* d2, uint64_t ols, const void* c0,
+                            const void* c1, const void* c0p, const void* c1p, uint64_t ils, void* scratch) {
+  if (k.B == 0 || k.L == 0) return hipSuccess;
+  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  const void* fn = (const void*)k_mf_tensor;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mf::kLdsBytes);
+  if (e != hipSuccess) return e;
+  uint32_t slots = (uint64_t)k.B * k.L >= kPlaneSlots ? 1u : 0u;  // plane_scratch_planes
+  const void* mft = k.t->mf;
+  const LimbConst<uint32_t>* lcs = (const LimbConst<uint32_t>*)k.t->lconst;
+  void* args[] = {&d0, &d1, &d2, &ols, &c0, &c1, &c0p, &c1p, &ils, &scratch, &slots, &mft, &lcs};
   return hipLaunchKernel(fn, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), args, mf::kLdsBytes, k.s);
 }
 

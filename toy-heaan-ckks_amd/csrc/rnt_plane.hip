@@ -654,7 +654,6 @@ k_plane_fused(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, ui
 // select keeps k_plane_fused's address form (its SGPR allocation).
 // Same-box A/B at the metric: 140.1k against 138.6k poly-muls/s, every word
 // of the 1024 x 16 output equal (profiles/r04/ab_plane_slots.txt).
-constexpr uint32_t kPlaneSlots = 1u << 11;
 static_assert(plane::LDS_WORDS * 4 > 80 * 1024, "one workgroup per CU");
 __global__ void __launch_bounds__(plane::T, 1)
 k_plane_fused_slots(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint32_t* __restrict__ scratch,
