@@ -179,3 +179,21 @@ def test_mf_tensor_slot_scratch_batch(ring, monkeypatch):
             want = _seeds_want(Bo, mod, *ch)
             for i in range(3):
                 assert np.array_equal(d[i].channels_of(p)[0], want[i]), (plane, i, p)
+
+
+def test_mf_tensor_full_output_32_ciphertexts(ring, monkeypatch):
+    """Every word of d0^, d1^ and d2 for 32 ciphertexts (512 (poly, limb)
+    pairs) equal to the four-step tensor's: the check that caught the MFMA
+    wait-state hazard (tile<..., W16> in rnt_mfma.hip; tools/tensor_stress2.py
+    runs it at larger batches)."""
+    rn, mod, *_ = ring
+    Bc = 32
+    outs = {}
+    for plane in (None, "0"):
+        Bd = _basis(rn, mod, monkeypatch, plane)
+        drng = rn.DeviceRng(4242)
+        c = [rn.RnsPoly.sample_uniform(Bd, drng, Bc) for _ in range(4)]
+        outs[plane] = [x.channels() for x in rn.ct_tensor(*c)]
+    for i in range(3):
+        bad = int((outs[None][i] != outs["0"][i]).sum())
+        assert bad == 0, (i, bad)

@@ -27,8 +27,14 @@ def short(kname):
     m = re.search(r"\bk_mf_ntt<(true|false)>", kname)
     if m:
         return "mf_ntt_inv" if m.group(1) == "true" else "mf_ntt_fwd"
-    if re.search(r"\bk_plane_fused\(", kname):
+    if re.search(r"\bk_plane_fused(_slots)?\(", kname):
         return "plane_fused"
+    if re.search(r"\bk_mf_tensor\(", kname):
+        return "mf_tensor"
+    if re.search(r"\bk_ks_whole<unsigned int", kname):
+        return "ks_whole"
+    if re.search(r"\bk_tensor_rows<unsigned (int|long), \d+, true>", kname):
+        return "tensor_whole"
     m = re.search(r"\bk_row<unsigned (int|long), (\d), \d+, (true|false), true>", kname)
     if m:
         return ("whole_fwd", "whole_inv", "whole_mul")[int(m.group(2))]
