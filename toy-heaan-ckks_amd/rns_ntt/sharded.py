@@ -292,6 +292,9 @@ def _device_of(t):
 # ---------------------------------------------------------------------------
 
 
+_TORCH_ALLOC_LOCK = threading.Lock()
+
+
 class GpuBackend:
     """Compute on this rank's GPU through librnsntt; exchange buffers are
     torch tensors wrapped as non-owning RnsPoly views (rnt_buf_wrap), so the
@@ -338,15 +341,21 @@ class GpuBackend:
             basis.sync()
 
     def _empty(self, basis, shape):
-        try:
-            return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
-        except self.torch.cuda.OutOfMemoryError:
-            # the library's device block cache may hold the memory torch needs
-            from . import pool_trim
+        # one allocation at a time across the backends of a process: thread
+        # ranks (ThreadComm) share one device, and concurrent torch.empty
+        # calls beside the library's own allocations in other threads took a
+        # pytest process down once (a segfault inside torch.empty,
+        # tests/test_gpu_sharded_configs.py, r04)
+        with _TORCH_ALLOC_LOCK:
+            try:
+                return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
+            except self.torch.cuda.OutOfMemoryError:
+                # the library's device block cache may hold the memory torch needs
+                from . import pool_trim
 
-            if pool_trim(self.device) == 0:
-                raise
-            return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
+                if pool_trim(self.device) == 0:
+                    raise
+                return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
 
     def _wrap(self, basis, t, B, ntt=False):
         from . import RnsPoly
