@@ -686,7 +686,8 @@ bool mul_truncated(const Tables* t) {
 // the product is one launch moving 3 planes per (poly, limb), a transform
 // one launch moving 2.
 template <class W, int MODE, int LOG_C, bool LZ = false, bool WHOLE = false>
-__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? (WHOLE ? kWholeMinWaves : kRowMinWaves) : 1)
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? (WHOLE ? kWholeMinWaves : kRowMinWaves)
+                                                                 : (WHOLE && MODE == 2 && LOG_C >= 13 ? 4 : 1))
 k_row(W* __restrict__ xg, const W* __restrict__ yg, W* __restrict__ outg, TabPtrs<W> tp, uint32_t log_n,
       uint32_t B, uint64_t ls, uint64_t rows_total) {
   using G = RowGeo<LOG_C>;
@@ -1641,13 +1642,15 @@ static hipError_t row_launch(const Launch& k, void* x, const void* y, uint64_t l
 // The whole-plane row path (k_row<..., WHOLE>): every (poly, limb) plane is
 // one row.  u32 and u64 words at 2^10 <= N <= 2^14 (a row of 2^14 words is
 // 1024 threads x 16 registers); RNT_PLANE=0 keeps the four-step kernels.
-// The u64 product stays on the four-step kernels above 2^12: its rows need
-// ~150 VGPRs, so a CU holds one 512- or 1024-thread workgroup of them (two
-// waves per SIMD) and measured slower (N = 2^13 x 7 x 61-bit: 0.67M against
-// 0.76M poly-muls/s; capped at 128 VGPRs it spills 76 bytes a lane).
+// The u64 product rows at 2^13 and 2^14 are capped at 128 VGPRs (four
+// waves per SIMD: 2^13 spills 92 bytes a lane, 2^14 12): uncapped they
+// took ~150 and a CU held one workgroup (2^13 x 7 x 61-bit: 0.67M against
+// the four-step kernels' 0.76M poly-muls/s); capped, 0.80M against 0.75M
+// at 2^13 x 7 and 0.80M against 0.795M at 2^14 x 3, same box
+// (profiles/r04/ab_u64_whole.txt).
 bool whole_ok(const Tables* t, int mode) {
-  if (t->plane == 0 || t->log_n < 10 || t->log_n > 14) return false;
-  return !(t->wide && mode == 2 && t->log_n > 12);
+  (void)mode;
+  return t->plane != 0 && t->log_n >= 10 && t->log_n <= 14;
 }
 
 template <class W>
@@ -1659,8 +1662,7 @@ static hipError_t whole_t(const Launch& k, int mode, void* out, void* x, const v
     if constexpr (sizeof(W) == 4) {                                                                   \
       if (lz) return row_launch<W, 2, C, true, true>(k, x, y, ls, out);                               \
     }                                                                                                 \
-    if constexpr (sizeof(W) == 8 && C > 12) return hipErrorInvalidValue; /* whole_ok */              \
-    else return row_launch<W, 2, C, false, true>(k, x, y, ls, out);
+    return row_launch<W, 2, C, false, true>(k, x, y, ls, out);
   switch (k.t->log_n) {
     RNT_W(10)
     RNT_W(11)
@@ -2296,7 +2298,10 @@ static hipError_t tensor_whole_t(const Launch& k, void* d0hat, void* d1hat, void
 #undef RNT_W
   return hipErrorInvalidValue;  // tensor_whole_ok
 }
-bool tensor_whole_ok(const Tables* t) { return whole_ok(t, 2) && t->log_n <= kKsWholeMaxLogN; }
+// (the u64 tensor holds four operand planes: N <= 2^12 only)
+bool tensor_whole_ok(const Tables* t) {
+  return whole_ok(t, 2) && t->log_n <= kKsWholeMaxLogN && !(t->wide && t->log_n > 12);
+}
 hipError_t launch_tensor_whole(const Launch& k, void* d0hat, void* d1hat, void* d2, uint64_t ls,
                                const void* c0, const void* c1, const void* c0p, const void* c1p,
                                uint64_t in_ls) {
