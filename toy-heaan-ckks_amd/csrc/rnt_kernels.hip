@@ -687,7 +687,7 @@ bool mul_truncated(const Tables* t) {
 // one launch moving 2.
 template <class W, int MODE, int LOG_C, bool LZ = false, bool WHOLE = false>
 __global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? (WHOLE ? kWholeMinWaves : kRowMinWaves)
-                                                                 : (WHOLE && MODE == 2 && LOG_C >= 13 ? 4 : 1))
+                                                                 : (MODE == 2 && LOG_C >= (WHOLE ? 13 : 7) ? 4 : 1))
 k_row(W* __restrict__ xg, const W* __restrict__ yg, W* __restrict__ outg, TabPtrs<W> tp, uint32_t log_n,
       uint32_t B, uint64_t ls, uint64_t rows_total) {
   using G = RowGeo<LOG_C>;
@@ -1642,6 +1642,10 @@ static hipError_t row_launch(const Launch& k, void* x, const void* y, uint64_t l
 // The whole-plane row path (k_row<..., WHOLE>): every (poly, limb) plane is
 // one row.  u32 and u64 words at 2^10 <= N <= 2^14 (a row of 2^14 words is
 // 1024 threads x 16 registers); RNT_PLANE=0 keeps the four-step kernels.
+// The u64 four-step product rows of 2^7..2^9 words are capped at 128 VGPRs
+// too (they took 131-132, three waves per SIMD; 12-28 bytes of spills):
+// k_row<2> at 2^16 x 16 x 62-bit 3.03-3.09 against 3.17-3.23 ms per 256
+// pairs (profiles/r04/ab_u64_rows.txt).
 // The u64 product rows at 2^13 and 2^14 are capped at 128 VGPRs (four
 // waves per SIMD: 2^13 spills 92 bytes a lane, 2^14 12): uncapped they
 // took ~150 and a CU held one workgroup (2^13 x 7 x 61-bit: 0.67M against
