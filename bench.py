@@ -15,8 +15,11 @@ per GPU fixed (weak scaling) and need no data-path collective for poly-mul;
 only the timing barrier / max-reduce crosses ranks (gloo control plane).
 
 `--workload ctmul` times BASELINE config 4's pipeline instead: ct x ct ->
-gadget relinearisation -> rescale, limb-sharded with the RCCL all-gather of
-d2 and broadcast of the last limb (rns_ntt.sharded).
+gadget relinearisation -> rescale.  At N > 1 its default layout is
+`--shard batch` (each rank its own ciphertexts over all limbs, no data-path
+collective: DESIGN.md §7's model puts it ahead at config 4); `--shard limb`
+runs it limb-sharded with the RCCL all-gather of d2 and broadcast of the
+last limb (rns_ntt.sharded).
 
 Prints ONE JSON line on rank 0.
 """
@@ -60,7 +63,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", choices=("polymul", "ctmul", "rotate", "encode", "ntt", "pointwise", "copy"),
                    default="polymul")
-    p.add_argument("--shard", choices=("limb", "batch"), default="limb")
+    p.add_argument("--shard", choices=("limb", "batch"), default=None,
+                   help="multi-GPU layout; default: batch for ctmul (no collective; DESIGN.md §7's "
+                        "model puts it 15-30%% ahead of the limb shard at config 4 on 8 GPUs), "
+                        "limb otherwise (the north star's layout)")
     p.add_argument("--batch", type=int, default=1024, help="poly-mul pairs per GPU per step")
     p.add_argument("--inputs", choices=("device", "host"), default="device",
                    help="poly-mul operands: seeded uniform residues drawn on the device (Philox, "
@@ -88,7 +94,10 @@ def parse():
     p.add_argument("--strong", action="store_true",
                    help="poly-mul: --batch is the fixed global batch split over the ranks (strong "
                         "scaling) instead of the per-GPU batch (weak, the default)")
-    return p.parse_args()
+    args = p.parse_args()
+    if args.shard is None:
+        args.shard = "batch" if args.workload == "ctmul" else "limb"
+    return args
 
 
 def relaunch_with_torchrun(args) -> int:

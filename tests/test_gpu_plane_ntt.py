@@ -181,19 +181,56 @@ def test_mf_tensor_slot_scratch_batch(ring, monkeypatch):
                 assert np.array_equal(d[i].channels_of(p)[0], want[i]), (plane, i, p)
 
 
-def test_mf_tensor_full_output_32_ciphertexts(ring, monkeypatch):
-    """Every word of d0^, d1^ and d2 for 32 ciphertexts (512 (poly, limb)
-    pairs) equal to the four-step tensor's: the check that caught the MFMA
-    wait-state hazard (tile<..., W16> in rnt_mfma.hip; tools/tensor_stress2.py
-    runs it at larger batches)."""
+@pytest.mark.parametrize("Bc", [32, 128])
+def test_mf_tensor_full_output(ring, monkeypatch, Bc):
+    """Every word of d0^, d1^ and d2 equal to the four-step tensor's, for 32
+    ciphertexts (512 (poly, limb) pairs: c1^ in the pairs' own scratch
+    planes) and 128 (2048 pairs: the CU-indexed scratch slots, kPlaneSlots).
+    The check that caught r04's MFMA hazard (16-300 wrong words per 2^26
+    before the tiles were made hazard-free by construction, DESIGN.md §3
+    "MFMA hazards")."""
     rn, mod, *_ = ring
-    Bc = 32
     outs = {}
     for plane in (None, "0"):
         Bd = _basis(rn, mod, monkeypatch, plane)
-        drng = rn.DeviceRng(4242)
+        drng = rn.DeviceRng(4242 + Bc)
         c = [rn.RnsPoly.sample_uniform(Bd, drng, Bc) for _ in range(4)]
-        outs[plane] = [x.channels() for x in rn.ct_tensor(*c)]
+        outs[plane] = rn.ct_tensor(*c)
     for i in range(3):
-        bad = int((outs[None][i] != outs["0"][i]).sum())
+        a, b = outs[None][i].channels_batch(), outs["0"][i].channels_batch()
+        bad = int((a != b).sum())
         assert bad == 0, (i, bad)
+        del a, b
+
+
+def test_mf_ntt_full_output_1024_planes(ring, monkeypatch):
+    """k_mf_ntt forward and inverse, every word of 64 polys x 16 limbs = 1024
+    planes against the four-step kernels (RNT_PLANE=0) on the same
+    device-drawn data: the forward on coefficient-domain input, the inverse
+    on the same words taken as NTT-domain input (device order), and
+    inverse(forward) = identity on the default path."""
+    rn, mod, *_ = ring
+    Bp = 64
+    fwd, inv, x0 = {}, {}, None
+    for plane in (None, "0"):
+        Bd = _basis(rn, mod, monkeypatch, plane)
+        x = rn.RnsPoly.sample_uniform(Bd, rn.DeviceRng(0x1024), Bp)
+        if plane is None:
+            x0 = x.channels_batch()
+        x.to_ntt_domain()
+        fwd[plane] = x.channels_batch()
+        if plane is None:
+            x.to_coeff_domain()
+            back = x.channels_batch()
+            assert int((back != x0).sum()) == 0
+            del back
+        del x
+        # the same sampled words as NTT-domain input: a fresh draw, relabelled
+        y = rn.RnsPoly.sample_uniform(Bd, rn.DeviceRng(0x1025), Bp)
+        z = rn.RnsPoly.wrap(Bd, y.device_ptr()[0], Bp, in_ntt_domain=True)
+        z.to_coeff_domain()
+        inv[plane] = y.channels_batch()
+        del z, y
+    bad_f = int((fwd[None] != fwd["0"]).sum())
+    bad_i = int((inv[None] != inv["0"]).sum())
+    assert bad_f == 0 and bad_i == 0, (bad_f, bad_i)

@@ -1,0 +1,62 @@
+"""tools/isa_check.py (the build-time ISA hazard check, DESIGN.md §3 "MFMA
+hazards") on synthetic gfx950 instruction sequences: each rule fires on the
+pattern it names and stays quiet on the shape the hazard-safe tile emits."""
+from __future__ import annotations
+
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+import isa_check as ic  # noqa: E402
+
+MF = "v_mfma_i32_16x16x64_i8"
+
+
+def kinds(lines):
+    body = [(None, t) for t in lines]
+    return sorted({k for k, _, _ in ic.check_kernel(body, 0)})
+
+
+def test_safe_tile_shape_is_clean():
+    # the asm tile: operands 2 states old, early-clobber D, 8 states of pad
+    lines = ["v_xor_b32_e32 v90, 0x80808080, v0", "s_nop 1",
+             f"{MF} v[0:3], v[10:13], v[90:93], v[20:23]", f"{MF} v[4:7], v[14:17], v[90:93], 0",
+             f"{MF} v[30:33], v[18:21], v[90:93], 0", f"{MF} v[34:37], v[22:25], v[90:93], 0", "s_nop 7",
+             "v_lshl_add_u32 v40, v34, 8, v30", "v_mov_b32_e32 v90, 0"]
+    assert kinds(lines) == []
+
+
+def test_d_overlapping_b_is_flagged():
+    lines = ["s_nop 1", f"{MF} v[88:91], v[10:13], v[88:91], 0", "s_nop 7"]
+    assert "M3" in kinds(lines)
+
+
+def test_early_read_of_d_is_flagged():
+    lines = ["s_nop 1", f"{MF} v[0:3], v[10:13], v[90:93], 0", "s_nop 2", "v_add_u32_e32 v5, v0, v1"]
+    assert "M1" in kinds(lines)
+
+
+def test_write_of_in_flight_operand_is_flagged():
+    lines = ["s_nop 1", f"{MF} v[0:3], v[10:13], v[90:93], 0", "s_nop 5", "v_mov_b64_e32 v[90:91], s[10:11]"]
+    assert "M2" in kinds(lines)
+
+
+def test_fresh_operand_is_flagged():
+    lines = ["v_xor_b32_e32 v90, 0x80808080, v0", f"{MF} v[0:3], v[10:13], v[90:93], 0", "s_nop 7"]
+    assert "M4" in kinds(lines)
+
+
+def test_unwaited_load_register_is_flagged_and_waited_one_is_not():
+    bad = ["ds_read_b32 v5, v1 offset:64", "v_mov_b32_e32 v6, v5", "s_waitcnt lgkmcnt(0)"]
+    good = ["ds_read_b32 v5, v1 offset:64", "s_waitcnt lgkmcnt(0)", "v_mov_b32_e32 v6, v5"]
+    assert kinds(bad) == ["L1"]
+    assert kinds(good) == []
+    # in-order VMEM returns: vmcnt(1) retires the older of two loads
+    two = ["buffer_load_dword v5, v1, s[4:7], 0 offen", "buffer_load_dword v6, v1, s[4:7], 0 offen",
+           "s_waitcnt vmcnt(1)", "v_mov_b32_e32 v7, v5", "v_mov_b32_e32 v8, v6"]
+    assert kinds(two) == ["L1"]
+
+
+def test_lds_dma_has_no_register_destination():
+    lines = ["global_load_lds_dword v20, s[44:45]", "v_mov_b32_e32 v20, 0"]
+    assert kinds(lines) == []

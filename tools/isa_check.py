@@ -1,0 +1,354 @@
+#!/usr/bin/env python3
+"""Build-time ISA hazard check of librnsntt's gfx950 code objects.
+
+hipcc's hazard recognizer pads the MFMA hazards of the instructions it
+generates, but not of inline asm (it schedules an asm statement as one opaque
+instruction), and it never counts an asm load's completion.  This scans the
+disassembly of every kernel in the given objects and reports, per kernel:
+
+  M1  a VGPR written by an MFMA (D) read or written by a later non-chained
+      instruction fewer than W_D wait states after that MFMA issued;
+  M2  a VGPR an MFMA reads (A, B or C) written by a later instruction fewer
+      than W_SRC wait states after it issued (the MFMA is still in flight);
+  M3  an MFMA whose D overlaps its A or B operand (partly or wholly);
+  M4  an MFMA operand written by a VALU / LDS / VMEM instruction fewer than
+      W_IN wait states before the MFMA;
+  L1  a VGPR that a DS / VMEM / scratch load writes, read or written before
+      the s_waitcnt that retires that load (the loads of inline asm are not
+      in hipcc's bookkeeping; a compiler copy of such a register before the
+      wait reads stale data).
+
+Wait states: one per instruction, N+1 for `s_nop N` (the ISA's counting,
+and LLVM's).  v_mfma_i32_16x16x64_i8 is a 4-pass XDL op on gfx950 (16
+cycles: the cycles of bf16 16x16x32, MI355X_MICROARCH.md "Matrix cores");
+hipcc's own window for an XDL D -> VALU read at 4 passes is 8 states
+(passes + 3, + 1 on gfx950), visible in every tile it emits.  The rule this
+repo applies ("MFMA hazards") is stricter and uniform: nothing
+touches any register an MFMA reads or writes until W_D = 8 states after the
+LAST MFMA of a tile has issued, an MFMA's D never overlaps its A/B, and an
+MFMA operand written by VALU / memory is 2+ states old at issue.
+
+Exit status 1 if any finding; `--allow KERNEL_SUBSTR` skips kernels.
+Usage: isa_check.py OBJ.o [OBJ.o ...] [--verbose]
+"""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+W_D = 8     # MFMA D -> any access (4-pass XDL on gfx950: passes + 4)
+W_SRC = 8   # MFMA A/B/C -> overwrite (in flight until its D is written)
+W_IN = 2    # VALU/memory write -> MFMA operand read
+
+REG = re.compile(r"^([vas])(?:(\d+)|\[(\d+):(\d+)\])$")
+
+
+def regs(tok: str):
+    """('v', {5,6}) for v[5:6]; None for non-register operands."""
+    m = REG.match(tok)
+    if not m:
+        return None
+    kind = m.group(1)
+    if m.group(2) is not None:
+        lo = hi = int(m.group(2))
+    else:
+        lo, hi = int(m.group(3)), int(m.group(4))
+    return kind, set(range(lo, hi + 1))
+
+
+def vset(toks):
+    out = set()
+    for t in toks:
+        r = regs(t)
+        if r and r[0] in "va":
+            out |= {(r[0], i) for i in r[1]}
+    return out
+
+
+def split_ops(s: str):
+    s = s.split("//")[0].strip()
+    parts = s.split(None, 1)
+    mn = parts[0]
+    rest = parts[1] if len(parts) > 1 else ""
+    ops = [o.strip() for o in rest.split(",")] if rest else []
+    # strip modifiers ("0 offen offset:16", "off offset:12")
+    clean = []
+    for o in ops:
+        clean.append(o.split()[0] if o else o)
+    return mn, clean, rest
+
+
+def defs_uses(mn: str, ops):
+    """VGPR/AGPR defs and uses of one instruction."""
+    if mn.startswith("s_") or not ops:
+        return set(), set()
+    if mn.startswith("v_mfma"):
+        return vset(ops[:1]), vset(ops[1:])
+    if mn.startswith(("v_cmp", "v_readlane", "v_readfirstlane")):
+        return set(), vset(ops[1:])
+    if mn.startswith(("v_permlane16_swap", "v_permlane32_swap")):
+        s = vset(ops[:2])
+        return s, s
+    if mn.startswith("v_writelane"):
+        s = vset(ops[:1])
+        return s, s | vset(ops[1:])
+    if mn.startswith(("global_load_lds", "buffer_load_lds")) or (mn.startswith("buffer_load") and " lds" in " ".join(ops)):
+        return set(), vset(ops)  # LDS DMA: the first operand is the address
+    if mn.startswith(("ds_read", "buffer_load", "global_load", "scratch_load", "flat_load")):
+        return vset(ops[:1]), vset(ops[1:])
+    if mn.startswith(("ds_write", "buffer_store", "global_store", "scratch_store", "flat_store")):
+        return set(), vset(ops)
+    if mn.startswith("v_"):
+        return vset(ops[:1]), vset(ops[1:])
+    if mn.startswith("ds_"):  # ds_swizzle, ds_bpermute, ds_add_rtn...
+        return vset(ops[:1]), vset(ops[1:])
+    return set(), vset(ops)
+
+
+def wait_states(mn: str, ops):
+    if mn == "s_nop":
+        return int(ops[0], 0) + 1
+    return 1
+
+
+def load_kind(mn: str):
+    if mn.startswith("ds_read") or (mn.startswith("ds_") and "rtn" in mn) or mn.startswith(("ds_swizzle", "ds_bpermute", "ds_permute")):
+        return "lgkm"
+    if mn.startswith(("buffer_load", "global_load", "scratch_load", "flat_load")):
+        return "vm"
+    return None
+
+
+def store_kind(mn: str):
+    if mn.startswith(("buffer_store", "global_store", "scratch_store", "flat_store")):
+        return "vm"
+    if mn.startswith("ds_write"):
+        return "lgkm"
+    return None
+
+
+WAITCNT = re.compile(r"(vmcnt|lgkmcnt|expcnt)\((\d+)\)")
+
+
+def disassemble(obj: str, tmp: str):
+    fat = os.path.join(tmp, "fat.bin")
+    co = os.path.join(tmp, "dev.co")
+    secs = subprocess.run([f"{LLVM}/llvm-readelf", "-S", obj], check=True, capture_output=True, text=True).stdout
+    if ".hip_fatbin" not in secs:
+        return ""  # host code only
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj, os.path.join(tmp, "x.o")],
+                   check=True, capture_output=True)
+    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+    out = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", co], check=True, capture_output=True,
+                         text=True).stdout
+    return out
+
+
+def kernels(dis: str):
+    cur, body, faddr = None, [], 0
+    for line in dis.splitlines():
+        m = re.match(r"^([0-9a-f]+) <(.+)>:$", line)
+        if m:
+            if cur:
+                yield cur, faddr, body
+            cur, body, faddr = m.group(2), [], int(m.group(1), 16)
+            continue
+        if cur and line.startswith("\t"):
+            txt = line.strip()
+            addr = None
+            am = re.search(r"//\s*([0-9A-F]+):", txt)
+            if am:
+                addr = int(am.group(1), 16)
+            body.append((addr, txt))
+    if cur:
+        yield cur, faddr, body
+
+
+TARGET = re.compile(r"<[^>+]+\+0x([0-9a-f]+)>")
+BRANCHES = ("s_branch", "s_cbranch_")
+
+
+class State:
+    """What is in flight at one point of the code: MFMAs (issue counter,
+    D, operands), un-waited loads, and the last VALU write of each register.
+    Counters are wait-state counts along the path."""
+
+    def __init__(self):
+        self.mfmas = []        # dict(end, dst, srcs, text)
+        self.alts = [[]]       # per incoming path: un-waited ops (kind, regs, text, is_smem)
+        self.last_write = {}   # reg -> counter after the write
+
+    def copy(self):
+        t = State()
+        t.mfmas = [dict(f) for f in self.mfmas]
+        t.alts = [list(a) for a in self.alts]
+        t.last_write = dict(self.last_write)
+        return t
+
+    def shifted(self, delta):
+        t = self.copy()
+        for f in t.mfmas:
+            f["end"] += delta
+        t.last_write = {r: v + delta for r, v in t.last_write.items()}
+        return t
+
+    def merge(self, o):
+        seen = {(f["text"], f["end"]) for f in self.mfmas}
+        self.mfmas += [f for f in o.mfmas if (f["text"], f["end"]) not in seen]
+        for a in o.alts:
+            if a not in self.alts:
+                self.alts.append(list(a))
+        for r, v in o.last_write.items():
+            self.last_write[r] = max(v, self.last_write.get(r, -10**9))
+
+
+def check_kernel(body, func_addr, verbose=False):
+    """One pass over the kernel in address order; forward branches carry
+    their state to the target (merged with the fall-through path); back
+    edges are not followed (the checked kernels are straight-line)."""
+    findings = []
+    st = State()
+    pending = {}  # target addr -> list of (State, counter at the branch)
+    since = 0
+    live = True   # the fall-through path reaches this instruction
+    for idx, (addr, txt) in enumerate(body):
+        if addr in pending:
+            arrivals = pending.pop(addr)
+            base = st if live else None
+            for s_b, c_b in arrivals:
+                moved = s_b.shifted(since - c_b - 1)
+                if base is None:
+                    base = moved
+                else:
+                    base.merge(moved)
+            st = base
+            live = True
+        if not live:
+            st = State()  # unreachable in this scan (a back-edge target)
+            live = True
+        mn, ops, rest = split_ops(txt)
+        d, u = defs_uses(mn, ops)
+        ws = wait_states(mn, ops)
+        # ---- L1: accesses to registers of loads not yet waited for
+        if mn == "s_waitcnt":
+            cnts = {k: int(v) for k, v in WAITCNT.findall(rest)}
+            for kind in ("vm", "lgkm"):
+                key = "vmcnt" if kind == "vm" else "lgkmcnt"
+                if key not in cnts:
+                    continue
+                n = cnts[key]
+                for ai, alt in enumerate(st.alts):
+                    ops_k = [o for o in alt if o[0] == kind]
+                    keep = [] if n == 0 else (ops_k[len(ops_k) - n:] if n < len(ops_k) else ops_k)
+                    st.alts[ai] = [o for o in alt if o[0] != kind] + keep
+        elif not mn.startswith("s_"):
+            touched = d | u
+            lk0 = load_kind(mn)
+            for o in {o for alt in st.alts for o in alt}:
+                if lk0 == o[0] and not (o[1] & u):
+                    continue  # a later load of the same counter: returns in order, lands last
+                if o[1] and (o[1] & touched):
+                    findings.append(("L1", idx, f"{txt}  touches {sorted(o[1] & touched)[:4]} of un-waited load `{o[2]}`"))
+        lk = load_kind(mn)
+        sk = store_kind(mn)
+        op = None
+        if mn.startswith("s_load") or mn.startswith("s_buffer_load"):
+            op = ("lgkm", frozenset(), f"{idx}: " + txt.split("//")[0].strip(), True)
+        elif lk:
+            op = (lk, frozenset(d), f"{idx}: " + txt.split("//")[0].strip(), False)
+        elif sk:
+            op = (sk, frozenset(), f"{idx}: " + txt.split("//")[0].strip(), False)
+        if op:
+            for alt in st.alts:
+                alt.append(op)
+        if len(st.alts) > 16:  # bound the path count: keep the longest lists
+            st.alts = sorted(st.alts, key=len)[-16:]
+        # ---- MFMA rules
+        is_mf = mn.startswith("v_mfma")
+        if is_mf:
+            a, b, c = vset(ops[1:2]), vset(ops[2:3]), vset(ops[3:4])
+            if vset(ops[:1]) & (a | b):
+                findings.append(("M3", idx, f"{txt}  D overlaps A/B"))
+            for r in a | b | c:
+                if r in st.last_write and since - st.last_write[r] < W_IN:
+                    findings.append(("M4", idx, f"{txt}  operand {r} written {since - st.last_write[r]} states before"))
+        for f in st.mfmas:
+            dist = since - f["end"]  # wait states between its issue and this instruction
+            if dist >= max(W_D, W_SRC):
+                continue
+            if is_mf:
+                cset = vset(ops[3:4])
+                if f["dst"] & vset(ops[1:3]) and dist < W_D:
+                    findings.append(("M1", idx, f"{txt}  reads D of `{f['text']}` as A/B after {dist}"))
+                if f["dst"] & cset and cset != f["dst"] and dist < W_D:
+                    findings.append(("M1", idx, f"{txt}  partial C overlap with D of `{f['text']}`"))
+                if (vset(ops[:1]) & f["srcs"]) and dist < W_SRC and vset(ops[:1]) != f["dst"]:
+                    findings.append(("M2", idx, f"{txt}  writes an operand of in-flight `{f['text']}` after {dist}"))
+                continue
+            if mn.startswith("s_"):
+                continue
+            if (f["dst"] & (d | u)) and dist < W_D:
+                findings.append(("M1", idx, f"{txt}  touches D {sorted(f['dst'] & (d | u))[:4]} of `{f['text']}` after {dist} states"))
+            if (f["srcs"] & d) and dist < W_SRC:
+                findings.append(("M2", idx, f"{txt}  overwrites operand {sorted(f['srcs'] & d)[:4]} of `{f['text']}` after {dist} states"))
+        since += ws
+        if is_mf:
+            st.mfmas.append({"end": since, "dst": vset(ops[:1]), "srcs": vset(ops[1:]), "text": txt.split("//")[0].strip()})
+        st.mfmas = [f for f in st.mfmas if since - f["end"] < 64]
+        if mn.startswith("v_") and not is_mf:
+            for r in d:
+                st.last_write[r] = since
+        # ---- control flow
+        if mn.startswith(BRANCHES):
+            m = TARGET.search(txt)
+            if m:
+                tgt = func_addr + int(m.group(1), 16)
+                if addr is None or tgt > addr:
+                    pending.setdefault(tgt, []).append((st.copy(), since))
+            if mn == "s_branch":
+                live = False
+        elif mn in ("s_setpc_b64", "s_endpgm"):
+            live = False
+    return findings
+
+
+def main(argv):
+    verbose = "--verbose" in argv
+    allow = []
+    objs = []
+    it = iter(argv)
+    for a in it:
+        if a == "--verbose":
+            continue
+        if a == "--allow":
+            allow.append(next(it))
+            continue
+        objs.append(a)
+    total = 0
+    with tempfile.TemporaryDirectory() as tmp:
+        for obj in objs:
+            dis = disassemble(obj, tmp)
+            for name, faddr, body in kernels(dis):
+                if any(s in name for s in allow):
+                    continue
+                fs = check_kernel(body, faddr, verbose)
+                n_mf = sum(1 for _, t in body if t.startswith("v_mfma"))
+                kinds = {}
+                for k, _, _ in fs:
+                    kinds[k] = kinds.get(k, 0) + 1
+                if fs or verbose:
+                    print(f"{os.path.basename(obj)} {name[:70]}: {len(body)} instrs, {n_mf} MFMA, findings {kinds}")
+                for k, i, msg in fs[: (10**9 if verbose else 12)]:
+                    print(f"  [{k}] #{i}: {msg}")
+                total += len(fs)
+    print(f"isa_check: {total} finding(s)")
+    return 1 if total else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))

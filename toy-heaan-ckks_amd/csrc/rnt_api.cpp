@@ -56,6 +56,7 @@ int fail_fields(int code, uint64_t a, uint64_t b, const char* fmt, ...) {
 }
 
 int hip_fail(hipError_t e, const char* where) {
+  (void)hipGetLastError();  // reported here: not pending for the next call
   if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
     return fail(RNT_ERR_OUT_OF_MEMORY, "%s: %s", where, hipGetErrorString(e));
   return fail(RNT_ERR_DEVICE, "%s: %s", where, hipGetErrorString(e));
@@ -97,6 +98,7 @@ const char* const kKernelNames[rnt::K_COUNT] = {
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
     "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd", "whole_inv", "whole_mul", "ks_whole", "tensor_whole", "mf_tensor"};
 
+inline void cleanup(hipError_t e, const char* where);
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
     hipEvent_t e = p->pool.back();
@@ -104,45 +106,84 @@ hipEvent_t prof_event(rnt::Prof* p) {
     return e;
   }
   hipEvent_t e = nullptr;
-  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  if (const hipError_t r = hipEventCreate(&e); r != hipSuccess) {
+    cleanup(r, "hipEventCreate(profile)");
+    return nullptr;
+  }
   return e;
 }
 
-// Bracket one launch with events when profiling is on.
-// A launcher reports hipGetLastError() after its launch, so an error an
-// earlier unchecked call left in the thread's last-error slot (a cleanup
-// path's (void)hipFree / hipEventDestroy) would be blamed on it: the slot
-// is read and cleared first (RNT_TRACE_STALE=1 names what it held).
-inline void clear_stale_error(int id) {
-  const hipError_t pre = hipGetLastError();
-  static const bool trace = [] {
-    const char* v = std::getenv("RNT_TRACE_STALE");
-    return v && *v && *v != '0';
-  }();
-  if (pre != hipSuccess && trace)
-    std::fprintf(stderr, "rnsntt: stale HIP error before %s: %s\n", kKernelNames[id], hipGetErrorString(pre));
+// HIP errors are never dropped.  A cleanup call whose failure cannot abort
+// the call making it (a block leaving the cache, a destructor, an event
+// released) goes through cleanup(): the first such failure on the thread is
+// kept with the call's name, and the runtime's last-error slot is cleared.
+// The library then reports it as RNT_ERR_DEVICE, naming that call: from the
+// entry point that made it when that one returns a status of its own
+// (rnt_buf_free, rnt_ctx_destroy, rnt_graph_destroy, rnt_pool_trim), else
+// from the next launch on the thread (check_pending).  A launcher reads
+// hipGetLastError() after its launch, so an error some other code left in
+// the slot would otherwise be blamed on the launch: check_pending reports it
+// before launching, as pending from an earlier call, instead of clearing it.
+struct Deferred {
+  hipError_t e = hipSuccess;
+  const char* where = nullptr;
+};
+thread_local Deferred g_deferred;
+
+inline void cleanup(hipError_t e, const char* where) {
+  if (e == hipSuccess) return;
+  (void)hipGetLastError();  // kept in g_deferred instead
+  if (g_deferred.e == hipSuccess) g_deferred = {e, where};
 }
 
+// RNT_OK, or the first deferred cleanup failure of this thread as a status.
+int take_deferred() {
+  if (g_deferred.e == hipSuccess) return RNT_OK;
+  const Deferred d = g_deferred;
+  g_deferred = {};
+  return fail(RNT_ERR_DEVICE, "%s failed: %s (a cleanup call, reported at the next status)", d.where,
+              hipGetErrorString(d.e));
+}
+
+// Before a launch: a deferred cleanup failure, or an error some earlier
+// runtime call on this thread left unreported in the last-error slot.
+int check_pending(int id) {
+  if (int rc = take_deferred()) return rc;
+  const hipError_t pre = hipGetLastError();
+  if (pre != hipSuccess)
+    return fail(RNT_ERR_DEVICE,
+                "a HIP error was pending before the %s launch, left by an earlier runtime call on this "
+                "thread that did not report it: %s",
+                kKernelNames[id], hipGetErrorString(pre));
+  return RNT_OK;
+}
+
+// Bracket one launch with events when profiling is on.
 template <class F>
 hipError_t prof_launch(const rnt::Tables* t, hipStream_t s, int id, F&& f) {
-  clear_stale_error(id);
   rnt::Prof* p = t->prof;
   if (p == nullptr || !p->on || g_capture != nullptr) return f();
   std::lock_guard<std::mutex> g(p->mu);
   hipEvent_t a = prof_event(p), b = prof_event(p);
-  if (a) (void)hipEventRecord(a, s);
+  if (a) cleanup(hipEventRecord(a, s), "hipEventRecord(profile)");
   hipError_t e = f();
-  if (b) (void)hipEventRecord(b, s);
+  if (b) cleanup(hipEventRecord(b, s), "hipEventRecord(profile)");
   if (a && b) p->pending.push_back({id, a, b});
   return e;
 }
 
 // Launch on the context's stream, or (LAUNCH_ON) on an explicit one; with
 // profiling on, the launch is bracketed by events on that same stream.
-#define LAUNCH(T, ID, EXPR, WHERE) \
-  HIP_TRY(prof_launch((T), (T)->stream, (ID), [&]() { return (EXPR); }), WHERE)
-#define LAUNCH_ON(T, S, ID, EXPR, WHERE) \
-  HIP_TRY(prof_launch((T), (S), (ID), [&]() { return (EXPR); }), WHERE)
+#define LAUNCH(T, ID, EXPR, WHERE)                                           \
+  do {                                                                       \
+    if (int rc_ = check_pending(ID)) return rc_;                             \
+    HIP_TRY(prof_launch((T), (T)->stream, (ID), [&]() { return (EXPR); }), WHERE); \
+  } while (0)
+#define LAUNCH_ON(T, S, ID, EXPR, WHERE)                                     \
+  do {                                                                       \
+    if (int rc_ = check_pending(ID)) return rc_;                             \
+    HIP_TRY(prof_launch((T), (S), (ID), [&]() { return (EXPR); }), WHERE);   \
+  } while (0)
 
 
 
@@ -207,13 +248,13 @@ static size_t pool_cap(int device) {  // g_pool_mu held
 }
 
 static void pool_release(const PoolBlock& w) {  // g_pool_mu NOT held
-  (void)hipSetDevice(w.device);
+  cleanup(hipSetDevice(w.device), "hipSetDevice(block leaving the cache)");
   if (w.ev) {
-    (void)hipEventSynchronize(w.ev);
+    cleanup(hipEventSynchronize(w.ev), "hipEventSynchronize(block leaving the cache)");
     std::lock_guard<std::mutex> lk(g_pool_mu);
     g_free_events.push_back(w.ev);
   }
-  (void)hipFree(w.p);
+  cleanup(hipFree(w.p), "hipFree(block leaving the cache)");
 }
 
 // Smallest idle block on `device` of at least `bytes` (and at most twice
@@ -249,8 +290,13 @@ static void* pool_take(int device, size_t bytes, hipStream_t s, size_t* got, boo
     // same stream: stream order already covers the last use; while a graph
     // is being recorded the wait is a host wait (a recording stream cannot
     // wait on an event from outside the recording)
-    if (w.s != s && (g_capture != nullptr || hipStreamWaitEvent(s, w.ev, 0) != hipSuccess))
-      (void)hipEventSynchronize(w.ev);
+    if (w.s != s) {
+      const hipError_t we = g_capture != nullptr ? hipErrorStreamCaptureUnsupported : hipStreamWaitEvent(s, w.ev, 0);
+      if (we != hipSuccess) {
+        if (g_capture == nullptr) (void)hipGetLastError();  // handled: a host wait instead
+        cleanup(hipEventSynchronize(w.ev), "hipEventSynchronize(block from the cache)");
+      }
+    }
     std::lock_guard<std::mutex> lk(g_pool_mu);
     g_free_events.push_back(w.ev);
   }
@@ -281,12 +327,14 @@ static void pool_give(int device, void* p, size_t bytes, hipStream_t s) {
     }
   }
   if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+  if (!ev) (void)hipGetLastError();  // handled: drain instead
   if (ev && hipEventRecord(ev, s) != hipSuccess) {
-    (void)hipStreamSynchronize(s);  // no event: drain instead
-    (void)hipEventDestroy(ev);
+    (void)hipGetLastError();  // handled: drain instead
+    cleanup(hipStreamSynchronize(s), "hipStreamSynchronize(block handed to the cache)");
+    cleanup(hipEventDestroy(ev), "hipEventDestroy(block handed to the cache)");
     ev = nullptr;
   } else if (!ev) {
-    (void)hipStreamSynchronize(s);
+    cleanup(hipStreamSynchronize(s), "hipStreamSynchronize(block handed to the cache)");
   }
   std::vector<PoolBlock> drop;
   {
@@ -306,7 +354,7 @@ static void pool_give(int device, void* p, size_t bytes, hipStream_t s) {
     }
   }
   for (const PoolBlock& w : drop) pool_release(w);
-  if (!drop.empty()) (void)hipSetDevice(device);
+  if (!drop.empty()) cleanup(hipSetDevice(device), "hipSetDevice(after the cache's release)");
 }
 
 // Free every idle block of `device` (-1: of every device).
@@ -341,7 +389,7 @@ static hipError_t pool_malloc(int device, size_t bytes, hipStream_t s, void** p,
   if (e == hipErrorOutOfMemory) {
     (void)hipGetLastError();
     if (pool_drain(device) > 0) {
-      (void)hipSetDevice(device);
+      cleanup(hipSetDevice(device), "hipSetDevice(after draining the cache)");
       e = hipMalloc(p, bytes);
     }
   }
@@ -439,20 +487,10 @@ int check_same(const rnt_buf* a, const rnt_buf* b, const char* what) {
 }
 
 // The MFMA transforms (rnt_mfma.hip) for this context: N = 2^16 on a u32
-// basis (unless RNT_PLANE=0), their tables built on first use.
-bool use_mf(const rnt::Launch& k) {
-  rnt::Tables* t = const_cast<rnt::Tables*>(k.t);
-  if (!rnt::mf_supported(t)) return false;
-  std::lock_guard<std::mutex> g(t->mf_mu);
-  if (!t->mf && !t->mf_failed) {
-    std::string err;
-    if (rnt::mf_build(t, &err) != 0) {
-      fprintf(stderr, "rnsntt: %s; the four-step transforms serve this basis\n", err.c_str());
-      t->mf_failed = true;
-    }
-  }
-  return t->mf != nullptr;
-}
+// basis (unless RNT_PLANE=0).  Their tables are built with the context
+// (rnt_ctx_create), so no op -- none recorded into a graph either -- ever
+// builds them, and a context whose build failed does not exist.
+bool use_mf(const rnt::Launch& k) { return rnt::mf_supported(k.t) && k.t->mf != nullptr; }
 
 // Inverse-transform src (NTT domain) into dst (same layout): dst may equal src.
 int to_coeff_into(const rnt_buf* src, void* dst) {
@@ -478,27 +516,23 @@ int to_coeff_into(const rnt_buf* src, void* dst) {
 }  // namespace
 
 rnt::Tables::~Tables() {
-  (void)hipSetDevice(device);
-  if (stream && stream != own_stream) (void)hipStreamSynchronize(stream);  // a caller's stream
+  cleanup(hipSetDevice(device), "hipSetDevice(context teardown)");
+  if (stream && stream != own_stream)  // a caller's stream
+    cleanup(hipStreamSynchronize(stream), "hipStreamSynchronize(context teardown)");
   if (own_stream) {
-    (void)hipStreamSynchronize(own_stream);
-    (void)hipStreamDestroy(own_stream);
+    cleanup(hipStreamSynchronize(own_stream), "hipStreamSynchronize(context teardown)");
+    cleanup(hipStreamDestroy(own_stream), "hipStreamDestroy(context teardown)");
   }
-  for (auto& e : resc_ext) (void)hipFree(e.second);
-  for (auto& e : crt_cache) (void)hipFree(e.second.dev);
-  (void)hipFree(tw_fwd);
-  (void)hipFree(tw_inv);
-  (void)hipFree(sfft_tw);
-  (void)hipFree(lconst);
-  (void)hipFree(resc);
-  (void)hipFree(resc_p);
-  (void)hipFree(mf);
+  for (auto& e : resc_ext) cleanup(hipFree(e.second), "hipFree(context tables)");
+  for (auto& e : crt_cache) cleanup(hipFree(e.second.dev), "hipFree(context tables)");
+  for (void* p : {tw_fwd, tw_inv, sfft_tw, lconst, resc, resc_p, mf})
+    cleanup(hipFree(p), "hipFree(context tables)");
   if (prof) {
     for (auto& r : prof->pending) {
-      (void)hipEventDestroy(r.a);
-      (void)hipEventDestroy(r.b);
+      cleanup(hipEventDestroy(r.a), "hipEventDestroy(profile)");
+      cleanup(hipEventDestroy(r.b), "hipEventDestroy(profile)");
     }
-    for (hipEvent_t e : prof->pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : prof->pool) cleanup(hipEventDestroy(e), "hipEventDestroy(profile)");
     delete prof;
   }
 }
@@ -716,6 +750,13 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     t->moduli.assign(moduli, moduli + count);
     int rc = wide ? build_tables<uint64_t>(t.get()) : build_tables<uint32_t>(t.get());
     if (rc != RNT_OK) return rc;
+    if (rnt::mf_supported(t.get())) {
+      std::string err;
+      if (const int m = rnt::mf_build(t.get(), &err); m != 0) {
+        (void)hipGetLastError();  // reported here
+        return fail(m == -3 ? RNT_ERR_OUT_OF_MEMORY : RNT_ERR_DEVICE, "%s", err.c_str());
+      }
+    }
     HIP_TRY(hipStreamCreateWithFlags(&t->own_stream, hipStreamNonBlocking), "hipStreamCreate");
     t->stream = t->own_stream;
     rnt_ctx* c = new rnt_ctx;
@@ -737,7 +778,7 @@ static void ctx_retain(const rnt_ctx* ctx) { const_cast<rnt_ctx*>(ctx)->refs.fet
 
 extern "C" int rnt_ctx_destroy(rnt_ctx* ctx) {
   ctx_release(ctx);  // freed once its last buffer is freed too
-  return RNT_OK;
+  return take_deferred();
 }
 
 extern "C" int rnt_ctx_drop_last(const rnt_ctx* ctx, size_t drop_count, rnt_ctx** out) {
@@ -809,7 +850,7 @@ extern "C" int rnt_ctx_set_stream(const rnt_ctx* ctx, void* stream) {
   HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
   hipError_t e = hipEventRecord(ev, t->stream);
   if (e == hipSuccess) e = hipStreamWaitEvent(next, ev, 0);
-  (void)hipEventDestroy(ev);  // released once it completes
+  cleanup(hipEventDestroy(ev), "hipEventDestroy(rnt_ctx_set_stream)");  // released once it completes
   if (e != hipSuccess) return hip_fail(e, "rnt_ctx_set_stream");
   t->stream = next;
   return RNT_OK;
@@ -823,13 +864,17 @@ extern "C" int rnt_ctx_set_stream(const rnt_ctx* ctx, void* stream) {
 // on `last` -- the stream the latest replay was queued on.  A replay on a
 // new stream (after rnt_ctx_set_stream) is first ordered after the previous
 // replays, so `last` covers every replay.
+// `done`: recorded after each replay, so the next replay (on whatever
+// stream the context uses by then) and the blocks' return to the cache wait
+// for it -- no stream handle outlives its use here.
 struct rnt_graph {
   std::shared_ptr<rnt::Tables> t;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   std::vector<OwnedBlock> owned;
   int device = 0;
-  hipStream_t last = nullptr;
+  hipEvent_t done = nullptr;
+  bool replayed = false;
 };
 
 extern "C" int rnt_capture_begin(const rnt_ctx* ctx) {
@@ -876,14 +921,15 @@ extern "C" int rnt_capture_end(const rnt_ctx* ctx, rnt_graph** out) {
     r->graph = g;
     r->owned = std::move(c->owned);
     r->device = c->device;
-    r->last = c->stream;
-    e = hipGraphInstantiate(&r->exec, g, nullptr, nullptr, 0);
+    e = hipEventCreateWithFlags(&r->done, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipGraphInstantiate(&r->exec, g, nullptr, nullptr, 0);
   }
   if (e != hipSuccess) {
     const int dev = c->device;
     const hipStream_t st = c->stream;
     std::vector<OwnedBlock> owned = r ? std::move(r->owned) : std::move(c->owned);
-    if (g) (void)hipGraphDestroy(g);
+    if (g) cleanup(hipGraphDestroy(g), "hipGraphDestroy(failed capture)");
+    if (r && r->done) cleanup(hipEventDestroy(r->done), "hipEventDestroy(failed capture)");
     delete r;
     delete c;
     for (auto& b : owned) pool_give(dev, b.p, b.bytes, st);
@@ -899,29 +945,28 @@ extern "C" int rnt_graph_launch(rnt_graph* g) {
   if (g_capture != nullptr) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_graph_launch while recording");
   HIP_TRY(hipSetDevice(g->device), "hipSetDevice");
   hipStream_t s = g->t->stream;
-  if (g->last != s) {  // order this replay after the ones queued on the old stream
-    hipEvent_t ev = nullptr;
-    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-    hipError_t e = hipEventRecord(ev, g->last);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s, ev, 0);
-    (void)hipEventDestroy(ev);
-    HIP_TRY(e, "hipStreamWaitEvent");
-    g->last = s;
-  }
+  if (int rc = take_deferred()) return rc;
+  // after the previous replay, wherever it was queued (same stream: free)
+  if (g->replayed) HIP_TRY(hipStreamWaitEvent(s, g->done, 0), "hipStreamWaitEvent");
   HIP_TRY(hipGraphLaunch(g->exec, s), "hipGraphLaunch");
+  HIP_TRY(hipEventRecord(g->done, s), "hipEventRecord");
+  g->replayed = true;
   return RNT_OK;
 }
 
 extern "C" int rnt_graph_destroy(rnt_graph* g) {
   if (!g) return RNT_OK;
-  (void)hipSetDevice(g->device);
-  // a replay may still be running: the blocks go back behind an event on
-  // the stream the replays were queued on
-  for (auto& b : g->owned) pool_give(g->device, b.p, b.bytes, g->last);
-  if (g->exec) (void)hipGraphExecDestroy(g->exec);
-  if (g->graph) (void)hipGraphDestroy(g->graph);
+  cleanup(hipSetDevice(g->device), "hipSetDevice(rnt_graph_destroy)");
+  // a replay may still be running: the blocks go back to the cache behind
+  // the context's current stream, made to wait for the last replay first
+  hipStream_t s = g->t->stream;
+  if (g->replayed) cleanup(hipStreamWaitEvent(s, g->done, 0), "hipStreamWaitEvent(rnt_graph_destroy)");
+  for (auto& b : g->owned) pool_give(g->device, b.p, b.bytes, s);
+  if (g->exec) cleanup(hipGraphExecDestroy(g->exec), "hipGraphExecDestroy");
+  if (g->graph) cleanup(hipGraphDestroy(g->graph), "hipGraphDestroy");
+  if (g->done) cleanup(hipEventDestroy(g->done), "hipEventDestroy(rnt_graph_destroy)");
   delete g;
-  return RNT_OK;
+  return take_deferred();
 }
 
 extern "C" int rnt_graph_workspace(const rnt_graph* g, size_t* blocks, size_t* bytes) {
@@ -983,20 +1028,20 @@ extern "C" int rnt_buf_free(rnt_buf* b) {
   if (b->ctx) {
     const int dev = b->ctx->t->device;
     hipStream_t s = b->ctx->t->stream;
-    (void)hipSetDevice(dev);
+    cleanup(hipSetDevice(dev), "hipSetDevice(rnt_buf_free)");
     if (b->owns) pool_give(dev, b->data, b->data_bytes, s);
     pool_give(dev, b->ws, b->ws_bytes, s);
     pool_give(dev, b->stage, b->stage_bytes, s);
   }
   ctx_release(b->ctx);
   delete b;
-  return RNT_OK;
+  return take_deferred();
 }
 
 extern "C" int rnt_pool_trim(int device, size_t* freed_bytes) {
   const size_t f = pool_drain(device);
   if (freed_bytes) *freed_bytes = f;
-  return RNT_OK;
+  return take_deferred();
 }
 
 extern "C" int rnt_buf_wrap(const rnt_ctx* ctx, void* device_ptr, size_t n_polys, int in_ntt,
@@ -1060,8 +1105,8 @@ extern "C" int rnt_upload(rnt_buf* b, const uint64_t* host, size_t n_polys, size
     const size_t ch = (size_t)((bad / n) % b->ctx->L);
     // device data is now partially written; the reference returns Err and
     // builds no polynomial, so zero the buffer to keep it well-defined.
-    (void)hipMemsetAsync(b->data, 0, words * word_bytes(k.t), k.s);
-    (void)hipStreamSynchronize(k.s);
+    cleanup(hipMemsetAsync(b->data, 0, words * word_bytes(k.t), k.s), "hipMemsetAsync(rejected upload)");
+    cleanup(hipStreamSynchronize(k.s), "hipStreamSynchronize(rejected upload)");
     b->in_ntt = 0;
     return fail_fields(RNT_ERR_NON_REDUCED, host[bad], b->ctx->t->moduli[ch],
                        "coefficient %" PRIu64 " is not reduced modulo %" PRIu64, host[bad],
@@ -1551,7 +1596,7 @@ static int sfft_table(const rnt_ctx* ctx, const void** tab) {
     HIP_TRY(hipMalloc(&d, h.size() * sizeof(double)), "hipMalloc(sfft twiddles)");
     const hipError_t e = hipMemcpy(d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
-      (void)hipFree(d);
+      cleanup(hipFree(d), "hipFree(sfft twiddles)");
       return hip_fail(e, "hipMemcpy(sfft twiddles)");
     }
     t->sfft_tw = d;
@@ -2136,9 +2181,11 @@ extern "C" int rnt_profile_read(const rnt_ctx* ctx, const char* kernel, uint64_t
   std::lock_guard<std::mutex> g(t->prof->mu);
   for (auto& r : t->prof->pending) {
     float ms = 0;
-    if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+    if (const hipError_t e = hipEventElapsedTime(&ms, r.a, r.b); e == hipSuccess) {
       t->prof->launches[r.id] += 1;
       t->prof->ms[r.id] += ms;
+    } else {
+      cleanup(e, "hipEventElapsedTime(profile)");
     }
     t->prof->pool.push_back(r.a);
     t->prof->pool.push_back(r.b);
@@ -2146,5 +2193,5 @@ extern "C" int rnt_profile_read(const rnt_ctx* ctx, const char* kernel, uint64_t
   t->prof->pending.clear();
   *launches = t->prof->launches[id];
   *total_ms = t->prof->ms[id];
-  return RNT_OK;
+  return take_deferred();
 }

@@ -109,11 +109,8 @@ struct Tables {
   void* sfft_tw = nullptr;
   struct Prof* prof = nullptr;  // per-kernel event timing (rnt_profile_*)
   // MFMA transform tables (rnt_mfma.hip: matrix operands, compensations and
-  // twists per limb), built on first use where mf_supported(); mf_failed:
-  // the build failed (reported once; the four-step transforms serve)
-  std::mutex mf_mu;
+  // twists per limb), built by rnt_ctx_create where mf_supported()
   void* mf = nullptr;
-  bool mf_failed = false;
   ~Tables();
 };
 

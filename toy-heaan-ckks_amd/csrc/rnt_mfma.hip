@@ -131,10 +131,6 @@ __device__ __forceinline__ void bst(v4i x, Rsrc r, uint32_t voff, uint32_t soff)
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
 }
 
-__device__ __forceinline__ v4i mfma(v4i a, v4i b, v4i c) {
-  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
-}
-
 // Output word from its four digit sums: r = T 2^-32 mod q (signed
 // representative), + 0x80808080 when WK (then ^ K32 packs it).
 template <bool WK>
@@ -176,27 +172,50 @@ __device__ __forceinline__ void pin4(uint32_t a, uint32_t b, uint32_t c, uint32_
 __device__ __forceinline__ uint32_t pk_canon(uint32_t x) { return (x + 0x40808080u) ^ K32; }  // x - 2^30, packed
 __device__ __forceinline__ uint32_t canon(int32_t r, int32_t q) { return (uint32_t)(r + ((r >> 31) & q)); }
 
-// One MFMA tile: the four digit planes of a 16 x 16 x 64 product.
-// DA: the data is the A operand (the matrix the B operand).
-template <bool DA, bool W16 = false>
+// One MFMA tile: the four digit planes of a 16 x 16 x 64 product, hazard-safe
+// by construction ("MFMA hazards"; tools/isa_check.py checks
+// the built code).  The four MFMAs are one asm statement:
+//  - the results are early-clobber outputs, so no MFMA's D overlaps any
+//    operand of the tile (hipcc's own allocation let the last MFMA's D take
+//    the data operand's registers, wholly or in part: the case that gave
+//    k_mf_tensor its wrong words, r04);
+//  - `s_nop 1` first: the operands hipcc's VALU just wrote are 2 wait
+//    states old when the first MFMA reads them (hipcc pads nothing it cannot
+//    see, and an asm MFMA is invisible to it);
+//  - `s_nop 7` last: nothing after the statement -- hipcc's code or an asm
+//    writer such as mont()'s v_mad_i64_i32, which its hazard recognizer does
+//    not check against MFMAs -- reads or writes a register any of the four
+//    MFMAs reads or writes until 8 wait states after the last one issued,
+//    the XDL write -> VALU access window of a 4-pass MFMA on gfx950 (the
+//    window hipcc itself pads for its own reads of a builtin MFMA's D).
+// DA: the data is the A operand (the matrix the B operand).  HC: the first
+// digit plane accumulates onto c0 (otherwise the inline constant 0).
+template <bool DA, bool HC>
 __device__ __forceinline__ void tile(v4i (&D)[4], const v4i (&M)[4], v4i dat, v4i c0) {
-  const v4i z = {0, 0, 0, 0};
-#pragma unroll
-  for (int a = 0; a < 4; ++a) D[a] = DA ? mfma(dat, M[a], a == 0 ? c0 : z) : mfma(M[a], dat, a == 0 ? c0 : z);
-  // W16: 16 more wait states than the compiler counts before anything
-  // touches the tile's registers.  k_mf_tensor needs them: without, the
-  // first result register of lanes 12..15 of a pass's last tile came out
-  // wrong now and then (16-300 words per 2^26 on the full-output stress,
-  // tools/tensor_stress2.py), where its register allocation lets an MFMA's
-  // destination partly overlap its B operand and the next VALU write lands
-  // on that operand after the compiler's 6 wait states.  The standalone
-  // transforms measured clean without them (tools/ntt_stress.py, 12288
-  // planes) and keep their speed.
-  if constexpr (W16) {
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_nop 7\n\ts_nop 7");
-    __builtin_amdgcn_sched_barrier(0);
-  }
+#define RNT_MF4(A0, B0, A1, B1, A2, B2, A3, B3, C0)                                  \
+  "s_nop 1\n\t"                                                                      \
+  "v_mfma_i32_16x16x64_i8 %0, " A0 ", " B0 ", " C0 "\n\t"                            \
+  "v_mfma_i32_16x16x64_i8 %1, " A1 ", " B1 ", 0\n\t"                                 \
+  "v_mfma_i32_16x16x64_i8 %2, " A2 ", " B2 ", 0\n\t"                                 \
+  "v_mfma_i32_16x16x64_i8 %3, " A3 ", " B3 ", 0\n\t"                                 \
+  "s_nop 7"
+  if constexpr (DA && HC)
+    asm volatile(RNT_MF4("%4", "%5", "%4", "%6", "%4", "%7", "%4", "%8", "%9")
+                 : "=&v"(D[0]), "=&v"(D[1]), "=&v"(D[2]), "=&v"(D[3])
+                 : "v"(dat), "v"(M[0]), "v"(M[1]), "v"(M[2]), "v"(M[3]), "v"(c0));
+  else if constexpr (DA)
+    asm volatile(RNT_MF4("%4", "%5", "%4", "%6", "%4", "%7", "%4", "%8", "0")
+                 : "=&v"(D[0]), "=&v"(D[1]), "=&v"(D[2]), "=&v"(D[3])
+                 : "v"(dat), "v"(M[0]), "v"(M[1]), "v"(M[2]), "v"(M[3]));
+  else if constexpr (HC)
+    asm volatile(RNT_MF4("%5", "%4", "%6", "%4", "%7", "%4", "%8", "%4", "%9")
+                 : "=&v"(D[0]), "=&v"(D[1]), "=&v"(D[2]), "=&v"(D[3])
+                 : "v"(dat), "v"(M[0]), "v"(M[1]), "v"(M[2]), "v"(M[3]), "v"(c0));
+  else
+    asm volatile(RNT_MF4("%5", "%4", "%6", "%4", "%7", "%4", "%8", "%4", "0")
+                 : "=&v"(D[0]), "=&v"(D[1]), "=&v"(D[2]), "=&v"(D[3])
+                 : "v"(dat), "v"(M[0]), "v"(M[1]), "v"(M[2]), "v"(M[3]));
+#undef RNT_MF4
 }
 // the table of one limb; lo = lam * 16 (the lane's 16 bytes of an operand row)
 __device__ __forceinline__ void load_mat(v4i (&M)[4], Rsrc tab, uint32_t slot, uint32_t lo) {
@@ -374,16 +393,15 @@ __device__ __forceinline__ void swap_q3p2(uint32_t (&x)[64]) {
 // ---- the passes -------------------------------------------------------------
 // pass 0 on P1 chunks [C0, C0 + 8): input canonical (BIAS: packed with the
 // -2^30 shift its compensation undoes) or packed; output packed.
-template <int C0, bool BIAS, bool W16>
+template <int C0, bool BIAS>
 __device__ __forceinline__ void pass_p1(uint32_t (&x1)[64], const v4i (&M)[4], v4i comp, const Mc& m) {
-  const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = C0; c < C0 + 8; ++c) {
     v4i b;
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)(BIAS ? pk_canon(x1[4 * c + i]) : x1[4 * c + i]);
     v4i D[4];
-    tile<false, W16>(D, M, b, BIAS ? comp : z);
+    tile<false, BIAS>(D, M, b, comp);
 #pragma unroll
     for (int i = 0; i < 4; ++i) x1[4 * c + i] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
     pin4(x1[4 * c + 0], x1[4 * c + 1], x1[4 * c + 2], x1[4 * c + 3]);
@@ -392,7 +410,7 @@ __device__ __forceinline__ void pass_p1(uint32_t (&x1)[64], const v4i (&M)[4], v
 }
 // pass 1 (per-wave matrix) on P2 chunks [C0, C0 + 8), then the pass-2 twist
 // (TW: the table in P2 positions).
-template <int C0, bool W16>
+template <int C0>
 __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
                                         const Mc& m) {
   const v4i z = {0, 0, 0, 0};
@@ -405,7 +423,7 @@ __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], R
     // tile-ahead prefetch measured 4 more spilled registers)
     const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 16u);
     v4i D[4];
-    tile<false, W16>(D, M, b, z);
+    tile<false, false>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -416,7 +434,6 @@ __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], R
   }
 }
 // pass 2 (F, data as A: P3 -> P4 positions), then the pass-3 twist.
-template <bool W16>
 __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
                                         const Mc& m) {
   const v4i z = {0, 0, 0, 0};
@@ -427,7 +444,7 @@ __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rs
     for (int i = 0; i < 4; ++i) a[i] = (int)x[p3(c, i)];
     const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 1024u);
     v4i D[4];
-    tile<true, W16>(D, M, a, z);
+    tile<true, false>(D, M, a, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -440,7 +457,7 @@ __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rs
 // pass 3 (F, P4 in place): each tile's centred outputs go to EPI(c, r, x)
 // at once (stored, or multiplied into the product), so no 64-bit reduction
 // result stays live beyond its tile.
-template <bool W16, class EPI>
+template <class EPI>
 __device__ __forceinline__ void pass_p4(uint32_t (&x)[64], const v4i (&M)[4], const Mc& m, const EPI& epi) {
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
@@ -449,7 +466,7 @@ __device__ __forceinline__ void pass_p4(uint32_t (&x)[64], const v4i (&M)[4], co
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x[p3(c, i)];
     v4i D[4];
-    tile<false, W16>(D, M, b, z);
+    tile<false, false>(D, M, b, z);
     int32_t r[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -477,7 +494,6 @@ __device__ __forceinline__ v4i stash_get(uint32_t addr, int c) {
 // inverse pass 3 (F^-1, data as A: P4 -> Q3) on the canonical words as
 // loaded (biased here, comp undoes it), then its twist; packed output.
 // tv: tile 0's twists (each tile loads the next one's).
-template <bool W16>
 __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v4i comp, v4i tv, Rsrc tab,
                                          uint32_t tvo, uint32_t tso, const Mc& m, uint32_t* lds, const Th& h) {
 #pragma unroll
@@ -487,7 +503,7 @@ __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v
     for (int i = 0; i < 4; ++i) a[i] = (int)pk_canon(x[p3(c, i)]);
     const v4i tn = c + 1 < 16 ? bld(tab, tvo, tso + (uint32_t)(c + 1) * 1024u) : tv;
     v4i D[4];
-    tile<true, W16>(D, M, a, comp);
+    tile<true, true>(D, M, a, comp);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -502,7 +518,6 @@ __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v
   }
 }
 // inverse pass 2 (F^-1 in Q3), then its twist; packed output.
-template <bool W16>
 __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rsrc tab, uint32_t tvo, uint32_t tso,
                                          const Mc& m, uint32_t* lds, const Th& h) {
   const v4i z = {0, 0, 0, 0};
@@ -517,7 +532,7 @@ __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], R
     }
     const v4i tv = bld(tab, tvo, tso + (uint32_t)c * 64u);
     v4i D[4];
-    tile<false, W16>(D, M, b, z);
+    tile<false, false>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -529,7 +544,7 @@ __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], R
 }
 // inverse pass 1 (per-wave matrix) on P2 chunks [C0, C0 + 8) at q2 slots
 // (the registers after the Q3 -> P2 swap); packed output.
-template <int C0, bool W16>
+template <int C0>
 __device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], const Mc& m) {
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
@@ -538,7 +553,7 @@ __device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], c
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x[q2(c, i)];
     v4i D[4];
-    tile<false, W16>(D, M, b, z);
+    tile<false, false>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       x[q2(c, i)] = (uint32_t)recomb<true>(D[0][i], D[1][i], D[2][i], D[3][i], m) ^ K32;
@@ -548,7 +563,7 @@ __device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], c
 }
 // inverse pass 0 on P1 chunks [C0, C0 + 8): canonical output; every four
 // chunks (the words of one 16-byte store per register) go to memory at once.
-template <int C0, bool W16>
+template <int C0>
 __device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], const Mc& m, Rsrc dst,
                                          const Th& h);
 
@@ -574,7 +589,7 @@ __device__ __forceinline__ void load_p1(uint32_t (&x1)[64], Rsrc src, const Th& 
       for (int e = 0; e < 4; ++e) x1[4 * (4 * hc + e) + i] = (uint32_t)v[e];
     }
 }
-template <int C0, bool W16>
+template <int C0>
 __device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], const Mc& m, Rsrc dst,
                                          const Th& h) {
   const v4i z = {0, 0, 0, 0};
@@ -584,7 +599,7 @@ __device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], 
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x1[4 * c + i];
     v4i D[4];
-    tile<false, W16>(D, M, b, z);
+    tile<false, false>(D, M, b, z);
 #pragma unroll
     for (int i = 0; i < 4; ++i) x1[4 * c + i] = canon(recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m), m.q);
     if ((c & 3) == 3) {
@@ -634,7 +649,7 @@ __device__ __forceinline__ Tabs tabs_of(const void* mf, const LimbConst<uint32_t
 struct NoEpi {
   __device__ void operator()(int, const int32_t (&)[4], uint32_t (&)[64]) const {}
 };
-template <bool SYNC1, bool W16 = false, class EPI = NoEpi>
+template <bool SYNC1, class EPI = NoEpi>
 __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds, const Th& h, const Tabs& T,
                                     const EPI& epi = EPI{}) {
   // the first pass's operands load ahead of the plane (cache hits, needed
@@ -646,12 +661,12 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   const v4i comp = bld(T.tab, lo, (uint32_t)kCompF1 * 16u);
   uint32_t x1[64];
   load_p1(x1, src, h);
-  pass_p1<0, true, W16>(x1, M, comp, m);
+  pass_p1<0, true>(x1, M, comp, m);
   if constexpr (SYNC1) __syncthreads();
   uint32_t wb[4], rb[4];
   p1_bases(wb, h);
   x_write_p1<0>(x1, lds, wb);
-  pass_p1<8, true, W16>(x1, M, comp, m);
+  pass_p1<8, true>(x1, M, comp, m);
   __syncthreads();
   p2_bases(rb, h);
   x_read_p2<0>(x2, lds, rb);
@@ -660,16 +675,16 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   x_write_p1<1>(x1, lds, wb);
   load_mat(M, T.tab, S_F2 + h.w, lo);
   const uint32_t t3v = h.g() * 256u, t3s = (uint32_t)(kTw3f + h.w * 64) * 16u;
-  pass_p2<0, W16>(x2, M, T.tab, t3v, t3s, m);
+  pass_p2<0>(x2, M, T.tab, t3v, t3s, m);
   __syncthreads();
   p2_bases(rb, h);
   x_read_p2<1>(x2, lds, rb);
-  pass_p2<8, W16>(x2, M, T.tab, t3v, t3s, m);
+  pass_p2<8>(x2, M, T.tab, t3v, t3s, m);
   swap_p2p3(x2);
   load_mat(M, T.tab, S_F3, lo);
-  pass_p3<W16>(x2, M, T.tab, lo, (uint32_t)(kTw4f + h.w * 1024) * 16u, m);
+  pass_p3(x2, M, T.tab, lo, (uint32_t)(kTw4f + h.w * 1024) * 16u, m);
   load_mat(M, T.tab, S_F4, lo);
-  pass_p4<W16>(x2, M, m, epi);
+  pass_p4(x2, M, m, epi);
 }
 
 // The inverse in place: the NTT-domain plane (device order, P4 positions)
@@ -681,7 +696,7 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
 // barriers, which it passes once it has used (so read) every word it loaded.
 // LOAD = false: the plane is already in x2 (P4 positions, canonical), as a
 // forward pass's epilogue left it; the LDS may still be read by other waves.
-template <bool LOAD, bool W16 = false>
+template <bool LOAD>
 __device__ __forceinline__ void inv_x(uint32_t (&x2)[64], Rsrc pr, uint32_t* lds, const Th& h, const Tabs& T) {
   const Mc& m = T.m;
   const uint32_t lo = h.lam() * 16u;
@@ -700,18 +715,18 @@ __device__ __forceinline__ void inv_x(uint32_t (&x2)[64], Rsrc pr, uint32_t* lds
   } else {
     __syncthreads();  // ipass_p4's stash reuses the LDS of the last exchange
   }
-  ipass_p4<W16>(x2, M, comp, tv0, T.tab, lo, t4s, m, lds, h);
+  ipass_p4(x2, M, comp, tv0, T.tab, lo, t4s, m, lds, h);
   load_mat(M, T.tab, S_I3, lo);
-  ipass_p3<W16>(x2, M, T.tab, h.g() * 16u, (uint32_t)(kTw3i + h.w * 64) * 16u, m, lds, h);
+  ipass_p3(x2, M, T.tab, h.g() * 16u, (uint32_t)(kTw3i + h.w * 64) * 16u, m, lds, h);
   swap_q3p2(x2);
   load_mat(M, T.tab, S_I2 + h.w, lo);
   uint32_t wb[4], rb[4];
   uint32_t x1[64];
-  ipass_p2<0, W16>(x2, M, m);
+  ipass_p2<0>(x2, M, m);
   __syncthreads();  // other waves may still read the LDS (the last forward exchange)
   p2_bases(rb, h);
   x_write_p2<0>(x2, lds, rb);
-  ipass_p2<8, W16>(x2, M, m);
+  ipass_p2<8>(x2, M, m);
   __syncthreads();
   p1_bases(wb, h);
   x_read_p1<0>(x1, lds, wb);
@@ -719,11 +734,11 @@ __device__ __forceinline__ void inv_x(uint32_t (&x2)[64], Rsrc pr, uint32_t* lds
   p2_bases(rb, h);
   x_write_p2<1>(x2, lds, rb);
   load_mat(M, T.tab, S_I1, lo);
-  ipass_p1<0, W16>(x1, M, m, pr, h);
+  ipass_p1<0>(x1, M, m, pr, h);
   __syncthreads();
   p1_bases(wb, h);
   x_read_p1<1>(x1, lds, wb);
-  ipass_p1<8, W16>(x1, M, m, pr, h);
+  ipass_p1<8>(x1, M, m, pr, h);
 }
 __device__ __forceinline__ void inv(Rsrc pr, uint32_t* lds, const Th& h, const Tabs& T) {
   uint32_t x2[64];
@@ -800,9 +815,8 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
   }
   const Rsrc R0 = rsrc(d0 + oo, kN * 4u), R1 = rsrc(d1 + oo, kN * 4u), R2 = rsrc(d2 + oo, kN * 4u);
   const Rsrc RS = rsrc(scratch + so, kN * 4u);
-  // Every transform runs with W16 (tile): the extra MFMA wait states this
-  // kernel's register allocation needs.  The lane offset is computed once
-  // per kernel, and the epilogues' products are plain C++.
+  // The lane offset is computed once per kernel, and the epilogues'
+  // products are plain C++.
   const uint32_t pl = p4_lane(h);
   auto canon4 = [q](const int32_t (&r)[4]) {
     return v4i{(int)canon(r[0], (int32_t)q), (int)canon(r[1], (int32_t)q), (int)canon(r[2], (int32_t)q),
@@ -816,13 +830,13 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
   };
   const uint32_t rm = lc.rmod, rmp = lc.rmod_p;
   uint32_t x[64];
-  fwd<false, true>(x, rsrc(c0 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  fwd<false>(x, rsrc(c0 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     bst(canon4(r), R1, pl, p4_soff(h, cc));
   });
-  fwd<true, true>(x, rsrc(c1 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  fwd<true>(x, rsrc(c1 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     bst(canon4(r), RS, pl, p4_soff(h, cc));
   });
-  fwd<true, true>(x, rsrc(c0p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  fwd<true>(x, rsrc(c0p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     const v4i a0 = bld(R1, pl, p4_soff(h, cc)), a1 = bld(RS, pl, p4_soff(h, cc));
     const v4i b = canon4(r);
     v4i o0, t;
@@ -834,7 +848,7 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
     bst(o0, R0, pl, p4_soff(h, cc));
     bst(t, R2, pl, p4_soff(h, cc));
   });
-  fwd<true, true>(x, rsrc(c1p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
+  fwd<true>(x, rsrc(c1p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
     const v4i a0 = bld(R1, pl, p4_soff(h, cc)), a1 = bld(RS, pl, p4_soff(h, cc));
     const v4i t = bld(R2, pl, p4_soff(h, cc));
     const v4i b = canon4(r);
@@ -851,7 +865,7 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
     }
     bst(o1, R1, pl, p4_soff(h, cc));
   });
-  inv_x<false, true>(x, R2, lds, h, T);
+  inv_x<false>(x, R2, lds, h, T);
 }
 
 // ---------------------------------------------------------------------------
@@ -1025,15 +1039,20 @@ int mf_build(Tables* t, std::string* err) {
             t4i[((w * 16 + c) * 64 + lam) * 4 + i] = mr(powmod(itw[32768 + 8 * Ui], (uint64_t)nn, q));
           }
   }
+  // t->mf is set only once the tables are on the device: a failed build
+  // leaves no half-built table behind
   const size_t bytes = all.size() * sizeof(int32_t);
-  if (hipMalloc(&t->mf, bytes) != hipSuccess) {
-    *err = "hipMalloc(MFMA tables)";
+  void* dev = nullptr;
+  if (hipError_t e = hipMalloc(&dev, bytes); e != hipSuccess) {
+    *err = std::string("hipMalloc(MFMA tables): ") + hipGetErrorString(e);
+    return -3;
+  }
+  if (hipError_t e = hipMemcpy(dev, all.data(), bytes, hipMemcpyHostToDevice); e != hipSuccess) {
+    (void)hipFree(dev);
+    *err = std::string("hipMemcpy(MFMA tables): ") + hipGetErrorString(e);
     return -2;
   }
-  if (hipMemcpy(t->mf, all.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) {
-    *err = "hipMemcpy(MFMA tables)";
-    return -2;
-  }
+  t->mf = dev;
   return 0;
 }
 

@@ -292,9 +292,6 @@ def _device_of(t):
 # ---------------------------------------------------------------------------
 
 
-_TORCH_ALLOC_LOCK = threading.Lock()
-
-
 class GpuBackend:
     """Compute on this rank's GPU through librnsntt; exchange buffers are
     torch tensors wrapped as non-owning RnsPoly views (rnt_buf_wrap), so the
@@ -319,11 +316,28 @@ class GpuBackend:
         return self.torch.int32 if max(basis.moduli()) < (1 << 31) else self.torch.int64
 
     def shared_stream(self, basis):
-        """The library context's HIP stream as a torch stream.  Run the
-        pipeline under ``with torch.cuda.stream(backend.shared_stream(basis))``
-        and torch's allocations, copies and collective joins are ordered with
-        the library's kernels on one stream, so the host syncs below drop out."""
-        return self.torch.cuda.ExternalStream(basis.stream(), device=self.tdev)
+        """One stream for torch and the library context.  Run the pipeline
+        under ``with torch.cuda.stream(backend.shared_stream(basis))`` and
+        torch's allocations, copies and collective joins are ordered with the
+        library's kernels on one stream, so the host syncs below drop out.
+
+        The stream is torch's (from its stream pool, alive until the process
+        ends) and the context is moved onto it (rnt_ctx_set_stream), not the
+        other way round: torch keeps stream handles beyond any tensor it
+        hands out -- a block allocated under the stream, or marked with
+        record_stream, has an event recorded on that stream when it is
+        freed, whenever that is.  Wrapping the context's own stream
+        (ExternalStream, r04) let those events land on a stream the
+        context's teardown had destroyed; with 8 thread ranks dropping their
+        contexts while gathered tensors were still alive, that took the
+        process down inside torch's allocator (the r04 segfault in
+        torch.empty)."""
+        s = getattr(basis, "_torch_stream", None)
+        if s is None or basis.stream() != s.cuda_stream:
+            s = self.torch.cuda.Stream(device=self.tdev)
+            basis.set_stream(s.cuda_stream)
+            basis._torch_stream = s
+        return s
 
     def _same_stream(self, basis) -> bool:
         return self.torch.cuda.current_stream(self.tdev).cuda_stream == basis.stream()
@@ -341,21 +355,15 @@ class GpuBackend:
             basis.sync()
 
     def _empty(self, basis, shape):
-        # one allocation at a time across the backends of a process: thread
-        # ranks (ThreadComm) share one device, and concurrent torch.empty
-        # calls beside the library's own allocations in other threads took a
-        # pytest process down once (a segfault inside torch.empty,
-        # tests/test_gpu_sharded_configs.py, r04)
-        with _TORCH_ALLOC_LOCK:
-            try:
-                return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
-            except self.torch.cuda.OutOfMemoryError:
-                # the library's device block cache may hold the memory torch needs
-                from . import pool_trim
+        try:
+            return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
+        except self.torch.cuda.OutOfMemoryError:
+            # the library's device block cache may hold the memory torch needs
+            from . import pool_trim
 
-                if pool_trim(self.device) == 0:
-                    raise
-                return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
+            if pool_trim(self.device) == 0:
+                raise
+            return self.torch.empty(shape, dtype=self._dtype(basis), device=self.tdev)
 
     def _wrap(self, basis, t, B, ntt=False):
         from . import RnsPoly
