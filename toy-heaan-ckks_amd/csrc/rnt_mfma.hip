@@ -67,6 +67,27 @@
 #include "rnt_device.hpp"
 
 namespace rnt {
+
+// Phase timeline of k_mf_ntt (measurement build only: MF_ONLY=1
+// tools/build_variant.sh mftrace -DRNT_MF_TRACE; tools/mf_trace.py): lane 0
+// of every wave of the first kMfTraceWg workgroups stamps the 100 MHz
+// real-time counter at each phase boundary (waiting only for the stamp's own
+// scalar read, so the plane's loads and stores stay asynchronous).
+#ifdef RNT_MF_TRACE
+constexpr int kMfTraceWg = 4096, kMfTraceSt = 16;
+__device__ uint64_t g_mf_trace[kMfTraceWg * 16 * kMfTraceSt];
+#define MF_STAMP(S)                                                                                  \
+  do {                                                                                               \
+    const uint32_t wg_ = blockIdx.x + blockIdx.y * gridDim.x;                                        \
+    if ((threadIdx.x & 63u) == 0 && wg_ < (uint32_t)kMfTraceWg)                                      \
+      g_mf_trace[(wg_ * 16 + (threadIdx.x >> 6)) * kMfTraceSt + (S)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define MF_STAMP(S) \
+  do {              \
+  } while (0)
+#endif
+
 namespace mf {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -661,30 +682,40 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   const v4i comp = bld(T.tab, lo, (uint32_t)kCompF1 * 16u);
   uint32_t x1[64];
   load_p1(x1, src, h);
+  MF_STAMP(1);
   pass_p1<0, true>(x1, M, comp, m);
+  MF_STAMP(2);
   if constexpr (SYNC1) __syncthreads();
   uint32_t wb[4], rb[4];
   p1_bases(wb, h);
   x_write_p1<0>(x1, lds, wb);
   pass_p1<8, true>(x1, M, comp, m);
+  MF_STAMP(3);
   __syncthreads();
+  MF_STAMP(4);
   p2_bases(rb, h);
   x_read_p2<0>(x2, lds, rb);
   __syncthreads();
+  MF_STAMP(5);
   p1_bases(wb, h);
   x_write_p1<1>(x1, lds, wb);
   load_mat(M, T.tab, S_F2 + h.w, lo);
   const uint32_t t3v = h.g() * 256u, t3s = (uint32_t)(kTw3f + h.w * 64) * 16u;
   pass_p2<0>(x2, M, T.tab, t3v, t3s, m);
+  MF_STAMP(6);
   __syncthreads();
+  MF_STAMP(7);
   p2_bases(rb, h);
   x_read_p2<1>(x2, lds, rb);
   pass_p2<8>(x2, M, T.tab, t3v, t3s, m);
+  MF_STAMP(8);
   swap_p2p3(x2);
   load_mat(M, T.tab, S_F3, lo);
   pass_p3(x2, M, T.tab, lo, (uint32_t)(kTw4f + h.w * 1024) * 16u, m);
+  MF_STAMP(9);
   load_mat(M, T.tab, S_F4, lo);
   pass_p4(x2, M, m, epi);
+  MF_STAMP(10);
 }
 
 // The inverse in place: the NTT-domain plane (device order, P4 positions)
@@ -758,6 +789,7 @@ k_mf_ntt(uint32_t* __restrict__ data, const void* __restrict__ mft, const LimbCo
   uint32_t* lds = (uint32_t*)smem_raw;
   const Th h(threadIdx.x);
   const uint32_t poly = blockIdx.x, l = blockIdx.y;
+  MF_STAMP(0);
   uint32_t* p = data + (uint64_t)l * ls + (uint64_t)poly * kN;
   const Tabs T = tabs_of(mft, lcs[l], l);
   const Rsrc pr = rsrc(p, kN * 4u);
@@ -773,6 +805,10 @@ k_mf_ntt(uint32_t* __restrict__ data, const void* __restrict__ mft, const LimbCo
   } else {
     inv(pr, lds, h, T);
   }
+#ifdef RNT_MF_TRACE
+  __builtin_amdgcn_s_waitcnt(0);  // the plane's stores have left the CU
+  MF_STAMP(11);
+#endif
 }
 
 // The ciphertext tensor product at N = 2^16 (rnt_ct_tensor and the
@@ -1079,6 +1115,12 @@ hipError_t launch_mf_tensor(const Launch& k, void* d0, void* d1, void* d2, uint6
   void* args[] = {&d0, &d1, &d2, &ols, &c0, &c1, &c0p, &c1p, &ils, &scratch, &slots, &mft, &lcs};
   return hipLaunchKernel(fn, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), args, mf::kLdsBytes, k.s);
 }
+
+#ifdef RNT_MF_TRACE
+extern "C" __attribute__((visibility("default"))) int rnt_debug_mf_trace(uint64_t* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mf_trace), sizeof(g_mf_trace));
+}
+#endif
 
 hipError_t launch_mf_ntt(const Launch& k, int inverse, void* data, uint64_t ls) {
   if (k.B == 0 || k.L == 0) return hipSuccess;
