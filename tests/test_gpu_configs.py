@@ -189,6 +189,33 @@ def test_metric_batch_1024_sampled_pairs(gpu, monkeypatch, plane):
         assert np.array_equal(a.channels_of(p)[0], c.channels_of(p)[0]), p
 
 
+def test_metric_product_full_output_vs_four_step(gpu, monkeypatch):
+    """Every word of 128 pairs x 16 limbs (2048 planes: the CU-indexed
+    scratch slots of k_plane_fused_slots) of the default product against the
+    four-step kernels' (RNT_PLANE=0), on the same device-drawn operands and
+    on all-(q-1) operands (the lazy-with-carry butterflies' largest sums)."""
+    rn = gpu
+    n, L, B = 1 << 16, 16, 128
+    mod = rn.generate_primes(31, L, n)
+    q = np.array(mod, dtype=np.uint64)[:, None]
+    out = {}
+    for plane in (None, "0"):
+        if plane is None:
+            monkeypatch.delenv("RNT_PLANE", raising=False)
+        else:
+            monkeypatch.setenv("RNT_PLANE", plane)
+        Bd = rn.RnsBasis(mod, n)
+        drng = rn.DeviceRng(77)
+        a = rn.RnsPoly.sample_uniform(Bd, drng, B)
+        b = rn.RnsPoly.sample_uniform(Bd, drng, B)
+        out[plane] = (a * b).channels_batch()
+        full = rn.RnsPoly.from_channels(np.broadcast_to(q - 1, (2, L, n)), Bd)
+        out[(plane, "full")] = (full * full).channels_batch()
+        del a, b, full, Bd
+    assert int((out[None] != out["0"]).sum()) == 0
+    assert np.array_equal(out[(None, "full")], out[("0", "full")])
+
+
 @pytest.mark.parametrize("jg", [3, 16])
 def test_decomposition_groups(gpu, monkeypatch, jg):
     """RNT_DEC_JG fixes the key-switch decomposition's target limbs per
