@@ -57,6 +57,44 @@ def test_error_payloads_match_reference_variants(gpu):
     assert e.value.kind == "ChannelCountMismatch" and e.value.fields == {"expected": 2, "actual": 1}
 
 
+def _hip_runtime():
+    """The process's one HIP runtime (the copy torch loaded, which the
+    library binds too), by its mapped path: loading another copy by name
+    would start a second runtime."""
+    import ctypes
+
+    with open("/proc/self/maps") as f:
+        paths = {ln.split()[-1] for ln in f if "libamdhip64" in ln and "/" in ln}
+    assert len(paths) == 1, paths
+    rt = ctypes.CDLL(paths.pop())
+    rt.hipSetDevice.argtypes = [ctypes.c_int]
+    rt.hipSetDevice.restype = ctypes.c_int
+    rt.hipGetLastError.restype = ctypes.c_int
+    return rt
+
+
+def test_pending_hip_error_is_reported_not_dropped(gpu):
+    """A HIP error some other code left in the runtime's last-error slot is
+    reported by the next launch as DeviceError, pending from an earlier
+    call (r04's clear_stale_error dropped it), and the launch after that
+    runs normally."""
+    rn = gpu
+    n, L = 1 << 12, 2
+    mod = rn.generate_primes(31, L, n)
+    Bd = rn.RnsBasis(mod, n)
+    x = rn.RnsPoly.from_channels(_rand(np.random.default_rng(9), mod, n, 2), Bd)
+    x.to_ntt_domain()
+    Bd.sync()
+    rt = _hip_runtime()
+    assert rt.hipSetDevice(4096) != 0  # invalid device: the slot now holds the error
+    with pytest.raises(rn.RnsNttError) as e:
+        x.to_coeff_domain()
+    assert e.value.kind == "DeviceError" and "pending" in str(e.value), str(e.value)
+    assert rt.hipGetLastError() == 0  # reported, so no longer pending
+    x.to_coeff_domain()  # the op itself was never launched: x is still NTT-domain
+    assert not x.is_ntt_domain()
+
+
 def test_freed_blocks_are_reused_without_host_wait(gpu):
     """Buffers freed while their kernels may still be queued hand their
     blocks to later allocations; results and zero-initialisation stay exact.

@@ -16,7 +16,7 @@
 # Usage: tools/sanitize.sh [log]   (default log: profiles/r03_sanitizer_cpu.log)
 set -euo pipefail
 cd "$(dirname "$0")/.."
-LOG=${1:-profiles/r04_sanitizer_cpu.log}
+LOG=${1:-profiles/r05_sanitizer_cpu.log}
 LLVM=/opt/rocm/lib/llvm/bin
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 OUT=build/asan
