@@ -13,7 +13,7 @@
 # preloaded into python.  One runtime for both libraries (clang's), so the
 # oracle is built with the ROCm clang rather than gcc here.
 #
-# Usage: tools/sanitize.sh [log]   (default log: profiles/r03_sanitizer_cpu.log)
+# Usage: tools/sanitize.sh [log]   (default log: profiles/r05_sanitizer_cpu.log)
 set -euo pipefail
 cd "$(dirname "$0")/.."
 LOG=${1:-profiles/r05_sanitizer_cpu.log}
