@@ -60,3 +60,17 @@ def test_unwaited_load_register_is_flagged_and_waited_one_is_not():
 def test_lds_dma_has_no_register_destination():
     lines = ["global_load_lds_dword v20, s[44:45]", "v_mov_b32_e32 v20, 0"]
     assert kinds(lines) == []
+
+
+def test_overwrite_of_wide_store_data_is_flagged():
+    # the r05 pattern: a 128-bit buffer store with an SGPR soffset, its data
+    # register rewritten by the next instruction (hipcc pads nothing here)
+    st = "buffer_store_dwordx4 v[0:3], v94, s[20:23], s78 offen"
+    assert kinds([st, "v_mov_b32_e32 v0, v126"]) == ["S1"]
+    assert kinds([st, "v_writelane_b32 v1, s78, 39"]) == ["S1"]
+    assert kinds([st, "s_nop 0", "v_mov_b32_e32 v3, v126"]) == ["S1"]
+    # two wait states on, or a register outside the data, or 64-bit data: clean
+    assert kinds([st, "s_nop 1", "v_mov_b32_e32 v0, v126"]) == []
+    assert kinds([st, "v_mov_b32_e32 v4, v126"]) == []
+    assert kinds(["buffer_store_dwordx2 v[0:1], v94, s[20:23], s78 offen", "v_mov_b32_e32 v0, v126"]) == []
+    assert kinds(["global_store_dwordx4 v[8:9], v[0:3], off", "v_mov_b32_e32 v2, 0"]) == ["S1"]

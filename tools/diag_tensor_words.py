@@ -1,8 +1,15 @@
 """Locate wrong words of the matrix-core tensor (default path) against the
-four-step tensor (RNT_PLANE=0) and test what they equal: for each wrong d1
-word, is it the forward transform of c0 or c1 (the values the tensor's
-first two epilogues stored at that address), or the four-step value?
-Diagnostic only (r05 split-load experiment)."""
+four-step tensor (RNT_PLANE=0) and infer which operand went wrong.
+
+With a0 = c0^, a1 = c1^, b3 = c0'^, b4 = c1'^ (device-order forward
+transforms), the tensor computes d0 = a0 b3 R^-1, d1 = (a1 b3 + a0 b4) R^-1
+and d2 = INTT(a1 b4) (R = 2^32).  A wrong a1 shows as
+  da1 = (d1_bad - d1) R / b3 = (NTT(d2_bad) - NTT(d2)) / b4   (mod q);
+the script prints both quotients at each wrong d1 word, the implied bad a1
+value and whether that value occurs anywhere among the batch's c0^..c1'^
+words of the same limb (misrouted data) or among the last 2^20 words of any
+operand.  Diagnostic only (the r05 split-load / persistent-forward
+experiments, profiles/r05/ab_mf_ntt_split_load.txt)."""
 import os
 import sys
 
@@ -15,6 +22,15 @@ import rns_ntt as rn  # noqa: E402
 N, L = 1 << 16, 16
 Bc = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 mod = rn.generate_primes(31, L, N)
+R = 1 << 32
+
+
+def ntt_dev(Bd, ch):
+    t = rn.RnsPoly.from_channels(ch, Bd)
+    t.to_ntt_domain()
+    return t.channels()
+
+
 for r in range(int(sys.argv[1]) if len(sys.argv) > 1 else 2):
     outs, fw = {}, {}
     for plane in ("1", "0"):
@@ -24,20 +40,29 @@ for r in range(int(sys.argv[1]) if len(sys.argv) > 1 else 2):
         c = [rn.RnsPoly.sample_uniform(Bd, drng, Bc) for _ in range(4)]
         if plane == "0":
             for k in range(4):
-                t = rn.RnsPoly.from_channels(c[k].channels(), Bd)
-                t.to_ntt_domain()
-                fw[k] = t.channels()
+                fw[k] = ntt_dev(Bd, c[k].channels())
         d = rn.ct_tensor(*c)
         outs[plane] = [x.channels() for x in d]
-        del c, d, Bd
-    a, b = outs["1"][1], outs["0"][1]
-    bad = np.argwhere(a != b)
-    print(f"round {r}: d1 {len(bad)} wrong words, d0 {int((outs['1'][0] != outs['0'][0]).sum())}, "
-          f"d2 {int((outs['1'][2] != outs['0'][2]).sum())}", flush=True)
-    for p, l, x in bad[:24]:
-        got = int(a[p, l, x])
-        tags = [f"c{k}^" for k in range(4) if int(fw[k][p, l, x]) == got]
-        # which other position of the same plane holds the wrong value
-        same = np.flatnonzero(b[p, l] == got)[:3].tolist()
-        print(f"  p{p} l{l} pos {x:5d} = {x:#06x}: got {got} want {int(b[p, l, x])} equals {tags} "
-              f"four-step d1 at {same}", flush=True)
+        if plane == "0":
+            xx = {"1": ntt_dev(Bd, outs["1"][2]), "0": ntt_dev(Bd, outs["0"][2])}
+        del c, d
+    bad = np.argwhere(outs["1"][1] != outs["0"][1])
+    bad2 = {(int(p), int(l)) for p, l in np.argwhere((outs["1"][2] != outs["0"][2]).any(axis=2))}
+    bad1 = {(int(p), int(l)) for p, l, _ in bad}
+    print(f"round {r}: d1 {len(bad)} wrong words in {len(bad1)} planes; d0 "
+          f"{int((outs['1'][0] != outs['0'][0]).sum())} wrong; d2 wrong in {len(bad2)} planes, "
+          f"same planes as d1: {bad1 == bad2}", flush=True)
+    for p, l, x in bad[:40]:
+        q = int(mod[l])
+        d1b, d1g = int(outs["1"][1][p, l, x]), int(outs["0"][1][p, l, x])
+        b3, b4 = int(fw[2][p, l, x]), int(fw[3][p, l, x])
+        e1 = (d1b - d1g) * R * pow(b3, -1, q) % q
+        e2 = (int(xx["1"][p, l, x]) - int(xx["0"][p, l, x])) * pow(b4, -1, q) % q
+        a1 = int(fw[1][p, l, x])
+        a1b = (a1 + e1) % q
+        where = []
+        for k in range(4):
+            hit = np.argwhere(fw[k][:, l, :] == a1b)
+            where += [f"c{k}^[p{int(a)}][{int(b)}]" for a, b in hit[:3]]
+        print(f"  p{p} l{l} pos {x:5d} = {x:#06x}: da1 via d1 {e1} via d2 {e2} equal {e1 == e2}; "
+              f"bad a1 {a1b} (a1 {a1}) found at {where}", flush=True)

@@ -16,7 +16,15 @@ disassembly of every kernel in the given objects and reports, per kernel:
   L1  a VGPR that a DS / VMEM / scratch load writes, read or written before
       the s_waitcnt that retires that load (the loads of inline asm are not
       in hipcc's bookkeeping; a compiler copy of such a register before the
-      wait reads stale data).
+      wait reads stale data);
+  S1  a VGPR holding the data of a VMEM store of more than 64 bits written
+      by a VALU instruction fewer than W_ST wait states after the store
+      issued.  The store reads
+      its data after issue; hipcc pads this hazard only for stores without
+      an SGPR soffset (LLVM's createsVALUHazard), but on gfx950 a buffer
+      store with an SGPR soffset lost single lanes of its data to a
+      `v_mov_b32` into the data register 0-1 states later (r05: k_mf_tensor's
+      scratch-slot words, profiles/r05/ab_mf_ntt_split_load.txt).
 
 Wait states: one per instruction, N+1 for `s_nop N` (the ISA's counting,
 and LLVM's).  v_mfma_i32_16x16x64_i8 is a 4-pass XDL op on gfx950 (16
@@ -43,6 +51,7 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 W_D = 8     # MFMA D -> any access (4-pass XDL on gfx950: passes + 4)
 W_SRC = 8   # MFMA A/B/C -> overwrite (in flight until its D is written)
 W_IN = 2    # VALU/memory write -> MFMA operand read
+W_ST = 2    # VMEM store (> 64-bit data) -> overwrite of its data VGPRs
 
 REG = re.compile(r"^([vas])(?:(\d+)|\[(\d+):(\d+)\])$")
 
@@ -180,19 +189,21 @@ class State:
 
     def __init__(self):
         self.mfmas = []        # dict(end, dst, srcs, text)
+        self.stores = []       # dict(end, data, text): wide VMEM stores still reading their data
         self.alts = [[]]       # per incoming path: un-waited ops (kind, regs, text, is_smem)
         self.last_write = {}   # reg -> counter after the write
 
     def copy(self):
         t = State()
         t.mfmas = [dict(f) for f in self.mfmas]
+        t.stores = [dict(f) for f in self.stores]
         t.alts = [list(a) for a in self.alts]
         t.last_write = dict(self.last_write)
         return t
 
     def shifted(self, delta):
         t = self.copy()
-        for f in t.mfmas:
+        for f in t.mfmas + t.stores:
             f["end"] += delta
         t.last_write = {r: v + delta for r, v in t.last_write.items()}
         return t
@@ -200,6 +211,8 @@ class State:
     def merge(self, o):
         seen = {(f["text"], f["end"]) for f in self.mfmas}
         self.mfmas += [f for f in o.mfmas if (f["text"], f["end"]) not in seen]
+        seen = {(f["text"], f["end"]) for f in self.stores}
+        self.stores += [f for f in o.stores if (f["text"], f["end"]) not in seen]
         for a in o.alts:
             if a not in self.alts:
                 self.alts.append(list(a))
@@ -296,7 +309,18 @@ def check_kernel(body, func_addr, verbose=False):
                 findings.append(("M1", idx, f"{txt}  touches D {sorted(f['dst'] & (d | u))[:4]} of `{f['text']}` after {dist} states"))
             if (f["srcs"] & d) and dist < W_SRC:
                 findings.append(("M2", idx, f"{txt}  overwrites operand {sorted(f['srcs'] & d)[:4]} of `{f['text']}` after {dist} states"))
+        # ---- S1: data registers of a wide store still being read
+        if mn.startswith("v_"):  # VALU writers (a load's data returns far later)
+            for f in st.stores:
+                if (f["data"] & d) and since - f["end"] < W_ST:
+                    findings.append(("S1", idx, f"{txt}  overwrites data {sorted(f['data'] & d)[:4]} of `{f['text']}` "
+                                                f"after {since - f['end']} states"))
         since += ws
+        if sk == "vm":
+            data = vset(ops[:1]) if mn.startswith("buffer_store") else vset(ops[1:2])
+            if len(data) > 2:
+                st.stores.append({"end": since, "data": data, "text": txt.split("//")[0].strip()})
+        st.stores = [f for f in st.stores if since - f["end"] < W_ST]
         if is_mf:
             st.mfmas.append({"end": since, "dst": vset(ops[:1]), "srcs": vset(ops[1:]), "text": txt.split("//")[0].strip()})
         st.mfmas = [f for f in st.mfmas if since - f["end"] < 64]

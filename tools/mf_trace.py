@@ -47,6 +47,10 @@ def main():
     assert lib.rnt_debug_mf_trace(buf.ctypes.data) == 0
     tr = buf.reshape(WG, WV, ST).astype(np.int64)[:, :, : len(PH) + 1]
     nwg = min(B * L, WG)
+    # the persistent forward (one workgroup per CU) stamps only its first
+    # gridDim.x slots, each with the workgroup's last plane
+    stamped = (tr[:nwg] != 0).all(axis=(1, 2))
+    nwg = int(stamped.sum()) if not stamped.all() else nwg
     w = tr[:nwg]
     first, last = w.min(axis=1), w.max(axis=1)
     t0 = first[:, :1]
