@@ -150,6 +150,13 @@ __device__ __forceinline__ void bst(v4i x, Rsrc r, uint32_t voff, uint32_t soff)
   v[2] = (uint32_t)x[2];
   v[3] = (uint32_t)x[3];
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+  // The store reads its 128-bit data after issue, and hipcc pads nothing
+  // for a buffer store with an SGPR soffset: a VALU write of the data
+  // registers 0-1 wait states later lost single lanes of stored words (r05,
+  // profiles/r05/ab_mf_ntt_split_load.txt).  The empty statement keeps v
+  // live, 2 wait states on, so nothing overwrites it sooner
+  // (tools/isa_check.py rule S1 checks every kernel).
+  asm volatile("s_nop 1" ::"v"(v));
 }
 
 // Output word from its four digit sums: r = T 2^-32 mod q (signed
@@ -412,6 +419,27 @@ __device__ __forceinline__ void swap_q3p2(uint32_t (&x)[64]) {
 }
 
 // ---- the passes -------------------------------------------------------------
+// Progress priority (RNT_MF_PRIO) over the forward's barrier-free stretch
+// (pass 1's second half, pass 2, pass 3: tiles p = 0..39): a wave lowers its
+// priority 3 -> 0 as it advances, so a wave that fell behind outranks the
+// ones ahead of it and the sixteen finish together instead of in age order
+// (r05 trace: the last wave of a CU ended 11 us after the first).
+#ifndef RNT_MF_PRIO
+#define RNT_MF_PRIO 1
+#endif
+template <int P>
+__device__ __forceinline__ void prio_at() {
+  if constexpr (RNT_MF_PRIO && P % 10 == 0 && P < 40) __builtin_amdgcn_s_setprio(3 - P / 10);
+}
+// the same over the inverse's first stretch (its passes 3, 2 and the first
+// half of 1: 40 tiles between the plane load and the first exchange)
+#ifndef RNT_MF_IPRIO
+#define RNT_MF_IPRIO 1
+#endif
+template <int P>
+__device__ __forceinline__ void iprio_at() {
+  if constexpr (RNT_MF_IPRIO && P % 10 == 0 && P < 40) __builtin_amdgcn_s_setprio(3 - P / 10);
+}
 // pass 0 on P1 chunks [C0, C0 + 8): input canonical (BIAS: packed with the
 // -2^30 shift its compensation undoes) or packed; output packed.
 template <int C0, bool BIAS>
@@ -437,6 +465,9 @@ __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], R
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = C0; c < C0 + 8; ++c) {
+    if constexpr (C0 == 8) {
+      if (c == 8) prio_at<0>();
+    }
     v4i b;
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x2[4 * c + i];
@@ -460,6 +491,8 @@ __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rs
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
+    if (c == 2) prio_at<10>();
+    if (c == 12) prio_at<20>();
     v4i a;
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = (int)x[p3(c, i)];
@@ -483,6 +516,7 @@ __device__ __forceinline__ void pass_p4(uint32_t (&x)[64], const v4i (&M)[4], co
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
+    if (c == 6) prio_at<30>();
     v4i b;
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x[p3(c, i)];
@@ -519,6 +553,8 @@ __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v
                                          uint32_t tvo, uint32_t tso, const Mc& m, uint32_t* lds, const Th& h) {
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
+    if (c == 0) iprio_at<0>();
+    if (c == 10) iprio_at<10>();
     v4i a;
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = (int)pk_canon(x[p3(c, i)]);
@@ -544,6 +580,8 @@ __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], R
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
+    if (c == 4) iprio_at<20>();
+    if (c == 14) iprio_at<30>();
     v4i b;
     if (c < kStash) {
       b = stash_get(stash_addr(lds, h), c);
