@@ -39,12 +39,15 @@ def short(kname):
     if m:
         return ("whole_fwd", "whole_inv", "whole_mul")[int(m.group(2))]
     m = re.search(r"(k_\w+)<([^>]*)>", kname)
-    if not m or not m.group(2).startswith("unsigned int"):
+    if not m or not m.group(2).startswith(("unsigned int", "unsigned long")):
         return None
     fn, targs = m.group(1), [t.strip() for t in m.group(2).split(",")]
+    sfx = "_u64" if targs[0] == "unsigned long" else ""  # the wide-prime (u64) kernels apart
     if fn == "k_row":
-        return ROW_MODES.get(targs[1])
-    return FN.get(fn)
+        r = ROW_MODES.get(targs[1])
+    else:
+        r = FN.get(fn)
+    return r + sfx if r else None
 
 
 def counters(d):
