@@ -337,6 +337,26 @@ __device__ __forceinline__ void plane_x1_round(uint32_t (&x)[64], uint32_t* lds,
 }
 __device__ __forceinline__ void plane_sync() { __syncthreads(); }
 
+// Progress priority (RNT_PLANE_PRIO) over the product's two long
+// barrier-free stretches (a's pass C, the a^ store, b's load and pass A;
+// then b's pass C, the block products, the inverse's gs C and X2): a wave
+// lowers its priority 3 -> 0 as it advances through a stretch, so a wave
+// that fell behind outranks those ahead of it and the sixteen reach the
+// next barrier together instead of in age order (as k_mf_ntt's passes,
+// profiles/r05/ab_mf_ntt_prio.txt).
+#ifndef RNT_PLANE_PRIO
+#define RNT_PLANE_PRIO 1
+#endif
+template <int P>
+__device__ __forceinline__ void plane_prio() {
+  if constexpr (RNT_PLANE_PRIO) __builtin_amdgcn_s_setprio(P);
+}
+// RNT_PLANE_PRIO >= 2: also over the tail (gs A at 3, the stores at 0)
+template <int P>
+__device__ __forceinline__ void plane_prio_tail() {
+  if constexpr (RNT_PLANE_PRIO >= 2) __builtin_amdgcn_s_setprio(P);
+}
+
 // Lane bit 5 <-> L1 register bit 5 and lane bit 4 <-> register bit 4
 // (self-inverse; the two commute).
 __device__ __forceinline__ void plane_swap54(uint32_t (&x)[64]) {
@@ -466,6 +486,7 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   // register bits only, pass B's (b >= 6) on register and wave bits: both
   // wave-uniform (scalar loads)
   plane_ct<0, 10, 5, 0, kPlaneChA>(x, N, tws, mo);
+  if constexpr (SYNC1) plane_prio<0>();  // b's pass A ends the first stretch
   PLANE_STAMP(K, 2);
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
   // X1 in its two rounds, pass B of round 0's half while round 1 drains
@@ -482,6 +503,7 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   plane_x1_round<true, 1, false>(x, lds, t);
   plane_ct<1, 6, 3, 0, kPlaneChB, 1>(x, N + (wu << 12), tws, mo);
   plane_sync();  // X2's buffers overlap the X1 region
+  plane_prio<3>();
   PLANE_STAMP(K, 4);
   const auto pc = plane_pre<kPreFwd>(tw, N + (t << 6));
   plane_x2<true>(x, lds, t);
@@ -489,6 +511,7 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   after_x2();
   // pass C: bits 5..2 (bits 1..0 are the product's truncated stages)
   plane_ct<2, 0, 5, 2, kPlaneChC>(x, N + (t << 6), pc, mo);
+  plane_prio<2>();
   PLANE_STAMP(K, 6);
 }
 
@@ -505,6 +528,7 @@ __device__ __forceinline__ void plane_inv_tail(uint32_t (&x)[64], uint32_t* lds,
   plane_gs<2, 0, 2, 5, kPlaneChC, false>(x, n0 + (t << 6), gsrc, mo, Fold<uint32_t>{});
   PLANE_STAMP(K, 8);
   plane_x2<false>(x, lds, t);
+  plane_prio<0>();
   PLANE_STAMP(K, 9);
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
   // gs B of round 0's half, X1 round 0 written while gs B of the other half runs
@@ -521,7 +545,9 @@ __device__ __forceinline__ void plane_inv_tail(uint32_t (&x)[64], uint32_t* lds,
   plane_x1_round<false, 1, false>(x, lds, t);
   plane_sync();
   PLANE_STAMP(K, 11);
+  plane_prio_tail<3>();
   plane_gs<0, 10, 0, 5, kPlaneChA, true>(x, n0, itws, mo, F);
+  plane_prio_tail<0>();
   PLANE_STAMP(K, 12);
   const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc((void*)c, 0, (int)(4u << 16), 0x00020000);
 #pragma unroll
@@ -572,6 +598,7 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
 #pragma unroll
     for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = cc[e];
   }
+  plane_prio<1>();
   PLANE_STAMP(K, 7);
   plane_inv_tail<K>(x, lds, t, c, itw, gpre, mo, Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p}, trace_id);
 }
@@ -612,6 +639,7 @@ __device__ __forceinline__ void plane_fused_one(uint32_t* __restrict__ c, const 
   PLANE_STAMP(0, 1);
   plane_fwd<0, false>(x, lds, t, tw, mo, trace_id);
   plane_store_hat(HatBuf(ah), x, t, lds);
+  plane_prio<1>();
   PLANE_STAMP(0, 7);
   PLANE_STAMP(1, 0);
   plane_load(x, b + off, t);
