@@ -111,6 +111,10 @@ constexpr int kLimb = kTw3i + 1024;
 // LDS: the P1 <-> P2 exchange (128 KiB: half a plane per round) and the
 // inverse's stash (10 KiB a wave); one workgroup per CU either way
 constexpr size_t kLdsBytes = (size_t)160 * 1024;
+// k_mf_tensor indexes its scratch slot by the CU it runs on: that needs one
+// resident workgroup per CU, which more than half the CU's 160 KiB of LDS
+// guarantees (as k_plane_fused_slots asserts for its own slots)
+static_assert(kLdsBytes > 80 * 1024, "one workgroup per CU");
 
 // Registers of a P3 / P4 / Q3 chunk (c, i) after the P2 -> P3 swap, as
 // physical slots of the P2 numbering 4c + i (see the header).
