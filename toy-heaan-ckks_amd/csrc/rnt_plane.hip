@@ -345,7 +345,7 @@ __device__ __forceinline__ void plane_sync() { __syncthreads(); }
 // next barrier together instead of in age order (as k_mf_ntt's passes,
 // profiles/r05/ab_mf_ntt_prio.txt).
 #ifndef RNT_PLANE_PRIO
-#define RNT_PLANE_PRIO 1
+#define RNT_PLANE_PRIO 2
 #endif
 template <int P>
 __device__ __forceinline__ void plane_prio() {
