@@ -351,6 +351,27 @@ template <int P>
 __device__ __forceinline__ void plane_prio() {
   if constexpr (RNT_PLANE_PRIO) __builtin_amdgcn_s_setprio(P);
 }
+// Level at each step point of the stretches, per RNT_PLANE_PRIO_VAR (A/B
+// of where the steps fall): F4 after X1, F5 before pass C, F6 after it,
+// H after the a^ store, A1 after b's pass A, P7 after the products (P8: at
+// their middle), G8 after gs C, G9 after the inverse X2.
+#ifndef RNT_PLANE_PRIO_VAR
+#define RNT_PLANE_PRIO_VAR 2
+#endif
+enum PrioPt { F4, F5, F6, H, A1, P8, P7, G8, G9, B0, NPT };
+template <int PT>
+__device__ __forceinline__ void plane_prio_pt() {
+  constexpr int tab[6][NPT] = {
+      {3, -1, 2, 1, 0, -1, 1, -1, 0, -1},   // 0: the first steps (r05 run 1)
+      {3, 2, 1, 0, 0, -1, 0, -1, 0, -1},    // 1: early
+      {3, -1, -1, 2, 0, -1, 2, 1, 0, -1},   // 2: late (adopted)
+      {3, -1, 2, 1, 0, 1, -1, 0, 0, -1},    // 3: the products split
+      {3, -1, -1, 2, 0, -1, -1, 2, 1, 0},   // 4: later in b's stretch
+      {3, -1, -1, -1, 1, -1, 2, 1, 0, -1},  // 5: later in a's stretch
+  };
+  constexpr int v = tab[RNT_PLANE_PRIO_VAR][PT];
+  if constexpr (RNT_PLANE_PRIO && v >= 0) __builtin_amdgcn_s_setprio(v);
+}
 // RNT_PLANE_PRIO >= 2: also over the tail (gs A at 3, the stores at 0)
 template <int P>
 __device__ __forceinline__ void plane_prio_tail() {
@@ -486,7 +507,7 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   // register bits only, pass B's (b >= 6) on register and wave bits: both
   // wave-uniform (scalar loads)
   plane_ct<0, 10, 5, 0, kPlaneChA>(x, N, tws, mo);
-  if constexpr (SYNC1) plane_prio<0>();  // b's pass A ends the first stretch
+  if constexpr (SYNC1) plane_prio_pt<A1>();  // b's pass A ends the first stretch
   PLANE_STAMP(K, 2);
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
   // X1 in its two rounds, pass B of round 0's half while round 1 drains
@@ -503,15 +524,16 @@ __device__ __forceinline__ void plane_fwd(uint32_t (&x)[64], uint32_t* lds, uint
   plane_x1_round<true, 1, false>(x, lds, t);
   plane_ct<1, 6, 3, 0, kPlaneChB, 1>(x, N + (wu << 12), tws, mo);
   plane_sync();  // X2's buffers overlap the X1 region
-  plane_prio<3>();
+  plane_prio_pt<F4>();
   PLANE_STAMP(K, 4);
   const auto pc = plane_pre<kPreFwd>(tw, N + (t << 6));
   plane_x2<true>(x, lds, t);
   PLANE_STAMP(K, 5);
   after_x2();
+  plane_prio_pt<F5>();
   // pass C: bits 5..2 (bits 1..0 are the product's truncated stages)
   plane_ct<2, 0, 5, 2, kPlaneChC>(x, N + (t << 6), pc, mo);
-  plane_prio<2>();
+  plane_prio_pt<F6>();
   PLANE_STAMP(K, 6);
 }
 
@@ -526,13 +548,15 @@ __device__ __forceinline__ void plane_inv_tail(uint32_t (&x)[64], uint32_t* lds,
   const uint32_t n0 = 1u << 16;
   const TwScalar<uint32_t> itws{(const RNT_CONST_AS Tw<uint32_t>*)itw};
   plane_gs<2, 0, 2, 5, kPlaneChC, false>(x, n0 + (t << 6), gsrc, mo, Fold<uint32_t>{});
+  plane_prio_pt<G8>();
   PLANE_STAMP(K, 8);
   plane_x2<false>(x, lds, t);
-  plane_prio<0>();
+  plane_prio_pt<G9>();
   PLANE_STAMP(K, 9);
   const uint32_t wu = __builtin_amdgcn_readfirstlane(t >> 6);
   // gs B of round 0's half, X1 round 0 written while gs B of the other half runs
   plane_gs<1, 6, 0, 3, kPlaneChB, false, 0>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
+  plane_prio_pt<B0>();
   plane_sync();  // other waves may still be in their X2
   plane_x1_round<false, 0, true>(x, lds, t);
   plane_gs<1, 6, 0, 3, kPlaneChB, false, 1>(x, n0 + (wu << 12), itws, mo, Fold<uint32_t>{});
@@ -591,6 +615,7 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
     const uint32_t aa[4] = {av.x, av.y, av.z, av.w};
     const uint32_t bb[4] = {x[plane::slot2(4 * kk)], x[plane::slot2(4 * kk + 1)], x[plane::slot2(4 * kk + 2)],
                             x[plane::slot2(4 * kk + 3)]};
+    if (kk == 8) plane_prio_pt<P8>();
     const uint32_t zeta = (kk & 1) ? lc.q - w.w : w.w;
     const uint32_t zeta_p = (kk & 1) ? ~w.p : w.p;
     uint32_t cc[4];
@@ -598,7 +623,7 @@ __device__ __forceinline__ void plane_mul_tail(uint32_t (&x)[64], uint32_t* lds,
 #pragma unroll
     for (int e = 0; e < 4; ++e) x[plane::slot2(4 * kk + e)] = cc[e];
   }
-  plane_prio<1>();
+  plane_prio_pt<P7>();
   PLANE_STAMP(K, 7);
   plane_inv_tail<K>(x, lds, t, c, itw, gpre, mo, Fold<uint32_t>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p}, trace_id);
 }
@@ -639,7 +664,7 @@ __device__ __forceinline__ void plane_fused_one(uint32_t* __restrict__ c, const 
   PLANE_STAMP(0, 1);
   plane_fwd<0, false>(x, lds, t, tw, mo, trace_id);
   plane_store_hat(HatBuf(ah), x, t, lds);
-  plane_prio<1>();
+  plane_prio_pt<H>();
   PLANE_STAMP(0, 7);
   PLANE_STAMP(1, 0);
   plane_load(x, b + off, t);
