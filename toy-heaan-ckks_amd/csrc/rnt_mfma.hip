@@ -431,18 +431,25 @@ __device__ __forceinline__ void swap_q3p2(uint32_t (&x)[64]) {
 #ifndef RNT_MF_PRIO
 #define RNT_MF_PRIO 1
 #endif
-template <int P>
-__device__ __forceinline__ void prio_at() {
-  if constexpr (RNT_MF_PRIO && P % 10 == 0 && P < 40) __builtin_amdgcn_s_setprio(3 - P / 10);
-}
 // the same over the inverse's first stretch (its passes 3, 2 and the first
 // half of 1: 40 tiles between the plane load and the first exchange)
 #ifndef RNT_MF_IPRIO
 #define RNT_MF_IPRIO 1
 #endif
-template <int P>
-__device__ __forceinline__ void iprio_at() {
-  if constexpr (RNT_MF_IPRIO && P % 10 == 0 && P < 40) __builtin_amdgcn_s_setprio(3 - P / 10);
+// RNT_MF_PRIO_VAR: where the steps fall (0: tiles 0, 10, 20, 30; 1: 0, 20,
+// 28, 34); p is a constant after unrolling
+#ifndef RNT_MF_PRIO_VAR
+#define RNT_MF_PRIO_VAR 0
+#endif
+template <bool ON>
+__device__ __forceinline__ void mf_prio(int p) {
+  if constexpr (ON) {
+    constexpr int s1 = RNT_MF_PRIO_VAR ? 20 : 10, s2 = RNT_MF_PRIO_VAR ? 28 : 20, s3 = RNT_MF_PRIO_VAR ? 34 : 30;
+    if (p == 0) __builtin_amdgcn_s_setprio(3);
+    if (p == s1) __builtin_amdgcn_s_setprio(2);
+    if (p == s2) __builtin_amdgcn_s_setprio(1);
+    if (p == s3) __builtin_amdgcn_s_setprio(0);
+  }
 }
 // pass 0 on P1 chunks [C0, C0 + 8): input canonical (BIAS: packed with the
 // -2^30 shift its compensation undoes) or packed; output packed.
@@ -469,9 +476,7 @@ __device__ __forceinline__ void pass_p2(uint32_t (&x2)[64], const v4i (&M)[4], R
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = C0; c < C0 + 8; ++c) {
-    if constexpr (C0 == 8) {
-      if (c == 8) prio_at<0>();
-    }
+    if constexpr (C0 == 8) mf_prio<RNT_MF_PRIO != 0>(c - 8);
     v4i b;
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x2[4 * c + i];
@@ -495,8 +500,7 @@ __device__ __forceinline__ void pass_p3(uint32_t (&x)[64], const v4i (&M)[4], Rs
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
-    if (c == 2) prio_at<10>();
-    if (c == 12) prio_at<20>();
+    mf_prio<RNT_MF_PRIO != 0>(8 + c);
     v4i a;
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = (int)x[p3(c, i)];
@@ -520,7 +524,7 @@ __device__ __forceinline__ void pass_p4(uint32_t (&x)[64], const v4i (&M)[4], co
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
-    if (c == 6) prio_at<30>();
+    mf_prio<RNT_MF_PRIO != 0>(24 + c);
     v4i b;
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x[p3(c, i)];
@@ -557,8 +561,7 @@ __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v
                                          uint32_t tvo, uint32_t tso, const Mc& m, uint32_t* lds, const Th& h) {
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
-    if (c == 0) iprio_at<0>();
-    if (c == 10) iprio_at<10>();
+    mf_prio<RNT_MF_IPRIO != 0>(c);
     v4i a;
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = (int)pk_canon(x[p3(c, i)]);
@@ -584,8 +587,7 @@ __device__ __forceinline__ void ipass_p3(uint32_t (&x)[64], const v4i (&M)[4], R
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = 0; c < 16; ++c) {
-    if (c == 4) iprio_at<20>();
-    if (c == 14) iprio_at<30>();
+    mf_prio<RNT_MF_IPRIO != 0>(16 + c);
     v4i b;
     if (c < kStash) {
       b = stash_get(stash_addr(lds, h), c);
@@ -612,6 +614,7 @@ __device__ __forceinline__ void ipass_p2(uint32_t (&x)[64], const v4i (&M)[4], c
   const v4i z = {0, 0, 0, 0};
 #pragma unroll
   for (int c = C0; c < C0 + 8; ++c) {
+    if constexpr (C0 == 0) mf_prio<RNT_MF_IPRIO != 0>(32 + c);
     v4i b;
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = (int)x[q2(c, i)];
