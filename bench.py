@@ -50,6 +50,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table); ~6.3 TB/s
 # 2.4 GHz maximum clock: 1024 * 64 * 2.4e9 / 29.9 = 5.26e12 butterflies/s.
 VALU_BFLY_CYCLES = 3 * 4.1 + 8 * 2.2
 VALU_PEAK_BFLY = 1024 * 64 * 2.4e9 / VALU_BFLY_CYCLES
+MFMA_PEAK_I8 = 5.0e15  # dense i8 MFMA ops/s (MI355X_MICROARCH.md: 2x BF16's ~2.5e15 per clock)
 
 
 def log(*a):
@@ -351,7 +352,7 @@ def run_polymul(args, comm, world, rank, local_rank):
     comm.barrier()
     elapsed = comm.max(t1 - t0)
     kernels = {}
-    for k in ("col_fwd", "row_mul", "col_inv", "plane_fused", "whole_mul"):
+    for k in ("col_fwd", "row_mul", "col_inv", "plane_fused", "mf_mul", "whole_mul"):
         cnt, ms = B.profile_read(k)
         if cnt:
             kernels[k] = {"launches": cnt, "avg_ms": ms / cnt, "total_ms": ms}
@@ -406,7 +407,7 @@ def run_polymul(args, comm, world, rank, local_rank):
     op_bytes = 3 * elem * wb
     achieved = op_bytes / (op_ms * 1e-3) / 1e9
     step_bytes = {"col_fwd": 4 * elem * wb, "row_mul": 3 * elem * wb, "col_inv": 2 * elem * wb,
-                  "plane_fused": 3 * elem * wb, "whole_mul": 3 * elem * wb}
+                  "plane_fused": 3 * elem * wb, "mf_mul": 3 * elem * wb, "whole_mul": 3 * elem * wb}
     per_gpu = value / world
     pmc = {k: traffic_for(k, "polymul", batch, args.log_n, Lr) if args.prime_bits == 31 else None
            for k in kernels}
@@ -414,7 +415,8 @@ def run_polymul(args, comm, world, rank, local_rank):
     for k, kv in kernels.items():
         kb = step_bytes.get(k)
         ent = {"avg_ms": kv["avg_ms"], "launches": kv["launches"], "alg_bytes_per_launch": kb,
-               "bound": "valu" if k in ("row_mul", "plane_fused", "whole_mul") else "hbm",
+               "bound": ("power (mfma + valu)" if k == "mf_mul" else
+                         "valu" if k in ("row_mul", "plane_fused", "whole_mul") else "hbm"),
                "pmc_bytes_per_launch": pmc.get(k)}
         if kb:
             ent["hbm_GBs"] = kb / (kv["avg_ms"] * 1e-3) / 1e9
@@ -478,6 +480,18 @@ def run_polymul(args, comm, world, rank, local_rank):
             ia = vi / (kernels["plane_fused"]["avg_ms"] * 1e-3)
             kroof["plane_fused"].update(valu_instr_per_launch_pmc=vi, valu_issue_per_s=ia,
                                         valu_issue_peak=ipeak, valu_issue_frac=ia / ipeak)
+    if "mf_mul" in kernels:
+        # the matrix-core product (k_mf_mul): three transforms
+        # of four radix-16 passes per (poly, limb), each pass 16 tiles x 4
+        # v_mfma_i32_16x16x64_i8 (16 x 16 x 64 MACs) per wave, 16 waves; its
+        # MFMA ops per second against the dense i8 peak (2x the BF16 rate
+        # per clock, MI355X_MICROARCH.md: ~5e15 ops/s).  The kernel runs at
+        # the package power limit, not at either peak.
+        mops = 3 * 4 * 16 * 4 * 16 * (16 * 16 * 64) * 2 * (Lr * batch) * args.steps \
+            / kernels["mf_mul"]["launches"]
+        ma = mops / (kernels["mf_mul"]["avg_ms"] * 1e-3)
+        kroof["mf_mul"].update(mfma_unit="i8 ops/s", mfma_ops_per_launch=mops, mfma_achieved=ma,
+                               mfma_peak=MFMA_PEAK_I8, mfma_frac=ma / MFMA_PEAK_I8)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(mod, n, args.cpu_seconds)

@@ -89,7 +89,8 @@ int rnt_device_count(int* n);
  * returns, for one kernel name ("col_fwd", "row_fwd", "row_inv",
  * "row_mul", "col_inv", "elementwise", "rescale", "automorphism",
  * "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt", "sfft",
- * "sample", "copy"), the
+ * "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd",
+ * "whole_inv", "whole_mul", "ks_whole", "tensor_whole", "mf_tensor", "mf_mul"), the
  * launch count and summed device milliseconds since enabling. */
 int rnt_profile_enable(const rnt_ctx* ctx, int enable);
 int rnt_profile_read(const rnt_ctx* ctx, const char* kernel, uint64_t* launches,

@@ -127,12 +127,18 @@ def test_metric_path_edge_operands(gpu, monkeypatch, plane):
     assert np.array_equal(t.channels(), a.channels())
 
 
-def test_plane_product_matches_oracle(gpu, monkeypatch):
-    """rnt_mul through the whole-plane kernel (k_plane_fused, the default at
-    N = 2^16 on u32 bases), bit-exact against the oracle's poly.rs:307-329
+@pytest.mark.parametrize("mf_mul", [None, "0"])
+def test_plane_product_matches_oracle(gpu, monkeypatch, mf_mul):
+    """rnt_mul through the whole-plane products at N = 2^16 on u32 bases --
+    the default matrix-core one (k_mf_mul) and, with RNT_MF_MUL=0, the VALU
+    one (k_plane_fused) -- bit-exact against the oracle's poly.rs:307-329
     product on random, all-(q-1), zero and negacyclic-monomial operands, and
-    in both in-place forms."""
+    in both in-place forms (out aliasing a, out aliasing b)."""
     monkeypatch.delenv("RNT_PLANE", raising=False)
+    if mf_mul is None:
+        monkeypatch.delenv("RNT_MF_MUL", raising=False)
+    else:
+        monkeypatch.setenv("RNT_MF_MUL", mf_mul)
     rn = gpu
     n, L = 1 << 16, 3
     mod = rn.generate_primes(31, L, n)
@@ -160,16 +166,19 @@ def test_plane_product_matches_oracle(gpu, monkeypatch):
     assert np.array_equal(b2.channels(), got)
 
 
-@pytest.mark.parametrize("plane", [None, "0"])
-def test_metric_batch_1024_sampled_pairs(gpu, monkeypatch, plane):
+@pytest.mark.parametrize("env", [{}, {"RNT_MF_MUL": "0"}, {"RNT_PLANE": "0"}], ids=["mf_mul", "plane_fused", "four_step"])
+def test_metric_batch_1024_sampled_pairs(gpu, monkeypatch, env):
     """The metric's own shape and batch (N = 2^16, L = 16 x 31-bit, 1024
     pairs, operands drawn on the device as in bench.py): eight pairs --
     the first, the last, both sides of the 512 midpoint and four random
     ones -- bit-exact against the oracle's poly.rs:307-329 product, and the
-    same batch through the in-place form (a *= b, out aliasing a); default
-    path (k_plane_fused) and the four-step kernels (RNT_PLANE=0)."""
-    if plane is not None:
-        monkeypatch.setenv("RNT_PLANE", plane)
+    same batch through the in-place form (a *= b, out aliasing a); the
+    default path (k_mf_mul), the VALU whole-plane product (RNT_MF_MUL=0) and
+    the four-step kernels (RNT_PLANE=0)."""
+    monkeypatch.delenv("RNT_MF_MUL", raising=False)
+    monkeypatch.delenv("RNT_PLANE", raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     rn = gpu
     n, L, B = 1 << 16, 16, 1024
     mod = rn.generate_primes(31, L, n)
@@ -189,15 +198,21 @@ def test_metric_batch_1024_sampled_pairs(gpu, monkeypatch, plane):
         assert np.array_equal(a.channels_of(p)[0], c.channels_of(p)[0]), p
 
 
-def test_metric_product_full_output_vs_four_step(gpu, monkeypatch):
+@pytest.mark.parametrize("mf_mul", [None, "0"])
+def test_metric_product_full_output_vs_four_step(gpu, monkeypatch, mf_mul):
     """Every word of 128 pairs x 16 limbs (2048 planes: the CU-indexed
-    scratch slots of k_plane_fused_slots) of the default product against the
-    four-step kernels' (RNT_PLANE=0), on the same device-drawn operands and
-    on all-(q-1) operands (the lazy-with-carry butterflies' largest sums)."""
+    scratch slots) of the whole-plane product -- the default matrix-core one
+    (k_mf_mul) and, with RNT_MF_MUL=0, the VALU one (k_plane_fused_slots) --
+    against the four-step kernels' (RNT_PLANE=0), on the same device-drawn
+    operands and on all-(q-1) operands (the largest sums)."""
     rn = gpu
     n, L, B = 1 << 16, 16, 128
     mod = rn.generate_primes(31, L, n)
     q = np.array(mod, dtype=np.uint64)[:, None]
+    if mf_mul is None:
+        monkeypatch.delenv("RNT_MF_MUL", raising=False)
+    else:
+        monkeypatch.setenv("RNT_MF_MUL", mf_mul)
     out = {}
     for plane in (None, "0"):
         if plane is None:

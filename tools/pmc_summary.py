@@ -31,6 +31,8 @@ def short(kname):
         return "plane_fused"
     if re.search(r"\bk_mf_tensor\(", kname):
         return "mf_tensor"
+    if re.search(r"\bk_mf_mul\(", kname):
+        return "mf_mul"
     if re.search(r"\bk_ks_whole<unsigned int", kname):
         return "ks_whole"
     if re.search(r"\bk_tensor_rows<unsigned (int|long), \d+, true>", kname):

@@ -96,7 +96,7 @@ thread_local Capture* g_capture = nullptr;
 const char* const kKernelNames[rnt::K_COUNT] = {
     "col_fwd", "row_fwd", "row_inv", "row_mul", "col_inv", "elementwise", "rescale",
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
-    "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd", "whole_inv", "whole_mul", "ks_whole", "tensor_whole", "mf_tensor"};
+    "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd", "whole_inv", "whole_mul", "ks_whole", "tensor_whole", "mf_tensor", "mf_mul"};
 
 inline void cleanup(hipError_t e, const char* where);
 hipEvent_t prof_event(rnt::Prof* p) {
@@ -737,6 +737,9 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     // the whole-plane product and MFMA transforms are the default where they
     // apply (N = 2^16, u32); RNT_PLANE=0 keeps the four-step kernels
     t->plane = env_long("RNT_PLANE", 1) != 0 ? 1 : 0;
+    // the product on the matrix-core transforms (k_mf_mul) where they apply;
+    // RNT_MF_MUL=0 keeps the VALU whole-plane product (k_plane_fused_slots)
+    t->mf_mul = env_long("RNT_MF_MUL", 1) != 0 ? 1 : 0;
     {
       const long jg = env_long("RNT_DEC_JG", 0);  // A/B knob: 0 = auto, else 1..1024
       t->dec_jg = (uint32_t)(jg < 0 ? 0 : jg > 1024 ? 1024 : jg);
@@ -1263,8 +1266,12 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
   if (rnt::plane_ok(k.t)) {
     const uint64_t planes = rnt::plane_scratch_planes((uint64_t)k.B * k.L);
     if (int rc = ensure_ws(out, planes * k.t->n * 4)) return rc;
-    LAUNCH(k.t, rnt::K_PLANE_FUSED, rnt::launch_plane_fused(k, out->data, a->data, b->data, out->ws, ls),
-           "plane fused product");
+    if (k.t->mf_mul && use_mf(k))
+      LAUNCH(k.t, rnt::K_MF_MUL, rnt::launch_mf_mul(k, out->data, a->data, b->data, ls, out->ws),
+             "matrix-core product");
+    else
+      LAUNCH(k.t, rnt::K_PLANE_FUSED, rnt::launch_plane_fused(k, out->data, a->data, b->data, out->ws, ls),
+             "plane fused product");
     out->in_ntt = 0;
     return RNT_OK;
   }

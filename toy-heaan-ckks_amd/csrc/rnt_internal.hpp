@@ -82,6 +82,7 @@ struct Tables {
   int wide = 0;            // 0: W = u32, 1: W = u64
   bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path
   int plane = 0;           // the whole-plane kernels where they apply (plane_ok, mf_ok);
+  int mf_mul = 1;          // rnt_mul at N = 2^16 on the matrix-core transforms (RNT_MF_MUL=0: k_plane_fused)
                            // RNT_PLANE=0: the four-step kernels everywhere
   uint32_t dec_jg = 0;     // key-switch decomposition: target limbs per workgroup (0 = auto)
   size_t ks_ws_bytes = (size_t)4096 << 20;  // key-switch scratch cap per chunk (RNT_KS_WS_MB)
@@ -119,7 +120,7 @@ enum KernelId {
   K_COL_FWD, K_ROW_FWD, K_ROW_INV, K_ROW_MUL, K_COL_INV, K_ELEMENTWISE, K_RESCALE,
   K_AUTOMORPHISM, K_KS_DECOMPOSE, K_KS_ROWS, K_TENSOR_ROWS, K_IMPORT, K_EXPORT, K_CRT,
   K_SFFT, K_SAMPLE, K_COPY, K_PLANE_FUSED, K_MF_NTT_FWD, K_MF_NTT_INV, K_WHOLE_FWD, K_WHOLE_INV, K_WHOLE_MUL,
-  K_KS_WHOLE, K_TENSOR_WHOLE, K_MF_TENSOR, K_COUNT
+  K_KS_WHOLE, K_TENSOR_WHOLE, K_MF_TENSOR, K_MF_MUL, K_COUNT
 };
 
 struct Prof {
@@ -219,6 +220,10 @@ hipError_t launch_mf_ntt(const Launch& k, int inverse, void* data, uint64_t ls);
 // planes of N words.
 hipError_t launch_mf_tensor(const Launch& k, void* d0, void* d1, void* d2, uint64_t ols, const void* c0,
                             const void* c1, const void* c0p, const void* c1p, uint64_t ils, void* scratch);
+// The coefficient-domain product c = a b at N = 2^16 on the matrix-core
+// transforms (k_mf_mul, mf_supported bases; in place allowed); scratch:
+// plane_scratch_planes(B L) planes of N words.
+hipError_t launch_mf_mul(const Launch& k, void* c, const void* a, const void* b, uint64_t ls, void* scratch);
 // Whether rnt_mul's row kernel stops its transforms two stages early and
 // multiplies degree-3 residues (u32 canonical bases, row length 2^(4k));
 // its inverse column pass then takes rfold = 2.

@@ -949,6 +949,60 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
   inv_x<false>(x, R2, lds, h, T);
 }
 
+// The coefficient-domain product c = a b at N = 2^16 (rnt_mul, poly.rs:307-329)
+// on the matrix-core transforms, one workgroup per (poly, limb): fwd a -> a^
+// into the CU's scratch slot (k_mf_tensor's indexing); fwd b, whose last
+// pass multiplies each tile by a^ (read back by the same thread) and keeps
+// the exact product in registers; the inverse from there stores c.  c may
+// be a or b: every wave has read its words of both before the exchange
+// barriers that precede the inverse's stores.
+__global__ void __launch_bounds__(mf::kT, 1)
+k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_t ls, uint32_t* __restrict__ scratch,
+         uint32_t slots, const void* __restrict__ mft, const LimbConst<uint32_t>* __restrict__ lcs) {
+  using namespace mf;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  const Th h(threadIdx.x);
+  const uint32_t poly = blockIdx.x, l = blockIdx.y;
+  const uint64_t o = (uint64_t)l * ls + (uint64_t)poly * kN;
+  const LimbConst<uint32_t> lc = lcs[l];
+  const Tabs T = tabs_of(mft, lc, l);
+  const uint32_t q = lc.q, nqi = T.m.nqinv;
+  uint64_t so;
+  if (slots) {
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;          // hwreg(HW_REG_XCC_ID)
+    const uint32_t cu = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8) & 0xffu;  // hwreg(HW_REG_HW_ID)[15:8]
+    so = (uint64_t)((xcc << 8) | cu) << 16;
+  } else {
+    so = (uint64_t)(poly + l * gridDim.x) << 16;
+  }
+  const Rsrc RS = rsrc(scratch + so, kN * 4u);
+  const uint32_t pl = p4_lane(h);
+  const uint32_t rm = lc.rmod, rmp = lc.rmod_p;
+  uint32_t x[64];
+  fwd<false>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+    bst(v4i{(int)canon(r[0], (int32_t)q), (int)canon(r[1], (int32_t)q), (int)canon(r[2], (int32_t)q),
+            (int)canon(r[3], (int32_t)q)},
+        RS, pl, p4_soff(h, cc));
+  });
+  fwd<true>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
+    const v4i ah = bld(RS, pl, p4_soff(h, cc));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // a^ b^ 2^-32 (Montgomery), times 2^32 (Shoup by 2^32 mod q): the exact product
+      const uint32_t bi = canon(r[i], (int32_t)q);
+      const uint64_t t = (uint64_t)(uint32_t)ah[i] * bi;
+      const uint32_t mm = (uint32_t)t * nqi;
+      uint32_t mo = (uint32_t)((t + (uint64_t)mm * q) >> 32);
+      mo = mo >= q ? mo - q : mo;
+      const uint32_t qh = (uint32_t)(((uint64_t)mo * rmp) >> 32);
+      const uint32_t v = mo * rm - qh * q;
+      xx[p3(cc, i)] = v >= q ? v - q : v;
+    }
+  });
+  inv_x<false>(x, rsrc(c + o, kN * 4u), lds, h, T);
+}
+
 // ---------------------------------------------------------------------------
 // host: the per-limb table
 // ---------------------------------------------------------------------------
@@ -1158,6 +1212,19 @@ hipError_t launch_mf_tensor(const Launch& k, void* d0, void* d1, void* d2, uint6
   const void* mft = k.t->mf;
   const LimbConst<uint32_t>* lcs = (const LimbConst<uint32_t>*)k.t->lconst;
   void* args[] = {&d0, &d1, &d2, &ols, &c0, &c1, &c0p, &c1p, &ils, &scratch, &slots, &mft, &lcs};
+  return hipLaunchKernel(fn, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), args, mf::kLdsBytes, k.s);
+}
+
+hipError_t launch_mf_mul(const Launch& k, void* c, const void* a, const void* b, uint64_t ls, void* scratch) {
+  if (k.B == 0 || k.L == 0) return hipSuccess;
+  if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
+  const void* fn = (const void*)k_mf_mul;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mf::kLdsBytes);
+  if (e != hipSuccess) return e;
+  uint32_t slots = (uint64_t)k.B * k.L >= kPlaneSlots ? 1u : 0u;  // plane_scratch_planes
+  const void* mft = k.t->mf;
+  const LimbConst<uint32_t>* lcs = (const LimbConst<uint32_t>*)k.t->lconst;
+  void* args[] = {&c, &a, &b, &ls, &scratch, &slots, &mft, &lcs};
   return hipLaunchKernel(fn, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), args, mf::kLdsBytes, k.s);
 }
 
