@@ -107,7 +107,12 @@ constexpr int kTw3f = kCompI4 + 64;       // [w][g][c], element i: pass 2 twist,
 constexpr int kTw4f = kTw3f + 1024;       // [w][c][lam]: pass 3 twist, P4 positions
 constexpr int kTw4i = kTw4f + 16384;      // [w][c][lam]: inverse pass 3 twist, Q3 positions
 constexpr int kTw3i = kTw4i + 16384;      // [w][c][g]: inverse pass 2 twist, Q3 positions
-constexpr int kLimb = kTw3i + 1024;
+// F4S: F4 times 2^32 (k_mf_mul's fwd(a), so a Montgomery product of its
+// output with b^ is the exact product), a matrix slot past the twists (the
+// offsets before it stay as they were: moving them cost hipcc SGPRs and
+// 170 bytes a lane of spills in k_mf_mul)
+constexpr int S_F4S = (kTw3i + 1024 + 255) / 256;
+constexpr int kLimb = (S_F4S + 1) * 256;
 // LDS: the P1 <-> P2 exchange (128 KiB: half a plane per round) and the
 // inverse's stash (10 KiB a wave); one workgroup per CU either way
 constexpr size_t kLdsBytes = (size_t)160 * 1024;
@@ -715,7 +720,7 @@ __device__ __forceinline__ Tabs tabs_of(const void* mf, const LimbConst<uint32_t
 struct NoEpi {
   __device__ void operator()(int, const int32_t (&)[4], uint32_t (&)[64]) const {}
 };
-template <bool SYNC1, class EPI = NoEpi>
+template <bool SYNC1, int F4 = S_F4, class EPI = NoEpi>
 __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds, const Th& h, const Tabs& T,
                                     const EPI& epi = EPI{}) {
   // the first pass's operands load ahead of the plane (cache hits, needed
@@ -758,7 +763,7 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   load_mat(M, T.tab, S_F3, lo);
   pass_p3(x2, M, T.tab, lo, (uint32_t)(kTw4f + h.w * 1024) * 16u, m);
   MF_STAMP(9);
-  load_mat(M, T.tab, S_F4, lo);
+  load_mat(M, T.tab, F4, lo);
   pass_p4(x2, M, m, epi);
   MF_STAMP(10);
 }
@@ -944,6 +949,7 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
       const uint32_t v = m * rm - qh * q;
       xx[p3(cc, i)] = v >= q ? v - q : v;
     }
+    pin4(xx[p3(cc, 0)], xx[p3(cc, 1)], xx[p3(cc, 2)], xx[p3(cc, 3)]);  // (as in k_mf_mul)
     bst(o1, R1, pl, p4_soff(h, cc));
   });
   inv_x<false>(x, R2, lds, h, T);
@@ -978,9 +984,9 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
   }
   const Rsrc RS = rsrc(scratch + so, kN * 4u);
   const uint32_t pl = p4_lane(h);
-  const uint32_t rm = lc.rmod, rmp = lc.rmod_p;
   uint32_t x[64];
-  fwd<false>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  // a^ 2^32: fwd(a)'s last pass runs on F4 2^32 (slot S_F4S)
+  fwd<false, S_F4S>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     bst(v4i{(int)canon(r[0], (int32_t)q), (int)canon(r[1], (int32_t)q), (int)canon(r[2], (int32_t)q),
             (int)canon(r[3], (int32_t)q)},
         RS, pl, p4_soff(h, cc));
@@ -989,16 +995,17 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
     const v4i ah = bld(RS, pl, p4_soff(h, cc));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      // a^ b^ 2^-32 (Montgomery), times 2^32 (Shoup by 2^32 mod q): the exact product
+      // (a^ 2^32) b^ 2^-32 (Montgomery): the exact product, canonical
       const uint32_t bi = canon(r[i], (int32_t)q);
       const uint64_t t = (uint64_t)(uint32_t)ah[i] * bi;
       const uint32_t mm = (uint32_t)t * nqi;
-      uint32_t mo = (uint32_t)((t + (uint64_t)mm * q) >> 32);
-      mo = mo >= q ? mo - q : mo;
-      const uint32_t qh = (uint32_t)(((uint64_t)mo * rmp) >> 32);
-      const uint32_t v = mo * rm - qh * q;
-      xx[p3(cc, i)] = v >= q ? v - q : v;
+      const uint32_t mo = (uint32_t)((t + (uint64_t)mm * q) >> 32);
+      xx[p3(cc, i)] = mo >= q ? mo - q : mo;
     }
+    // computed here: left free, hipcc sinks each reduction to the inverse's
+    // first use of the word and keeps its 64-bit partial live (232 bytes a
+    // lane of spills)
+    pin4(xx[p3(cc, 0)], xx[p3(cc, 1)], xx[p3(cc, 2)], xx[p3(cc, 3)]);
   });
   inv_x<false>(x, rsrc(c + o, kN * 4u), lds, h, T);
 }
@@ -1117,6 +1124,9 @@ int mf_build(Tables* t, std::string* err) {
     }
     expand(F, q, R, true, 0, slot(S_F3));
     expand(F, q, R, false, 1, slot(S_F4));
+    for (int j = 0; j < 16; ++j)
+      for (int k = 0; k < 16; ++k) W[j][k] = mulmod(F[j][k], R, q);
+    expand(W, q, R, false, 1, slot(S_F4S));
     expand(Fi, q, R, true, 1, slot(S_I4));
     expand(Fi, q, R, false, 1, slot(S_I3));
     for (int k = 0; k < 16; ++k)
