@@ -973,7 +973,7 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
   const uint64_t o = (uint64_t)l * ls + (uint64_t)poly * kN;
   const LimbConst<uint32_t> lc = lcs[l];
   const Tabs T = tabs_of(mft, lc, l);
-  const uint32_t q = lc.q, nqi = T.m.nqinv;
+  const uint32_t q = lc.q;
   uint64_t so;
   if (slots) {
     const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;          // hwreg(HW_REG_XCC_ID)
@@ -986,21 +986,18 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
   const uint32_t pl = p4_lane(h);
   uint32_t x[64];
   // a^ 2^32: fwd(a)'s last pass runs on F4 2^32 (slot S_F4S)
+  // the signed representatives (|r| < q) go to the slot as they are
   fwd<false, S_F4S>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
-    bst(v4i{(int)canon(r[0], (int32_t)q), (int)canon(r[1], (int32_t)q), (int)canon(r[2], (int32_t)q),
-            (int)canon(r[3], (int32_t)q)},
-        RS, pl, p4_soff(h, cc));
+    bst(v4i{r[0], r[1], r[2], r[3]}, RS, pl, p4_soff(h, cc));
   });
   fwd<true>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
     const v4i ah = bld(RS, pl, p4_soff(h, cc));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      // (a^ 2^32) b^ 2^-32 (Montgomery): the exact product, canonical
-      const uint32_t bi = canon(r[i], (int32_t)q);
-      const uint64_t t = (uint64_t)(uint32_t)ah[i] * bi;
-      const uint32_t mm = (uint32_t)t * nqi;
-      const uint32_t mo = (uint32_t)((t + (uint64_t)mm * q) >> 32);
-      xx[p3(cc, i)] = mo >= q ? mo - q : mo;
+      // (a^ 2^32) b^ 2^-32, a signed Montgomery product of two signed
+      // representatives (|a^|, |b^| < q < 2^31: |a b| + |m q| < 2^63, the
+      // result in (-q, q)), made canonical: the exact product
+      xx[p3(cc, i)] = canon(mont<false>(ah[i], r[i], T.m), (int32_t)q);
     }
     // computed here: left free, hipcc sinks each reduction to the inverse's
     // first use of the word and keeps its 64-bit partial live (232 bytes a
