@@ -955,6 +955,11 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
   inv_x<false>(x, R2, lds, h, T);
 }
 
+#ifndef RNT_MF_MUL_LDS
+#define RNT_MF_MUL_LDS 2
+#endif
+constexpr int kMulLdsTiles = RNT_MF_MUL_LDS;  // a^ tiles per wave kept in the LDS (k_mf_mul)
+static_assert(kMulLdsTiles * 16 * 1024 <= 32 * 1024, "beside the 128 KiB exchange region");
 // The coefficient-domain product c = a b at N = 2^16 (rnt_mul, poly.rs:307-329)
 // on the matrix-core transforms, one workgroup per (poly, limb): fwd a -> a^
 // into the CU's scratch slot (k_mf_tensor's indexing); fwd b, whose last
@@ -986,12 +991,18 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
   const uint32_t pl = p4_lane(h);
   uint32_t x[64];
   // a^ 2^32: fwd(a)'s last pass runs on F4 2^32 (slot S_F4S)
-  // the signed representatives (|r| < q) go to the slot as they are
+  // the signed representatives (|r| < q) go to the slot as they are; the
+  // last kMulLdsTiles tiles of each wave stay in the LDS past the exchange
+  // region (free until the inverse's stash), 1 KiB a tile per wave
+  v4i* hat = (v4i*)(lds + (1u << 15)) + h.w * (kMulLdsTiles * 64) + h.lam();
   fwd<false, S_F4S>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
-    bst(v4i{r[0], r[1], r[2], r[3]}, RS, pl, p4_soff(h, cc));
+    if (cc >= 16 - kMulLdsTiles)
+      hat[(cc - (16 - kMulLdsTiles)) * 64] = v4i{r[0], r[1], r[2], r[3]};
+    else
+      bst(v4i{r[0], r[1], r[2], r[3]}, RS, pl, p4_soff(h, cc));
   });
   fwd<true>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
-    const v4i ah = bld(RS, pl, p4_soff(h, cc));
+    const v4i ah = cc >= 16 - kMulLdsTiles ? hat[(cc - (16 - kMulLdsTiles)) * 64] : bld(RS, pl, p4_soff(h, cc));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       // (a^ 2^32) b^ 2^-32, a signed Montgomery product of two signed
