@@ -77,6 +77,28 @@ def uniform(moduli, n, n_polys, seed, stream):
     return out
 
 
+def uniform_poly(moduli, n, p, seed, stream):
+    """[L][N] residues of poly p alone (the draws depend only on the poly,
+    limb and index, so one poly of a large batch is checkable by itself)."""
+    out = np.zeros((len(moduli), n), dtype=np.uint64)
+    idx = np.arange(n, dtype=np.uint64)
+    for li, q in enumerate(moduli):
+        rem = (1 << 64) % q
+        lim = (1 << 64) - rem
+        val = np.zeros(n, dtype=object)
+        todo = np.ones(n, dtype=bool)
+        for att in range(16):
+            v = draw(seed, stream, idx, att, p, li, KIND_UNIFORM)
+            for x in (_lo(v), _hi(v)):
+                ok = todo & ((rem == 0) | (x.astype(object) < lim))
+                val[ok] = x[ok].astype(object) % q
+                todo &= ~ok
+            if not todo.any():
+                break
+        out[li] = val.astype(np.uint64)
+    return out
+
+
 def round_away(z):
     r = np.trunc(z)
     return (r + np.where(np.abs(z - r) >= 0.5, np.sign(z), 0.0)).astype(np.int64)

@@ -33,6 +33,23 @@ def test_uniform_matches_oracle(gpu, log_n, mods):
     assert rng.stream == 8
 
 
+def test_uniform_beyond_one_dispatch_grid(gpu):
+    """1100 polys x 16 limbs at N = 2^16 (1.15e9 words, past the 2^30
+    work-items of the capped grid, so the kernel's grid-stride loop covers
+    the rest; 4096 polys -- 2^32 words -- used to fail the launch): the
+    first and the last poly bit-exact against the oracle."""
+    rn = gpu
+    n, L, B = 1 << 16, 16, 1100
+    mods = rn.generate_primes(31, L, n)
+    basis = rn.RnsBasis(mods, n)
+    rng = rn.DeviceRng(0xC0FFEE)
+    rng.stream = 3
+    x = rn.RnsPoly.sample_uniform(basis, rng, n_polys=B)
+    for p in (0, B - 1):
+        assert np.array_equal(x.channels_of(p)[0], smp.uniform_poly(mods, n, p, 0xC0FFEE, 3)), p
+    del x
+
+
 def test_gaussian_matches_oracle(gpu):
     rn = gpu
     n = 4096

@@ -62,11 +62,8 @@ __device__ __forceinline__ uint64_t lo64(uint4 v) { return (uint64_t)v.x | ((uin
 __device__ __forceinline__ uint64_t hi64(uint4 v) { return (uint64_t)v.z | ((uint64_t)v.w << 32); }
 
 template <class W>
-__global__ void __launch_bounds__(256)
-k_sample_uniform(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, SampleKey s,
-                 uint32_t log_n, uint32_t B, uint64_t total) {
-  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;  // [L][B][N]
+__device__ __forceinline__ void sample_uniform_one(W* __restrict__ out, const LimbConst<W>* __restrict__ lc,
+                                                   SampleKey s, uint32_t log_n, uint32_t B, uint64_t gid) {
   const uint32_t k = (uint32_t)(gid & ((1ull << log_n) - 1));
   const uint64_t lp = gid >> log_n;
   const uint32_t l = (uint32_t)(lp / B);
@@ -84,6 +81,16 @@ k_sample_uniform(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, Sampl
   }
   out[gid] = mag_mod<W>(x, lc[l]);
 }
+template <class W>
+__global__ void __launch_bounds__(256)
+k_sample_uniform(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, SampleKey s,
+                 uint32_t log_n, uint32_t B, uint64_t total) {
+  // [L][B][N]; grid-stride (a dispatch holds fewer than 2^32 work-items,
+  // and 4096 polys x 16 limbs at 2^16 are 2^32 words)
+  for (uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
+       gid += (uint64_t)gridDim.x * blockDim.x)
+    sample_uniform_one<W>(out, lc, s, log_n, B, gid);
+}
 
 // f64::round (ties away from zero), then `as i64` (saturating).
 __device__ __forceinline__ int64_t round_away(double z) {
@@ -98,17 +105,19 @@ template <class W>
 __global__ void __launch_bounds__(256)
 k_sample_gaussian(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, SampleKey s,
                   double sigma, uint32_t log_n, uint32_t L, uint32_t B, uint64_t total) {
-  const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= total) return;  // [B][N]
-  const uint32_t k = (uint32_t)(gid & ((1ull << log_n) - 1));
-  const uint32_t p = (uint32_t)(gid >> log_n);
-  const uint4 v = draw(s, k, 0, p, 0, kDrawGauss);
-  const double u1 = (double)((lo64(v) >> 11) + 1) * 0x1.0p-53;  // (0, 1]
-  const double u2 = (double)(hi64(v) >> 11) * 0x1.0p-53;        // [0, 1)
-  const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2) * sigma;
-  const int64_t e = round_away(z);
-  const uint64_t ls = (uint64_t)B << log_n;
-  for (uint32_t l = 0; l < L; ++l) out[l * ls + gid] = rem_euclid<W>(e, lc[l]);
+  // [B][N], grid-stride as k_sample_uniform
+  for (uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; gid < total;
+       gid += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t k = (uint32_t)(gid & ((1ull << log_n) - 1));
+    const uint32_t p = (uint32_t)(gid >> log_n);
+    const uint4 v = draw(s, k, 0, p, 0, kDrawGauss);
+    const double u1 = (double)((lo64(v) >> 11) + 1) * 0x1.0p-53;  // (0, 1]
+    const double u2 = (double)(hi64(v) >> 11) * 0x1.0p-53;        // [0, 1)
+    const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2) * sigma;
+    const int64_t e = round_away(z);
+    const uint64_t ls = (uint64_t)B << log_n;
+    for (uint32_t l = 0; l < L; ++l) out[l * ls + gid] = rem_euclid<W>(e, lc[l]);
+  }
 }
 
 constexpr uint32_t kTernThreads = 1024;
@@ -159,7 +168,12 @@ k_sample_ternary(W* __restrict__ out, const LimbConst<W>* __restrict__ lc, Sampl
   }
 }
 
-unsigned grid_for_total(uint64_t total) { return (unsigned)((total + 255) / 256); }
+// Blocks of 256 for `total` items, capped so a dispatch stays under 2^32
+// work-items (the kernels stride over the rest).
+unsigned grid_for_total(uint64_t total) {
+  const uint64_t b = (total + 255) / 256;
+  return (unsigned)(b < (1ull << 22) ? b : (1ull << 22));
+}
 
 template <class W>
 hipError_t sample_impl(const Launch& k, int kind, void* out, SampleKey s, double sigma,
