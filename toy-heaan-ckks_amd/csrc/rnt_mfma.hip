@@ -562,6 +562,9 @@ __device__ __forceinline__ v4i stash_get(uint32_t addr, int c) {
 // inverse pass 3 (F^-1, data as A: P4 -> Q3) on the canonical words as
 // loaded (biased here, comp undoes it), then its twist; packed output.
 // tv: tile 0's twists (each tile loads the next one's).
+// PK: the words are already in the passes' packed signed form (a product
+// epilogue's Montgomery output), so no bias and no compensation.
+template <bool PK = false>
 __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v4i comp, v4i tv, Rsrc tab,
                                          uint32_t tvo, uint32_t tso, const Mc& m, uint32_t* lds, const Th& h) {
 #pragma unroll
@@ -569,10 +572,13 @@ __device__ __forceinline__ void ipass_p4(uint32_t (&x)[64], const v4i (&M)[4], v
     mf_prio<RNT_MF_IPRIO != 0>(c);
     v4i a;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = (int)pk_canon(x[p3(c, i)]);
+    for (int i = 0; i < 4; ++i) a[i] = (int)(PK ? x[p3(c, i)] : pk_canon(x[p3(c, i)]));
     const v4i tn = c + 1 < 16 ? bld(tab, tvo, tso + (uint32_t)(c + 1) * 1024u) : tv;
     v4i D[4];
-    tile<true, true>(D, M, a, comp);
+    if constexpr (PK)
+      tile<true, false>(D, M, a, v4i{0, 0, 0, 0});
+    else
+      tile<true, true>(D, M, a, comp);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int32_t r = recomb<false>(D[0][i], D[1][i], D[2][i], D[3][i], m);
@@ -777,7 +783,7 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
 // barriers, which it passes once it has used (so read) every word it loaded.
 // LOAD = false: the plane is already in x2 (P4 positions, canonical), as a
 // forward pass's epilogue left it; the LDS may still be read by other waves.
-template <bool LOAD>
+template <bool LOAD, bool PK = false>
 __device__ __forceinline__ void inv_x(uint32_t (&x2)[64], Rsrc pr, uint32_t* lds, const Th& h, const Tabs& T) {
   const Mc& m = T.m;
   const uint32_t lo = h.lam() * 16u;
@@ -796,7 +802,7 @@ __device__ __forceinline__ void inv_x(uint32_t (&x2)[64], Rsrc pr, uint32_t* lds
   } else {
     __syncthreads();  // ipass_p4's stash reuses the LDS of the last exchange
   }
-  ipass_p4(x2, M, comp, tv0, T.tab, lo, t4s, m, lds, h);
+  ipass_p4<PK>(x2, M, comp, tv0, T.tab, lo, t4s, m, lds, h);
   load_mat(M, T.tab, S_I3, lo);
   ipass_p3(x2, M, T.tab, h.g() * 16u, (uint32_t)(kTw3i + h.w * 64) * 16u, m, lds, h);
   swap_q3p2(x2);
@@ -1007,15 +1013,16 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
     for (int i = 0; i < 4; ++i) {
       // (a^ 2^32) b^ 2^-32, a signed Montgomery product of two signed
       // representatives (|a^|, |b^| < q < 2^31: |a b| + |m q| < 2^63, the
-      // result in (-q, q)), made canonical: the exact product
-      xx[p3(cc, i)] = canon(mont<false>(ah[i], r[i], T.m), (int32_t)q);
+      // result in (-q, q)): the exact product, in the packed signed form
+      // the inverse's first pass takes as it is (inv_x<false, true>)
+      xx[p3(cc, i)] = (uint32_t)mont<true>(ah[i], r[i], T.m) ^ K32;
     }
     // computed here: left free, hipcc sinks each reduction to the inverse's
     // first use of the word and keeps its 64-bit partial live (232 bytes a
     // lane of spills)
     pin4(xx[p3(cc, 0)], xx[p3(cc, 1)], xx[p3(cc, 2)], xx[p3(cc, 3)]);
   });
-  inv_x<false>(x, rsrc(c + o, kN * 4u), lds, h, T);
+  inv_x<false, true>(x, rsrc(c + o, kN * 4u), lds, h, T);
 }
 
 // ---------------------------------------------------------------------------
