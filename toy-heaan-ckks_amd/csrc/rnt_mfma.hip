@@ -546,7 +546,8 @@ __device__ __forceinline__ void pass_p4(uint32_t (&x)[64], const v4i (&M)[4], co
 // worth of operands in registers: the outputs of ipass_p4's first kStash
 // tiles wait in a per-wave LDS stash (the LDS is idle until the exchanges)
 // until ipass_p3 takes them, instead of being spilled to scratch memory.
-constexpr int kStash = 10;
+constexpr int kStash = 10;  // the most that fits: fewer measured more spills (8: 52 B a lane in the inverse)
+static_assert((size_t)kStash * 16 * 1024 <= kLdsBytes, "sixteen waves' stashes in the LDS");
 __device__ __forceinline__ uint32_t stash_addr(const uint32_t* lds, const Th& h) {
   return (uint32_t)(uintptr_t)lds + (h.w * (kStash * 64u) + h.lam()) * 16u;
 }
