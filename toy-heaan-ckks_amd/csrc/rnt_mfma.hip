@@ -185,7 +185,10 @@ __device__ __forceinline__ int32_t recomb(int32_t c0, int32_t c1, int32_t c2, in
   const int64_t v = (int64_t)(int32_t)mm * m.q + t;
   return (int32_t)(v >> 32);
 }
-// Signed Montgomery product a b 2^-32 mod q (|a|, |b| < 2^30.01), + 0x80808080 when WK.
+// Signed Montgomery product a b 2^-32 mod q, + 0x80808080 when WK.  Any
+// |a|, |b| < q < 2^31: |a b + m q| < q^2 + 2^31 q < 2^63 and the result lies
+// in (-q, q); the bias K only adds to the high word (its low word is 0), so
+// a wrap of the 64-bit sum does not change the returned word mod 2^32.
 template <bool WK>
 __device__ __forceinline__ int32_t mont(int32_t a, int32_t b, const Mc& m) {
   // one v_mad_i64_i32 (left to itself hipcc widens a -- the high word of
@@ -985,7 +988,6 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
   const uint64_t o = (uint64_t)l * ls + (uint64_t)poly * kN;
   const LimbConst<uint32_t> lc = lcs[l];
   const Tabs T = tabs_of(mft, lc, l);
-  const uint32_t q = lc.q;
   uint64_t so;
   if (slots) {
     const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;          // hwreg(HW_REG_XCC_ID)
