@@ -354,6 +354,62 @@ __device__ __forceinline__ void x_read_p2(uint32_t (&x2)[64], const uint32_t* ld
   lds_wait8<32 * H + 16>(x2);
   lds_wait8<32 * H + 24>(x2);
 }
+// ---- the quarter-plane (64 KiB) P1 -> P2 exchange ---------------------------
+// k_mf_mul's fwd(b) exchanges in four rounds so the LDS above 64 KiB can hold
+// six of a^'s sixteen tiles a wave.  The LDS word function above without
+// index bit 10 (weight 32): bits (7, 10) pick the round -- P1 chunk bits 3
+// and 2, P2 chunk bit 3 and register bit i0 -- and the weights above 32
+// halve.  The low five address bits are unchanged, so both layouts stay
+// conflict-free.
+__device__ __forceinline__ void p1_bases4(uint32_t (&wb)[4], const Th& h) {
+  const uint32_t n0 = h.n() & 1, n1 = (h.n() >> 1) & 1, n2 = (h.n() >> 2) & 1, n3 = h.n() >> 3;
+  const uint32_t g0 = h.g() & 1, g1 = h.g() >> 1;
+  const uint32_t w0 = h.w & 1, w1 = (h.w >> 1) & 1, w2 = (h.w >> 2) & 1, w3 = h.w >> 3;
+  const uint32_t rest = 4 * n0 + 8 * n1 + 16 * (w1 ^ g0) + 128 * w0 + 256 * w3 + 512 * n2 + 1024 * n3 +
+                        2048 * g0 + 4096 * g1 + 8192 * w2;
+#pragma unroll
+  for (uint32_t e = 0; e < 4; ++e) wb[e] = rest + ((e & 1) ^ n2) + 2 * ((e >> 1) ^ n3);
+}
+__device__ __forceinline__ void p2_bases4(uint32_t (&rb)[4], const Th& h) {
+  const uint32_t n0 = h.n() & 1, n1 = (h.n() >> 1) & 1, n2 = (h.n() >> 2) & 1, n3 = h.n() >> 3;
+  const uint32_t g0 = h.g() & 1, g1 = h.g() >> 1;
+  const uint32_t w0 = h.w & 1, w1 = (h.w >> 1) & 1, w2 = (h.w >> 2) & 1, w3 = h.w >> 3;
+  const uint32_t rest = 4 * n2 + 8 * n3 + 16 * (g0 ^ w0) + 32 * w2 + 64 * w3 + 2048 * w0 + 4096 * w1 + 8192 * g1;
+#pragma unroll
+  for (uint32_t e = 0; e < 4; ++e) rb[e] = rest + (n0 ^ (e & 1)) + 2 * (n1 ^ (e >> 1)) + 512 * (e & 1) + 1024 * (e >> 1);
+}
+__host__ __device__ constexpr uint32_t p1_off4(int, int i) { return 32u * (i & 1) + 64u * (i >> 1); }
+__host__ __device__ constexpr uint32_t p2_off4(int c, int i) { return 256u * (i >> 1) + 128u * ((c >> 2) & 1); }
+// Round Q: P1 chunks 4Q .. 4Q+3 out; P2 chunks 8(Q >> 1) .. +7, registers
+// i = Q & 1 and (Q & 1) + 2, in.
+template <int Q>
+__device__ __forceinline__ void x_write_p1q(const uint32_t (&x1)[64], uint32_t* lds, const uint32_t (&wb)[4]) {
+#pragma unroll
+  for (int c = 4 * Q; c < 4 * Q + 4; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lds[wb[c & 3] + p1_off4(c, i)] = x1[4 * c + i];
+}
+template <int C, int I>
+__device__ __forceinline__ void x_read_p2q_one(uint32_t (&x2)[64], uint32_t lds0, const uint32_t (&rb)[4]) {
+  x2[4 * C + I] = lds_rd<p2_off4(C, I) * 4u>(lds0 + rb[C & 3] * 4u);
+}
+template <int Q>
+__device__ __forceinline__ void x_read_p2q(uint32_t (&x2)[64], const uint32_t* lds, const uint32_t (&rb)[4]) {
+  constexpr int H = Q >> 1, X = Q & 1;
+  const uint32_t l0 = (uint32_t)(uintptr_t)lds;
+#define RNT_MF_RDQ(C)                    \
+  x_read_p2q_one<C, X>(x2, l0, rb);      \
+  x_read_p2q_one<C, X + 2>(x2, l0, rb);
+  RNT_MF_RDQ(8 * H + 0) RNT_MF_RDQ(8 * H + 1) RNT_MF_RDQ(8 * H + 2) RNT_MF_RDQ(8 * H + 3)
+  RNT_MF_RDQ(8 * H + 4) RNT_MF_RDQ(8 * H + 5) RNT_MF_RDQ(8 * H + 6) RNT_MF_RDQ(8 * H + 7)
+#undef RNT_MF_RDQ
+  constexpr int B = 32 * H + X;
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(x2[B + 0]), "+v"(x2[B + 2]), "+v"(x2[B + 4]), "+v"(x2[B + 6]), "+v"(x2[B + 8]),
+                 "+v"(x2[B + 10]), "+v"(x2[B + 12]), "+v"(x2[B + 14]), "+v"(x2[B + 16]), "+v"(x2[B + 18]),
+                 "+v"(x2[B + 20]), "+v"(x2[B + 22]), "+v"(x2[B + 24]), "+v"(x2[B + 26]), "+v"(x2[B + 28]),
+                 "+v"(x2[B + 30]));
+}
 // the inverse direction: P2 words at q2(c, i) out, P1 words in
 template <int H>
 __device__ __forceinline__ void x_write_p2(const uint32_t (&x2)[64], uint32_t* lds, const uint32_t (&rb)[4]) {
@@ -730,7 +786,10 @@ __device__ __forceinline__ Tabs tabs_of(const void* mf, const LimbConst<uint32_t
 struct NoEpi {
   __device__ void operator()(int, const int32_t (&)[4], uint32_t (&)[64]) const {}
 };
-template <bool SYNC1, int F4 = S_F4, class EPI = NoEpi>
+// Q4: the exchange in four quarter-plane rounds (the LDS above 64 KiB stays
+// free); SYNCX: a barrier after the last exchange read (the caller writes
+// the exchange region's upper half from the last pass on).
+template <bool SYNC1, int F4 = S_F4, bool Q4 = false, bool SYNCX = false, class EPI = NoEpi>
 __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds, const Th& h, const Tabs& T,
                                     const EPI& epi = EPI{}) {
   // the first pass's operands load ahead of the plane (cache hits, needed
@@ -747,6 +806,35 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   MF_STAMP(2);
   if constexpr (SYNC1) __syncthreads();
   uint32_t wb[4], rb[4];
+  const uint32_t t3v = h.g() * 256u, t3s = (uint32_t)(kTw3f + h.w * 64) * 16u;
+  if constexpr (Q4) {
+    p1_bases4(wb, h);
+    x_write_p1q<0>(x1, lds, wb);
+    pass_p1<8, true>(x1, M, comp, m);
+    __syncthreads();
+    p2_bases4(rb, h);
+    x_read_p2q<0>(x2, lds, rb);
+    __syncthreads();
+    p1_bases4(wb, h);
+    x_write_p1q<1>(x1, lds, wb);
+    __syncthreads();
+    p2_bases4(rb, h);
+    x_read_p2q<1>(x2, lds, rb);
+    __syncthreads();
+    p1_bases4(wb, h);
+    x_write_p1q<2>(x1, lds, wb);
+    load_mat(M, T.tab, S_F2 + h.w, lo);
+    pass_p2<0>(x2, M, T.tab, t3v, t3s, m);
+    __syncthreads();
+    p2_bases4(rb, h);
+    x_read_p2q<2>(x2, lds, rb);
+    __syncthreads();
+    p1_bases4(wb, h);
+    x_write_p1q<3>(x1, lds, wb);
+    __syncthreads();
+    p2_bases4(rb, h);
+    x_read_p2q<3>(x2, lds, rb);
+  } else {
   p1_bases(wb, h);
   x_write_p1<0>(x1, lds, wb);
   pass_p1<8, true>(x1, M, comp, m);
@@ -760,13 +848,14 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   p1_bases(wb, h);
   x_write_p1<1>(x1, lds, wb);
   load_mat(M, T.tab, S_F2 + h.w, lo);
-  const uint32_t t3v = h.g() * 256u, t3s = (uint32_t)(kTw3f + h.w * 64) * 16u;
   pass_p2<0>(x2, M, T.tab, t3v, t3s, m);
   MF_STAMP(6);
   __syncthreads();
   MF_STAMP(7);
   p2_bases(rb, h);
   x_read_p2<1>(x2, lds, rb);
+  }
+  if constexpr (SYNCX) __syncthreads();
   pass_p2<8>(x2, M, T.tab, t3v, t3s, m);
   MF_STAMP(8);
   swap_p2p3(x2);
@@ -965,11 +1054,14 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
   inv_x<false>(x, R2, lds, h, T);
 }
 
-#ifndef RNT_MF_MUL_LDS
-#define RNT_MF_MUL_LDS 2
+// RNT_MF_MUL_Q4: fwd(b) exchanges in quarter-plane rounds, and six a^
+// tiles a wave stay in the LDS above 64 KiB (else two above 128 KiB)
+#ifndef RNT_MF_MUL_Q4
+#define RNT_MF_MUL_Q4 1
 #endif
-constexpr int kMulLdsTiles = RNT_MF_MUL_LDS;  // a^ tiles per wave kept in the LDS (k_mf_mul)
-static_assert(kMulLdsTiles * 16 * 1024 <= 32 * 1024, "beside the 128 KiB exchange region");
+constexpr int kMulLdsTiles = RNT_MF_MUL_Q4 ? 6 : 2;  // a^ tiles per wave kept in the LDS (k_mf_mul)
+constexpr uint32_t kMulLdsBase = RNT_MF_MUL_Q4 ? (1u << 14) : (1u << 15);  // words
+static_assert(kMulLdsBase * 4 + (size_t)kMulLdsTiles * 16 * 1024 <= mf::kLdsBytes, "in the LDS");
 // The coefficient-domain product c = a b at N = 2^16 (rnt_mul, poly.rs:307-329)
 // on the matrix-core transforms, one workgroup per (poly, limb): fwd a -> a^
 // into the CU's scratch slot (k_mf_tensor's indexing); fwd b, whose last
@@ -1003,14 +1095,16 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
   // the signed representatives (|r| < q) go to the slot as they are; the
   // last kMulLdsTiles tiles of each wave stay in the LDS past the exchange
   // region (free until the inverse's stash), 1 KiB a tile per wave
-  v4i* hat = (v4i*)(lds + (1u << 15)) + h.w * (kMulLdsTiles * 64) + h.lam();
-  fwd<false, S_F4S>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  v4i* hat = (v4i*)(lds + kMulLdsBase) + h.w * (kMulLdsTiles * 64) + h.lam();
+  // (with Q4 the tiles overlap fwd(a)'s exchange region: SYNCX holds every
+  // wave's last pass until all have read their last exchange words)
+  fwd<false, S_F4S, false, RNT_MF_MUL_Q4 != 0>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     if (cc >= 16 - kMulLdsTiles)
       hat[(cc - (16 - kMulLdsTiles)) * 64] = v4i{r[0], r[1], r[2], r[3]};
     else
       bst(v4i{r[0], r[1], r[2], r[3]}, RS, pl, p4_soff(h, cc));
   });
-  fwd<true>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
+  fwd<true, S_F4, RNT_MF_MUL_Q4 != 0>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
     const v4i ah = cc >= 16 - kMulLdsTiles ? hat[(cc - (16 - kMulLdsTiles)) * 64] : bld(RS, pl, p4_soff(h, cc));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
