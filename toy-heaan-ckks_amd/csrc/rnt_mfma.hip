@@ -1059,6 +1059,9 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
 #ifndef RNT_MF_MUL_Q4
 #define RNT_MF_MUL_Q4 1
 #endif
+#ifndef RNT_MF_MUL_NOSYNC1
+#define RNT_MF_MUL_NOSYNC1 1
+#endif
 constexpr int kMulLdsTiles = RNT_MF_MUL_Q4 ? 6 : 2;  // a^ tiles per wave kept in the LDS (k_mf_mul)
 constexpr uint32_t kMulLdsBase = RNT_MF_MUL_Q4 ? (1u << 14) : (1u << 15);  // words
 static_assert(kMulLdsBase * 4 + (size_t)kMulLdsTiles * 16 * 1024 <= mf::kLdsBytes, "in the LDS");
@@ -1104,7 +1107,10 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
     else
       bst(v4i{r[0], r[1], r[2], r[3]}, RS, pl, p4_soff(h, cc));
   });
-  fwd<true, S_F4, RNT_MF_MUL_Q4 != 0>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
+  // fwd(b) needs no barrier before its first exchange write with Q4: every
+  // wave passed fwd(a)'s SYNCX after its last read of fwd(a)'s exchange,
+  // and fwd(b)'s quarter rounds stay below the a^ tiles
+  fwd<!(RNT_MF_MUL_Q4 && RNT_MF_MUL_NOSYNC1), S_F4, RNT_MF_MUL_Q4 != 0>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
     const v4i ah = cc >= 16 - kMulLdsTiles ? hat[(cc - (16 - kMulLdsTiles)) * 64] : bld(RS, pl, p4_soff(h, cc));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
