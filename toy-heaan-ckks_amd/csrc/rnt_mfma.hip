@@ -495,6 +495,10 @@ __device__ __forceinline__ void swap_q3p2(uint32_t (&x)[64]) {
 #ifndef RNT_MF_PRIO
 #define RNT_MF_PRIO 1
 #endif
+// k_mf_tensor: each forward's exchange fenced after its own last read
+#ifndef RNT_MF_TENSOR_SYNCX
+#define RNT_MF_TENSOR_SYNCX 1
+#endif
 // the same over the inverse's first stretch (its passes 3, 2 and the first
 // half of 1: 40 tiles between the plane load and the first exchange)
 #ifndef RNT_MF_IPRIO
@@ -1015,13 +1019,18 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
   };
   const uint32_t rm = lc.rmod, rmp = lc.rmod_p;
   uint32_t x[64];
-  fwd<false>(x, rsrc(c0 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  // each forward's LDS exchange is fenced by a barrier right after its own
+  // last exchange read (SYNCX: the waves are together there) rather than
+  // before the next forward's first write (SYNC1, after a drift of three
+  // passes); RNT_MF_TENSOR_SYNCX=0 keeps the latter
+  constexpr bool SX = RNT_MF_TENSOR_SYNCX != 0;
+  fwd<false, S_F4, false, SX>(x, rsrc(c0 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     bst(canon4(r), R1, pl, p4_soff(h, cc));
   });
-  fwd<true>(x, rsrc(c1 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  fwd<!SX, S_F4, false, SX>(x, rsrc(c1 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     bst(canon4(r), RS, pl, p4_soff(h, cc));
   });
-  fwd<true>(x, rsrc(c0p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  fwd<!SX, S_F4, false, SX>(x, rsrc(c0p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     const v4i a0 = bld(R1, pl, p4_soff(h, cc)), a1 = bld(RS, pl, p4_soff(h, cc));
     const v4i b = canon4(r);
     v4i o0, t;
@@ -1033,7 +1042,7 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
     bst(o0, R0, pl, p4_soff(h, cc));
     bst(t, R2, pl, p4_soff(h, cc));
   });
-  fwd<true>(x, rsrc(c1p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
+  fwd<!SX>(x, rsrc(c1p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
     const v4i a0 = bld(R1, pl, p4_soff(h, cc)), a1 = bld(RS, pl, p4_soff(h, cc));
     const v4i t = bld(R2, pl, p4_soff(h, cc));
     const v4i b = canon4(r);
