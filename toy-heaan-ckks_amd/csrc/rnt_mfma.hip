@@ -499,6 +499,12 @@ __device__ __forceinline__ void swap_q3p2(uint32_t (&x)[64]) {
 #ifndef RNT_MF_TENSOR_SYNCX
 #define RNT_MF_TENSOR_SYNCX 1
 #endif
+#ifndef RNT_MF_TENSOR_PARK
+#define RNT_MF_TENSOR_PARK 0
+#endif
+#ifndef RNT_MF_TENSOR_PARK4
+#define RNT_MF_TENSOR_PARK4 0
+#endif
 // the same over the inverse's first stretch (its passes 3, 2 and the first
 // half of 1: 40 tiles between the plane load and the first exchange)
 #ifndef RNT_MF_IPRIO
@@ -793,7 +799,17 @@ struct NoEpi {
 // Q4: the exchange in four quarter-plane rounds (the LDS above 64 KiB stays
 // free); SYNCX: a barrier after the last exchange read (the caller writes
 // the exchange region's upper half from the last pass on).
-template <bool SYNC1, int F4 = S_F4, bool Q4 = false, bool SYNCX = false, class EPI = NoEpi>
+// NPARK: P2 chunks 0..NPARK-1 (idle through pass 1's second half) wait in
+// the LDS at byte PBASE + wave * PSTRIDE from SYNCX to the P2 -> P3 swap,
+// instead of being spilled to scratch memory (whose write-back is HBM
+// traffic); the caller guarantees no other wave touches that LDS then.
+template <int NPARK, uint32_t PBASE, uint32_t PSTRIDE>
+__device__ __forceinline__ uint32_t park_addr(const uint32_t* lds, const Th& h) {
+  static_assert(NPARK * 1024 <= (int)PSTRIDE && PBASE + 16 * PSTRIDE <= kLdsBytes, "park area");
+  return (uint32_t)(uintptr_t)lds + PBASE + h.w * PSTRIDE + h.lam() * 16u;
+}
+template <bool SYNC1, int F4 = S_F4, bool Q4 = false, bool SYNCX = false, int NPARK = 0, uint32_t PBASE = 0,
+          uint32_t PSTRIDE = 0, class EPI = NoEpi>
 __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds, const Th& h, const Tabs& T,
                                     const EPI& epi = EPI{}) {
   // the first pass's operands load ahead of the plane (cache hits, needed
@@ -860,8 +876,18 @@ __device__ __forceinline__ void fwd(uint32_t (&x2)[64], Rsrc src, uint32_t* lds,
   x_read_p2<1>(x2, lds, rb);
   }
   if constexpr (SYNCX) __syncthreads();
+  static_assert(NPARK == 0 || SYNCX, "the park area is free only past SYNCX");
+#pragma unroll
+  for (int c = 0; c < NPARK; ++c)
+    stash_put(park_addr<NPARK, PBASE, PSTRIDE>(lds, h), c, x2[4 * c], x2[4 * c + 1], x2[4 * c + 2], x2[4 * c + 3]);
   pass_p2<8>(x2, M, T.tab, t3v, t3s, m);
   MF_STAMP(8);
+#pragma unroll
+  for (int c = 0; c < NPARK; ++c) {
+    const v4i v = stash_get(park_addr<NPARK, PBASE, PSTRIDE>(lds, h), c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x2[4 * c + i] = (uint32_t)v[i];
+  }
   swap_p2p3(x2);
   load_mat(M, T.tab, S_F3, lo);
   pass_p3(x2, M, T.tab, lo, (uint32_t)(kTw4f + h.w * 1024) * 16u, m);
@@ -1024,13 +1050,19 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
   // before the next forward's first write (SYNC1, after a drift of three
   // passes); RNT_MF_TENSOR_SYNCX=0 keeps the latter
   constexpr bool SX = RNT_MF_TENSOR_SYNCX != 0;
-  fwd<false, S_F4, false, SX>(x, rsrc(c0 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  // RNT_MF_TENSOR_PARK: P2 chunks parked past SYNCX in [128 KiB, 160 KiB),
+  // which the exchanges (the lower 128 KiB) leave free: spills 128 -> 88
+  // bytes a lane, the kernel flat to -0.6% (profiles/r05/ab_mf_tensor_syncx.txt),
+  // off by default
+  constexpr int NP = SX ? RNT_MF_TENSOR_PARK : 0;
+  constexpr uint32_t PB = 128u * 1024u, PS = 2048u;
+  fwd<false, S_F4, false, SX, NP, PB, PS>(x, rsrc(c0 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     bst(canon4(r), R1, pl, p4_soff(h, cc));
   });
-  fwd<!SX, S_F4, false, SX>(x, rsrc(c1 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  fwd<!SX, S_F4, false, SX, NP, PB, PS>(x, rsrc(c1 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     bst(canon4(r), RS, pl, p4_soff(h, cc));
   });
-  fwd<!SX, S_F4, false, SX>(x, rsrc(c0p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  fwd<!SX, S_F4, false, SX, NP, PB, PS>(x, rsrc(c0p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     const v4i a0 = bld(R1, pl, p4_soff(h, cc)), a1 = bld(RS, pl, p4_soff(h, cc));
     const v4i b = canon4(r);
     v4i o0, t;
@@ -1042,7 +1074,7 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
     bst(o0, R0, pl, p4_soff(h, cc));
     bst(t, R2, pl, p4_soff(h, cc));
   });
-  fwd<!SX>(x, rsrc(c1p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
+  fwd<!SX, S_F4, false, RNT_MF_TENSOR_PARK4 && SX, RNT_MF_TENSOR_PARK4 ? NP : 0, PB, PS>(x, rsrc(c1p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
     const v4i a0 = bld(R1, pl, p4_soff(h, cc)), a1 = bld(RS, pl, p4_soff(h, cc));
     const v4i t = bld(R2, pl, p4_soff(h, cc));
     const v4i b = canon4(r);
@@ -1070,6 +1102,12 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
 #endif
 #ifndef RNT_MF_MUL_NOSYNC1
 #define RNT_MF_MUL_NOSYNC1 1
+#endif
+// RNT_MF_MUL_PARK: P2 chunks parked in the LDS over pass 1's second half
+// (fwd(a): in the wave's own a^ tile area, not yet written; fwd(b): in its
+// 4 KiB of the quarter-round region, behind a SYNCX barrier)
+#ifndef RNT_MF_MUL_PARK
+#define RNT_MF_MUL_PARK 4
 #endif
 constexpr int kMulLdsTiles = RNT_MF_MUL_Q4 ? 6 : 2;  // a^ tiles per wave kept in the LDS (k_mf_mul)
 constexpr uint32_t kMulLdsBase = RNT_MF_MUL_Q4 ? (1u << 14) : (1u << 15);  // words
@@ -1101,26 +1139,28 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
     so = (uint64_t)(poly + l * gridDim.x) << 16;
   }
   const Rsrc RS = rsrc(scratch + so, kN * 4u);
-  const uint32_t pl = p4_lane(h);
   uint32_t x[64];
   // a^ 2^32: fwd(a)'s last pass runs on F4 2^32 (slot S_F4S)
   // the signed representatives (|r| < q) go to the slot as they are; the
   // last kMulLdsTiles tiles of each wave stay in the LDS past the exchange
   // region (free until the inverse's stash), 1 KiB a tile per wave
-  v4i* hat = (v4i*)(lds + kMulLdsBase) + h.w * (kMulLdsTiles * 64) + h.lam();
+  // (recomputed where used from the opaque thread index, as is the lane
+  // offset p4_lane: kept live across the passes they cost 16-byte spills)
+  auto hat = [&](int t) -> v4i& { return ((v4i*)(lds + kMulLdsBase) + h.w * (kMulLdsTiles * 64) + h.lam())[t * 64]; };
   // (with Q4 the tiles overlap fwd(a)'s exchange region: SYNCX holds every
   // wave's last pass until all have read their last exchange words)
-  fwd<false, S_F4S, false, RNT_MF_MUL_Q4 != 0>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
+  constexpr int NP = RNT_MF_MUL_Q4 ? RNT_MF_MUL_PARK : 0;
+  fwd<false, S_F4S, false, RNT_MF_MUL_Q4 != 0, NP, kMulLdsBase * 4, kMulLdsTiles * 1024>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     if (cc >= 16 - kMulLdsTiles)
-      hat[(cc - (16 - kMulLdsTiles)) * 64] = v4i{r[0], r[1], r[2], r[3]};
+      hat(cc - (16 - kMulLdsTiles)) = v4i{r[0], r[1], r[2], r[3]};
     else
-      bst(v4i{r[0], r[1], r[2], r[3]}, RS, pl, p4_soff(h, cc));
+      bst(v4i{r[0], r[1], r[2], r[3]}, RS, p4_lane(h), p4_soff(h, cc));
   });
   // fwd(b) needs no barrier before its first exchange write with Q4: every
   // wave passed fwd(a)'s SYNCX after its last read of fwd(a)'s exchange,
   // and fwd(b)'s quarter rounds stay below the a^ tiles
-  fwd<!(RNT_MF_MUL_Q4 && RNT_MF_MUL_NOSYNC1), S_F4, RNT_MF_MUL_Q4 != 0>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
-    const v4i ah = cc >= 16 - kMulLdsTiles ? hat[(cc - (16 - kMulLdsTiles)) * 64] : bld(RS, pl, p4_soff(h, cc));
+  fwd<!(RNT_MF_MUL_Q4 && RNT_MF_MUL_NOSYNC1), S_F4, RNT_MF_MUL_Q4 != 0, (NP > 0), NP, 0, 4096>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
+    const v4i ah = cc >= 16 - kMulLdsTiles ? hat(cc - (16 - kMulLdsTiles)) : bld(RS, p4_lane(h), p4_soff(h, cc));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       // (a^ 2^32) b^ 2^-32, a signed Montgomery product of two signed
