@@ -176,7 +176,11 @@ __device__ __forceinline__ int32_t recomb(int32_t c0, int32_t c1, int32_t c2, in
   const int32_t hi = c2 + (int32_t)((uint32_t)c3 << 8);
   int64_t t;
   if constexpr (WK) {
-    t = (int64_t)lo * m.one + m.K;  // the digit bias rides in the addend's high word
+    // the digit bias rides in the addend's high word; the multiplier is the
+    // inline constant 1 (as lo * m.one + m.K, two SGPR operands exceed the
+    // one-scalar operand limit and hipcc kept K in a VGPR pair all kernel)
+    uint64_t cc;
+    asm("v_mad_i64_i32 %0, %1, %2, 1, %3" : "=v"(t), "=s"(cc) : "v"(lo), "s"(m.K));
   } else {
     t = (int64_t)lo;  // sign extension: one shift instead of a 64-bit multiply-add
   }
