@@ -147,10 +147,19 @@ typedef __amdgpu_buffer_rsrc_t Rsrc;
 __device__ __forceinline__ Rsrc rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)bytes, 0x00020000);
 }
+// RNT_MF_NT: the cache-policy bits of the plane loads and stores that
+// stream (the operand planes in, the result out): 2 = nt, so they do not
+// push the re-read lines (the tables, the a^ slot) out of the L2.
+#ifndef RNT_MF_NT
+#define RNT_MF_NT 2
+#endif
+constexpr int kStreamAux = RNT_MF_NT;
+template <int AUX = 0>
 __device__ __forceinline__ v4i bld(Rsrc r, uint32_t voff, uint32_t soff) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX);
   return v4i{(int)v[0], (int)v[1], (int)v[2], (int)v[3]};
 }
+template <int AUX = 0>
 __device__ __forceinline__ void bst(v4i x, Rsrc r, uint32_t voff, uint32_t soff) {
   using V4 = decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0));
   V4 v;
@@ -158,7 +167,7 @@ __device__ __forceinline__ void bst(v4i x, Rsrc r, uint32_t voff, uint32_t soff)
   v[1] = (uint32_t)x[1];
   v[2] = (uint32_t)x[2];
   v[3] = (uint32_t)x[3];
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, AUX);
   // The store reads its 128-bit data after issue, and hipcc pads nothing
   // for a buffer store with an SGPR soffset: a VALU write of the data
   // registers 0-1 wait states later lost single lanes of stored words (r05,
@@ -735,7 +744,7 @@ __device__ __forceinline__ void load_p1(uint32_t (&x1)[64], Rsrc src, const Th& 
   for (int hc = 0; hc < 4; ++hc)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const v4i v = bld(src, lo, wo + p1_reg(i, hc));
+      const v4i v = bld<kStreamAux>(src, lo, wo + p1_reg(i, hc));
 #pragma unroll
       for (int e = 0; e < 4; ++e) x1[4 * (4 * hc + e) + i] = (uint32_t)v[e];
     }
@@ -761,7 +770,7 @@ __device__ __forceinline__ void ipass_p1(uint32_t (&x1)[64], const v4i (&M)[4], 
         v4i v;
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = (int)x1[4 * (4 * hc + e) + i];
-        bst(v, dst, lo, wo + p1_reg(i, hc));
+        bst<kStreamAux>(v, dst, lo, wo + p1_reg(i, hc));
       }
     } else {
       pin4(x1[4 * c + 0], x1[4 * c + 1], x1[4 * c + 2], x1[4 * c + 3]);
@@ -982,7 +991,7 @@ k_mf_ntt(uint32_t* __restrict__ data, const void* __restrict__ mft, const LimbCo
     // place: every wave read its words of the plane before the first
     // exchange's barrier)
     fwd<false>(x, pr, lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
-      bst(v4i{(int)canon(r[0], T.m.q), (int)canon(r[1], T.m.q), (int)canon(r[2], T.m.q), (int)canon(r[3], T.m.q)}, pr,
+      bst<kStreamAux>(v4i{(int)canon(r[0], T.m.q), (int)canon(r[1], T.m.q), (int)canon(r[2], T.m.q), (int)canon(r[3], T.m.q)}, pr,
           p4_lane(h), p4_soff(h, cc));
     });
   } else {
