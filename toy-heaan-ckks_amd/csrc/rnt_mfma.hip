@@ -154,6 +154,14 @@ __device__ __forceinline__ Rsrc rsrc(const void* base, uint32_t bytes) {
 #define RNT_MF_NT 2
 #endif
 constexpr int kStreamAux = RNT_MF_NT;
+// RNT_MF_LAST_NT: the same hint on k_mf_tensor's last reads of its
+// temporaries (c0^, c1^, t in the last epilogue) and its final d0, d1
+// stores (-2.8% tensor time; on k_mf_mul's a^ reads it measured -0.3%, so
+// those keep the default, profiles/r05/ab_mf_nt.txt)
+#ifndef RNT_MF_LAST_NT
+#define RNT_MF_LAST_NT 2
+#endif
+constexpr int kLastAux = RNT_MF_LAST_NT;
 template <int AUX = 0>
 __device__ __forceinline__ v4i bld(Rsrc r, uint32_t voff, uint32_t soff) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, AUX);
@@ -1084,12 +1092,12 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
       o0[i] = (int)mmul((uint32_t)a0[i], (uint32_t)b[i]);
       t[i] = (int)mmul((uint32_t)a1[i], (uint32_t)b[i]);
     }
-    bst(o0, R0, pl, p4_soff(h, cc));
+    bst<kLastAux>(o0, R0, pl, p4_soff(h, cc));
     bst(t, R2, pl, p4_soff(h, cc));
   });
   fwd<!SX, S_F4, false, RNT_MF_TENSOR_PARK4 && SX, RNT_MF_TENSOR_PARK4 ? NP : 0, PB, PS>(x, rsrc(c1p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
-    const v4i a0 = bld(R1, pl, p4_soff(h, cc)), a1 = bld(RS, pl, p4_soff(h, cc));
-    const v4i t = bld(R2, pl, p4_soff(h, cc));
+    const v4i a0 = bld<kLastAux>(R1, pl, p4_soff(h, cc)), a1 = bld<kLastAux>(RS, pl, p4_soff(h, cc));
+    const v4i t = bld<kLastAux>(R2, pl, p4_soff(h, cc));
     const v4i b = canon4(r);
     v4i o1;
 #pragma unroll
@@ -1103,7 +1111,7 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
       xx[p3(cc, i)] = v >= q ? v - q : v;
     }
     pin4(xx[p3(cc, 0)], xx[p3(cc, 1)], xx[p3(cc, 2)], xx[p3(cc, 3)]);  // (as in k_mf_mul)
-    bst(o1, R1, pl, p4_soff(h, cc));
+    bst<kLastAux>(o1, R1, pl, p4_soff(h, cc));
   });
   inv_x<false>(x, R2, lds, h, T);
 }
