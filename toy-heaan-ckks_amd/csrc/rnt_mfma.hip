@@ -939,7 +939,7 @@ __device__ __forceinline__ void inv_x(uint32_t (&x2)[64], Rsrc pr, uint32_t* lds
   if constexpr (LOAD) {
 #pragma unroll
     for (int cc = 0; cc < 16; ++cc) {
-      const v4i v = bld(pr, p4_lane(h), p4_soff(h, cc));
+      const v4i v = bld<kStreamAux>(pr, p4_lane(h), p4_soff(h, cc));
 #pragma unroll
       for (int i = 0; i < 4; ++i) x2[p3(cc, i)] = (uint32_t)v[i];
     }
