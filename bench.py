@@ -15,11 +15,11 @@ per GPU fixed (weak scaling) and need no data-path collective for poly-mul;
 only the timing barrier / max-reduce crosses ranks (gloo control plane).
 
 `--workload ctmul` times BASELINE config 4's pipeline instead: ct x ct ->
-gadget relinearisation -> rescale.  At N > 1 its default layout is
-`--shard batch` (each rank its own ciphertexts over all limbs, no data-path
-collective: DESIGN.md §7's model puts it ahead at config 4); `--shard limb`
-runs it limb-sharded with the RCCL all-gather of d2 and broadcast of the
-last limb (rns_ntt.sharded).
+gadget relinearisation -> rescale.  Its default layout at N > 1 is config
+4's own, `--shard limb`: the RCCL all-gather of d2 and the broadcast of the
+last limb (rns_ntt.sharded).  `--shard batch` is SURVEY §8e's zero-collective
+comparison (each rank its own ciphertexts over all limbs, a full key
+replica); the line's config.parallelism names the layout that ran.
 
 Prints ONE JSON line on rank 0.
 """
@@ -64,10 +64,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--workload", choices=("polymul", "ctmul", "rotate", "encode", "ntt", "pointwise", "copy"),
                    default="polymul")
-    p.add_argument("--shard", choices=("limb", "batch"), default=None,
-                   help="multi-GPU layout; default: batch for ctmul (no collective; DESIGN.md §7's "
-                        "model puts it 15-30%% ahead of the limb shard at config 4 on 8 GPUs), "
-                        "limb otherwise (the north star's layout)")
+    p.add_argument("--shard", choices=("limb", "batch"), default="limb",
+                   help="multi-GPU layout: limb (default, the north star's and config 4's layout; "
+                        "ctmul/rotate join over RCCL) or batch (SURVEY 8e's zero-collective comparison)")
     p.add_argument("--batch", type=int, default=1024, help="poly-mul pairs per GPU per step")
     p.add_argument("--inputs", choices=("device", "host"), default="device",
                    help="poly-mul operands: seeded uniform residues drawn on the device (Philox, "
@@ -92,13 +91,13 @@ def parse():
                         "rnt_graph_launch); reports device-busy = kernel time / step time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-power", action="store_true", help="skip the rocm-smi power/clock samples")
+    p.add_argument("--no-live-pmc", action="store_true",
+                   help="poly-mul at N=1: skip the two rocprofv3 --pmc child passes that measure "
+                        "roofline.traffic in this run (then it comes from the committed pass)")
     p.add_argument("--strong", action="store_true",
                    help="poly-mul: --batch is the fixed global batch split over the ranks (strong "
                         "scaling) instead of the per-GPU batch (weak, the default)")
-    args = p.parse_args()
-    if args.shard is None:
-        args.shard = "batch" if args.workload == "ctmul" else "limb"
-    return args
+    return p.parse_args()
 
 
 def relaunch_with_torchrun(args) -> int:
@@ -298,6 +297,66 @@ def traffic_for(kernel, workload, batch, log_n, L):
     return None
 
 
+def _pmc_csv_means(d, kernel_re):
+    """Per-dispatch counter values of the kernels matching kernel_re in a
+    rocprofv3 --pmc output dir (summed over the XCD/SE instances of one
+    dispatch), averaged over dispatches: {counter: mean per launch}."""
+    import collections
+    import csv
+    import glob
+    import re
+
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if re.search(kernel_re, r["Kernel_Name"]):
+                per[r["Counter_Name"]][r.get("Dispatch_Id", "")] += float(r["Counter_Value"])
+    return {c: sum(v.values()) / len(v) for c, v in per.items() if v}
+
+
+def live_pmc(args, kernel_re):
+    """roofline.traffic measured in THIS run: two rocprofv3 --pmc passes of the
+    same workload shape (FETCH_SIZE; WRITE_SIZE + GRBM_GUI_ACTIVE: the
+    per-block counter limits allow no single pass), each a child process
+    (python3 bench.py after `--`, as the profiler requires) under its own
+    time limit, on this box right after the timed region.  HBM bytes per
+    launch = 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md § HBM: gfx950
+    FETCH_SIZE tallies 128-B requests at 64 B; rocprofv3 reports KB).
+    None (and the reason) when the profiler is missing or a pass fails."""
+    import shutil
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    child = [sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+             "--no-power", "--no-live-pmc", "--batch", str(args.batch), "--log-n", str(args.log_n),
+             "--limbs", str(args.limbs), "--prime-bits", str(args.prime_bits), "--inputs", args.inputs]
+    res = {}
+    tmp = tempfile.mkdtemp(prefix="bench_pmc_")
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        for name, ctrs in (("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE", "GRBM_GUI_ACTIVE"])):
+            out = os.path.join(tmp, name)
+            cmd = ["timeout", "-s", "KILL", "240", prof, "--pmc", *ctrs, "--output-format", "csv", "-d", out,
+                   "-o", "run", "--", *child]
+            t0 = time.perf_counter()
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {' '.join(ctrs)} exited {r.returncode}: {r.stderr[-300:]}"
+            m = _pmc_csv_means(out, kernel_re)
+            if not all(c in m for c in ctrs):
+                return None, f"no {kernel_re} dispatches with {ctrs} in the pass"
+            res.update(m)
+            res[f"{name}_pass_s"] = time.perf_counter() - t0
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    fetch, write = res["FETCH_SIZE"] * 1024, res["WRITE_SIZE"] * 1024
+    return {"bytes_per_launch": 2 * fetch + write, "fetch_size_bytes": fetch, "write_size_bytes": write,
+            "grbm_gui_active": res["GRBM_GUI_ACTIVE"],
+            "pass_seconds": [round(res["fetch_pass_s"], 1), round(res["write_pass_s"], 1)]}, None
+
+
 def run_polymul(args, comm, world, rank, local_rank):
     import numpy as np
 
@@ -423,6 +482,24 @@ def run_polymul(args, comm, world, rank, local_rank):
             ent["hbm_frac"] = ent["hbm_GBs"] / HBM_PEAK_GBS
         kroof[k] = ent
     traffic = sum(v for v in pmc.values() if v) if all(pmc.values()) else None
+    traffic_source = "profiles/pmc_traffic.json (committed rocprofv3 --pmc passes, not this run)"
+    traffic_committed = traffic
+    live = None
+    if rank == 0 and world == 1 and not args.no_live_pmc and len(kernels) == 1:
+        (kname,) = kernels
+        kre = {"mf_mul": r"\bk_mf_mul\(", "plane_fused": r"\bk_plane_fused(_slots)?\(",
+               "whole_mul": r"\bk_row<unsigned (int|long), 2, \d+, (true|false), true>"}.get(kname)
+        if kre:
+            live, why = live_pmc(args, kre)
+            if live:
+                traffic = live["bytes_per_launch"]
+                traffic_source = ("live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes of this "
+                                  "workload in this run, 2 x FETCH_SIZE + WRITE_SIZE per launch")
+                # the kernel's clock under the counter pass: GRBM_GUI_ACTIVE
+                # (summed over the 8 XCDs) over this run's HIP-event launch time
+                live["clock_ghz_est"] = live["grbm_gui_active"] / 8 / (kernels[kname]["avg_ms"] * 1e6)
+            else:
+                live = {"error": why}
     roofline = {
         "bound": "hbm",
         "kernel": "rnt_mul (" + " + ".join(kernels) + ")",
@@ -433,7 +510,10 @@ def run_polymul(args, comm, world, rank, local_rank):
         # HBM bytes per rnt_mul from the committed PMC passes of this shape
         # (profiles/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per kernel)
         "traffic": traffic,
-        "traffic_source": "profiles/pmc_traffic.json (committed rocprofv3 --pmc passes, not this run)",
+        "traffic_source": traffic_source,
+        "traffic_committed": traffic_committed,
+        "traffic_live": live,
+        "traffic_ratio": traffic / op_bytes if traffic else None,
         "alg_bytes_per_launch": op_bytes,
         "launch_ms": op_ms,
         "launches": launches,

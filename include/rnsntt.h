@@ -95,6 +95,12 @@ int rnt_device_count(int* n);
 int rnt_profile_enable(const rnt_ctx* ctx, int enable);
 int rnt_profile_read(const rnt_ctx* ctx, const char* kernel, uint64_t* launches,
                      double* total_ms);
+/* Test hook for the deferred-error path: records a failed cleanup call
+ * (HIP error `hip_error`, named "rnt_debug_defer") on the calling thread,
+ * as a block leaving the device cache would.  The next launch on the thread
+ * reports it as RNT_ERR_DEVICE; free / destroy / trim entry points report
+ * only their own cleanup failures and leave it pending. */
+int rnt_debug_defer(int hip_error);
 
 /* ---- host-side number theory (no device needed) ----------------------- */
 /* is_ntt_friendly_prime (src/math/primes.rs:125-131); writes 0/1. */

@@ -7,6 +7,7 @@ from __future__ import annotations
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -215,3 +216,48 @@ def test_integration_rust_block_matches_header():
     for needed in ("rnt_to_coeffs", "rnt_mod_drop_last", "rnt_sub", "rnt_ctx_moduli",
                    "rnt_ctx_total_bits", "rnt_ctx_channel_count"):
         assert needed in r
+
+
+# ---- the Makefile's dependency lists against the sources' #include lines ---
+
+def _local_includes(path, seen=None):
+    """Every header `path` includes with #include "...", transitively, as
+    repo-relative paths."""
+    import re
+
+    seen = set() if seen is None else seen
+    base = os.path.dirname(path)
+    for line in open(path):
+        m = re.match(r'\s*#\s*include\s+"([^"]+)"', line)
+        if not m:
+            continue
+        h = os.path.normpath(os.path.join(base, m.group(1)))
+        rel = os.path.relpath(h, REPO)
+        if rel not in seen:
+            seen.add(rel)
+            _local_includes(h, seen)
+    return seen
+
+
+def test_makefile_dependencies_match_includes():
+    """a `make` build must rebuild an object when any
+    header it includes changes, so each DEP_<tu> list in the Makefile equals
+    the transitive closure of that translation unit's #include lines, every
+    TU build() compiles has one, and `all` runs the ISA hazard check."""
+    import re
+
+    sys.path.insert(0, REPO)
+    import __graft_entry__ as ge
+
+    mk = open(os.path.join(REPO, "Makefile")).read().replace("\\\n", " ")
+    deps = {m.group(1): set(m.group(2).split()) for m in re.finditer(r"^DEP_(\w+)\s*:=\s*(.*)$", mk, re.M)}
+    for src in ge.SOURCES:
+        tu = os.path.splitext(src)[0]
+        assert tu in deps, f"Makefile has no DEP_{tu}"
+        want = _local_includes(os.path.join(ge.CSRC, src))
+        got = {d.replace("$(CSRC)", "toy-heaan-ckks_amd/csrc") for d in deps[tu]}
+        assert got == want, f"DEP_{tu}: Makefile {sorted(got)} vs #include closure {sorted(want)}"
+        assert re.search(rf"^\$\(LIBDIR\)/{tu}\.o:\s*\$\(CSRC\)/{re.escape(src)}\s+\$\(DEP_{tu}\)\s*$", mk, re.M), tu
+    all_line = re.search(r"^all:(.*)$", mk, re.M).group(1)
+    assert "isa_check.ok" in all_line
+    assert re.search(r"^\t.*tools/isa_check\.py \$\(OBJS\)", mk, re.M)

@@ -378,3 +378,28 @@ def test_graph_records_share_one_keyswitch_workspace(gpu):
     g.replay()
     Bd.sync()
     assert np.array_equal(outs[1][0].channels(), v0)
+
+
+def test_deferred_failure_survives_an_intervening_free(gpu):
+    """a free / destroy reports only its own cleanup failures.  A
+    failure deferred earlier on the thread (rnt_debug_defer stands in for a
+    block that failed to leave the cache) is neither consumed nor blamed by
+    an intervening rnt_buf_free -- whose status the bindings' __del__ drops
+    -- and reaches the next launch, which reports it and does not run."""
+    rn = gpu
+    lib = rn.load()
+    n, L = 1 << 12, 2
+    mod = rn.generate_primes(31, L, n)
+    Bd = rn.RnsBasis(mod, n)
+    x = rn.RnsPoly.from_channels(_rand(np.random.default_rng(3), mod, n, 2), Bd)
+    tmp = rn.RnsPoly(Bd, 4)
+    Bd.sync()
+    assert lib.rnt_debug_defer(1) == 0  # hipErrorInvalidValue, deferred
+    assert lib.rnt_buf_free(tmp.handle) == 0  # its own cleanup succeeded: OK, not the earlier failure
+    tmp._h = None
+    with pytest.raises(rn.RnsNttError) as e:
+        x.to_ntt_domain()
+    assert e.value.kind == "DeviceError" and "rnt_debug_defer" in str(e.value), str(e.value)
+    assert not x.is_ntt_domain()  # reported before any launch
+    x.to_ntt_domain()  # reported once: the next launch runs
+    assert x.is_ntt_domain()

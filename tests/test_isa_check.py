@@ -74,3 +74,48 @@ def test_overwrite_of_wide_store_data_is_flagged():
     assert kinds([st, "v_mov_b32_e32 v4, v126"]) == []
     assert kinds(["buffer_store_dwordx2 v[0:1], v94, s[20:23], s78 offen", "v_mov_b32_e32 v0, v126"]) == []
     assert kinds(["global_store_dwordx4 v[8:9], v[0:3], off", "v_mov_b32_e32 v2, 0"]) == ["S1"]
+
+
+def kinds_at(lines):
+    """Lines with addresses (4 bytes apart from 0x100) so branch targets
+    `<k+0xADDR>` resolve; function base 0."""
+    body = [(0x100 + 4 * i, t) for i, t in enumerate(lines)]
+    return sorted({k for k, _, _ in ic.check_kernel(body, 0)})
+
+
+def test_loop_carried_wide_store_hazard_is_caught():
+    # the store is the last instruction of the loop body; the loop head's
+    # first instruction rewrites its data: a hazard only along the back edge
+    loop = ["v_mov_b32_e32 v0, v126",                                  # 0x100: loop head
+            "v_add_u32_e32 v5, v5, v6",
+            "buffer_store_dwordx4 v[0:3], v94, s[20:23], s78 offen",   # 0x108
+            "s_cbranch_scc1 65533 <k+0x100>",                          # back to the head
+            "s_endpgm"]
+    assert kinds_at(loop) == ["S1"]
+    # two wait states at the loop head: clean
+    safe = ["s_nop 1", "v_mov_b32_e32 v0, v126", "buffer_store_dwordx4 v[0:3], v94, s[20:23], s78 offen",
+            "s_cbranch_scc1 65533 <k+0x100>", "s_endpgm"]
+    assert kinds_at(safe) == []
+
+
+def test_loop_carried_mfma_and_load_hazards_are_caught():
+    # an MFMA issued at the loop's end, its D read at the head
+    mf = ["v_add_u32_e32 v40, v0, v1", "s_nop 7", "s_nop 1",
+          f"{MF} v[0:3], v[10:13], v[90:93], 0",
+          "s_cbranch_scc1 65532 <k+0x100>", "s_endpgm"]
+    assert "M1" in kinds_at(mf)
+    # a load issued at the loop's end and waited for only after the head read it
+    ld = ["v_mov_b32_e32 v6, v5", "s_waitcnt vmcnt(0)", "buffer_load_dword v5, v1, s[4:7], 0 offen",
+          "s_cbranch_scc1 65533 <k+0x100>", "s_endpgm"]
+    assert kinds_at(ld) == ["L1"]
+    ld_ok = ["s_waitcnt vmcnt(0)", "v_mov_b32_e32 v6, v5", "buffer_load_dword v5, v1, s[4:7], 0 offen",
+             "s_cbranch_scc1 65533 <k+0x100>", "s_endpgm"]
+    assert kinds_at(ld_ok) == []
+
+
+def test_loop_states_converge_with_a_load_issued_every_iteration():
+    # a load re-issued each iteration and waited at the head: a fixpoint,
+    # no X1 and no finding
+    lines = ["s_waitcnt vmcnt(0)", "v_add_u32_e32 v6, v5, v6", "buffer_load_dword v5, v1, s[4:7], 0 offen",
+             "buffer_store_dword v6, v1, s[4:7], 0 offen", "s_cbranch_scc1 65532 <k+0x100>", "s_endpgm"]
+    assert kinds_at(lines) == []

@@ -36,6 +36,10 @@ touches any register an MFMA reads or writes until W_D = 8 states after the
 LAST MFMA of a tile has issued, an MFMA's D never overlaps its A/B, and an
 MFMA operand written by VALU / memory is 2+ states old at issue.
 
+  X1  a kernel with loops whose loop-carried states (in-flight MFMAs, wide
+      stores, un-waited loads) do not reach a fixpoint: back edges are
+      followed, so a loop-carried hazard is checked like a straight-line one.
+
 Exit status 1 if any finding; `--allow KERNEL_SUBSTR` skips kernels.
 Usage: isa_check.py OBJ.o [OBJ.o ...] [--verbose]
 """
@@ -184,20 +188,25 @@ BRANCHES = ("s_branch", "s_cbranch_")
 
 class State:
     """What is in flight at one point of the code: MFMAs (issue counter,
-    D, operands), un-waited loads, and the last VALU write of each register.
-    Counters are wait-state counts along the path."""
+    D, operands), wide stores still reading their data, un-waited loads and
+    stores, and the last VALU write of each register.  Counters are
+    wait-state counts along the path.  Un-waited memory ops are kept as
+    op -> depth, the number of ops of the same counter issued after it
+    (`s_waitcnt vmcnt(n)` retires exactly the ops of depth >= n: returns are
+    in order); where paths join, an op keeps its smallest depth (pending on
+    any path means pending), so the state is path-insensitive and finite."""
 
     def __init__(self):
         self.mfmas = []        # dict(end, dst, srcs, text)
         self.stores = []       # dict(end, data, text): wide VMEM stores still reading their data
-        self.alts = [[]]       # per incoming path: un-waited ops (kind, regs, text, is_smem)
+        self.pend = {}         # (kind, regs, text) -> depth
         self.last_write = {}   # reg -> counter after the write
 
     def copy(self):
         t = State()
         t.mfmas = [dict(f) for f in self.mfmas]
         t.stores = [dict(f) for f in self.stores]
-        t.alts = [list(a) for a in self.alts]
+        t.pend = dict(self.pend)
         t.last_write = dict(self.last_write)
         return t
 
@@ -213,28 +222,56 @@ class State:
         self.mfmas += [f for f in o.mfmas if (f["text"], f["end"]) not in seen]
         seen = {(f["text"], f["end"]) for f in self.stores}
         self.stores += [f for f in o.stores if (f["text"], f["end"]) not in seen]
-        for a in o.alts:
-            if a not in self.alts:
-                self.alts.append(list(a))
+        for k, dpt in o.pend.items():
+            self.pend[k] = min(dpt, self.pend.get(k, dpt))
         for r, v in o.last_write.items():
             self.last_write[r] = max(v, self.last_write.get(r, -10**9))
 
 
-def check_kernel(body, func_addr, verbose=False):
-    """One pass over the kernel in address order; forward branches carry
+AGE_CAP = 64  # wait states after which nothing in State can still matter (W_D, W_SRC, W_IN, W_ST < 64)
+MAX_ITERS = 16
+VM_CAP = 64    # outstanding ops of one counter kept per path (vmcnt is a 6-bit counter)
+
+
+def _normalize(st: State, at: int) -> State:
+    """The state at a back-edge branch, ages relative to the branch (ends
+    made <= 0), with everything too old to matter dropped: a finite form, so
+    the loop iteration below reaches a fixpoint."""
+    t = st.shifted(-at)
+    t.mfmas = [f for f in t.mfmas if -f["end"] < AGE_CAP]
+    t.stores = [f for f in t.stores if -f["end"] < W_ST]
+    t.last_write = {r: v for r, v in t.last_write.items() if -v < W_IN}
+    return t
+
+
+def _signature(st: State):
+    return (frozenset((f["text"], f["end"]) for f in st.mfmas),
+            frozenset((f["text"], f["end"]) for f in st.stores),
+            frozenset(st.pend.items()),
+            frozenset(st.last_write.items()))
+
+
+def _scan(body, func_addr, back_in):
+    """One pass over the kernel in address order.  Forward branches carry
     their state to the target (merged with the fall-through path); back
-    edges are not followed (the checked kernels are straight-line)."""
+    edges carry theirs (normalized) into the next pass through `back_in`.
+    Returns the findings and the back-edge states this pass produced."""
     findings = []
+    back_out = {}
     st = State()
     pending = {}  # target addr -> list of (State, counter at the branch)
     since = 0
     live = True   # the fall-through path reaches this instruction
     for idx, (addr, txt) in enumerate(body):
-        if addr in pending:
-            arrivals = pending.pop(addr)
+        arrivals = list(pending.pop(addr, [])) if addr is not None else []
+        if addr is not None and addr in back_in:
+            arrivals.append((back_in[addr], 0))  # normalized: ages relative to its branch
+        if arrivals:
             base = st if live else None
             for s_b, c_b in arrivals:
-                moved = s_b.shifted(since - c_b - 1)
+                # the taken branch counts as its one wait state (already in
+                # c_b), nothing more: conservative
+                moved = s_b.shifted(since - c_b)
                 if base is None:
                     base = moved
                 else:
@@ -242,7 +279,7 @@ def check_kernel(body, func_addr, verbose=False):
             st = base
             live = True
         if not live:
-            st = State()  # unreachable in this scan (a back-edge target)
+            st = State()  # reached by no path in this scan
             live = True
         mn, ops, rest = split_ops(txt)
         d, u = defs_uses(mn, ops)
@@ -255,14 +292,11 @@ def check_kernel(body, func_addr, verbose=False):
                 if key not in cnts:
                     continue
                 n = cnts[key]
-                for ai, alt in enumerate(st.alts):
-                    ops_k = [o for o in alt if o[0] == kind]
-                    keep = [] if n == 0 else (ops_k[len(ops_k) - n:] if n < len(ops_k) else ops_k)
-                    st.alts[ai] = [o for o in alt if o[0] != kind] + keep
+                st.pend = {o: dp for o, dp in st.pend.items() if o[0] != kind or dp < n}
         elif not mn.startswith("s_"):
             touched = d | u
             lk0 = load_kind(mn)
-            for o in {o for alt in st.alts for o in alt}:
+            for o in st.pend:
                 if lk0 == o[0] and not (o[1] & u):
                     continue  # a later load of the same counter: returns in order, lands last
                 if o[1] and (o[1] & touched):
@@ -271,16 +305,17 @@ def check_kernel(body, func_addr, verbose=False):
         sk = store_kind(mn)
         op = None
         if mn.startswith("s_load") or mn.startswith("s_buffer_load"):
-            op = ("lgkm", frozenset(), f"{idx}: " + txt.split("//")[0].strip(), True)
+            op = ("lgkm", frozenset(), f"{idx}: " + txt.split("//")[0].strip())
         elif lk:
-            op = (lk, frozenset(d), f"{idx}: " + txt.split("//")[0].strip(), False)
+            op = (lk, frozenset(d), f"{idx}: " + txt.split("//")[0].strip())
         elif sk:
-            op = (sk, frozenset(), f"{idx}: " + txt.split("//")[0].strip(), False)
+            op = (sk, frozenset(), f"{idx}: " + txt.split("//")[0].strip())
         if op:
-            for alt in st.alts:
-                alt.append(op)
-        if len(st.alts) > 16:  # bound the path count: keep the longest lists
-            st.alts = sorted(st.alts, key=len)[-16:]
+            # one more op behind every pending op of its counter; beyond
+            # VM_CAP the counter cannot hold them: those have retired
+            st.pend = {o: dp + (o[0] == op[0]) for o, dp in st.pend.items()
+                       if dp + (o[0] == op[0]) < VM_CAP}
+            st.pend[op] = 0
         # ---- MFMA rules
         is_mf = mn.startswith("v_mfma")
         if is_mf:
@@ -323,7 +358,7 @@ def check_kernel(body, func_addr, verbose=False):
         st.stores = [f for f in st.stores if since - f["end"] < W_ST]
         if is_mf:
             st.mfmas.append({"end": since, "dst": vset(ops[:1]), "srcs": vset(ops[1:]), "text": txt.split("//")[0].strip()})
-        st.mfmas = [f for f in st.mfmas if since - f["end"] < 64]
+        st.mfmas = [f for f in st.mfmas if since - f["end"] < AGE_CAP]
         if mn.startswith("v_") and not is_mf:
             for r in d:
                 st.last_write[r] = since
@@ -334,11 +369,50 @@ def check_kernel(body, func_addr, verbose=False):
                 tgt = func_addr + int(m.group(1), 16)
                 if addr is None or tgt > addr:
                     pending.setdefault(tgt, []).append((st.copy(), since))
+                else:  # back edge: into the next pass, at the loop head
+                    nb = _normalize(st, since)
+                    if tgt in back_out:
+                        back_out[tgt].merge(nb)
+                    else:
+                        back_out[tgt] = nb
             if mn == "s_branch":
                 live = False
         elif mn in ("s_setpc_b64", "s_endpgm"):
             live = False
-    return findings
+    return findings, back_out
+
+
+def check_kernel(body, func_addr, verbose=False):
+    """Every path of the kernel, loops included: passes over the code in
+    address order, each feeding the states its back edges carry to their
+    loop heads into the next, until those states stop changing (a fixpoint:
+    every loop-carried hazard -- an MFMA, a wide store or a load still in
+    flight across the back edge -- has then reached the loop body).  The
+    findings of every pass are reported; a kernel whose loop states do not
+    converge within MAX_ITERS passes is itself a finding (X1), so a looping
+    kernel is never passed unchecked."""
+    back_in = {}
+    found = {}
+    for _ in range(MAX_ITERS):
+        fs, back_out = _scan(body, func_addr, back_in)
+        for f in fs:
+            found.setdefault((f[0], f[1], f[2]), f)
+        merged = {}
+        for tgt in set(back_in) | set(back_out):
+            m = back_in[tgt].copy() if tgt in back_in else None
+            if tgt in back_out:
+                if m is None:
+                    m = back_out[tgt].copy()
+                else:
+                    m.merge(back_out[tgt])
+            merged[tgt] = m
+        if {t: _signature(v) for t, v in merged.items()} == {t: _signature(v) for t, v in back_in.items()}:
+            break
+        back_in = merged
+    else:
+        found[("X1", 0, "loop states did not converge")] = (
+            "X1", 0, f"loop-carried states did not converge in {MAX_ITERS} passes")
+    return sorted(found.values(), key=lambda f: (f[1], f[0]))
 
 
 def main(argv):

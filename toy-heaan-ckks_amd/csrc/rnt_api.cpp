@@ -98,7 +98,16 @@ const char* const kKernelNames[rnt::K_COUNT] = {
     "automorphism", "ks_decompose", "ks_rows", "tensor_rows", "import", "export", "crt",
     "sfft", "sample", "copy", "plane_fused", "mf_ntt_fwd", "mf_ntt_inv", "whole_fwd", "whole_inv", "whole_mul", "ks_whole", "tensor_whole", "mf_tensor", "mf_mul"};
 
-inline void cleanup(hipError_t e, const char* where);
+// A profiling call failed: clear the runtime's slot, keep the first failure
+// in the profiler, and stop profiling (rnt_profile_read reports it).
+void prof_fail(rnt::Prof* p, hipError_t e, const char* where) {
+  (void)hipGetLastError();
+  if (p->err == hipSuccess) {
+    p->err = e;
+    p->err_where = where;
+  }
+  p->on = false;
+}
 hipEvent_t prof_event(rnt::Prof* p) {
   if (!p->pool.empty()) {
     hipEvent_t e = p->pool.back();
@@ -107,7 +116,7 @@ hipEvent_t prof_event(rnt::Prof* p) {
   }
   hipEvent_t e = nullptr;
   if (const hipError_t r = hipEventCreate(&e); r != hipSuccess) {
-    cleanup(r, "hipEventCreate(profile)");
+    prof_fail(p, r, "hipEventCreate(profile)");
     return nullptr;
   }
   return e;
@@ -145,6 +154,26 @@ int take_deferred() {
               hipGetErrorString(d.e));
 }
 
+// A free / destroy / trim entry point reports only the failures of its own
+// cleanup calls: a failure some earlier call deferred stays pending for the
+// next launch (check_pending) instead of being consumed -- or blamed on the
+// free -- here.  Bindings may drop a free's status (a destructor, __del__);
+// an unrelated earlier failure then still reaches a status that is checked.
+struct OwnCleanup {
+  Deferred saved;
+  OwnCleanup() : saved(g_deferred) { g_deferred = {}; }
+  int finish() {
+    const Deferred mine = g_deferred;
+    g_deferred = saved;
+    saved = {};
+    if (mine.e == hipSuccess) return RNT_OK;
+    return fail(RNT_ERR_DEVICE, "%s failed: %s", mine.where, hipGetErrorString(mine.e));
+  }
+  ~OwnCleanup() {
+    if (saved.e != hipSuccess && g_deferred.e == hipSuccess) g_deferred = saved;
+  }
+};
+
 // Before a launch: a deferred cleanup failure, or an error some earlier
 // runtime call on this thread left unreported in the last-error slot.
 int check_pending(int id) {
@@ -165,10 +194,26 @@ hipError_t prof_launch(const rnt::Tables* t, hipStream_t s, int id, F&& f) {
   if (p == nullptr || !p->on || g_capture != nullptr) return f();
   std::lock_guard<std::mutex> g(p->mu);
   hipEvent_t a = prof_event(p), b = prof_event(p);
-  if (a) cleanup(hipEventRecord(a, s), "hipEventRecord(profile)");
+  bool ok = a && b;
+  if (ok) {
+    if (const hipError_t r = hipEventRecord(a, s); r != hipSuccess) {
+      prof_fail(p, r, "hipEventRecord(profile)");
+      ok = false;
+    }
+  }
   hipError_t e = f();
-  if (b) cleanup(hipEventRecord(b, s), "hipEventRecord(profile)");
-  if (a && b) p->pending.push_back({id, a, b});
+  if (ok && e == hipSuccess) {
+    if (const hipError_t r = hipEventRecord(b, s); r != hipSuccess) {
+      prof_fail(p, r, "hipEventRecord(profile)");
+      ok = false;
+    }
+  }
+  if (ok && e == hipSuccess) {
+    p->pending.push_back({id, a, b});
+  } else {
+    if (a) p->pool.push_back(a);
+    if (b) p->pool.push_back(b);
+  }
   return e;
 }
 
@@ -780,8 +825,9 @@ static void ctx_release(const rnt_ctx* ctx) {
 static void ctx_retain(const rnt_ctx* ctx) { const_cast<rnt_ctx*>(ctx)->refs.fetch_add(1); }
 
 extern "C" int rnt_ctx_destroy(rnt_ctx* ctx) {
+  OwnCleanup own;
   ctx_release(ctx);  // freed once its last buffer is freed too
-  return take_deferred();
+  return own.finish();
 }
 
 extern "C" int rnt_ctx_drop_last(const rnt_ctx* ctx, size_t drop_count, rnt_ctx** out) {
@@ -959,6 +1005,7 @@ extern "C" int rnt_graph_launch(rnt_graph* g) {
 
 extern "C" int rnt_graph_destroy(rnt_graph* g) {
   if (!g) return RNT_OK;
+  OwnCleanup own;
   cleanup(hipSetDevice(g->device), "hipSetDevice(rnt_graph_destroy)");
   // a replay may still be running: the blocks go back to the cache behind
   // the context's current stream, made to wait for the last replay first
@@ -969,7 +1016,7 @@ extern "C" int rnt_graph_destroy(rnt_graph* g) {
   if (g->graph) cleanup(hipGraphDestroy(g->graph), "hipGraphDestroy");
   if (g->done) cleanup(hipEventDestroy(g->done), "hipEventDestroy(rnt_graph_destroy)");
   delete g;
-  return take_deferred();
+  return own.finish();
 }
 
 extern "C" int rnt_graph_workspace(const rnt_graph* g, size_t* blocks, size_t* bytes) {
@@ -1028,6 +1075,7 @@ extern "C" int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out) 
 // context stream, behind every op queued on this buffer.
 extern "C" int rnt_buf_free(rnt_buf* b) {
   if (!b) return RNT_OK;
+  OwnCleanup own;
   if (b->ctx) {
     const int dev = b->ctx->t->device;
     hipStream_t s = b->ctx->t->stream;
@@ -1038,13 +1086,20 @@ extern "C" int rnt_buf_free(rnt_buf* b) {
   }
   ctx_release(b->ctx);
   delete b;
-  return take_deferred();
+  return own.finish();
+}
+
+extern "C" int rnt_debug_defer(int hip_error) {
+  if (hip_error == 0) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_debug_defer: hip_error must be nonzero");
+  cleanup(static_cast<hipError_t>(hip_error), "rnt_debug_defer");
+  return RNT_OK;
 }
 
 extern "C" int rnt_pool_trim(int device, size_t* freed_bytes) {
+  OwnCleanup own;
   const size_t f = pool_drain(device);
   if (freed_bytes) *freed_bytes = f;
-  return take_deferred();
+  return own.finish();
 }
 
 extern "C" int rnt_buf_wrap(const rnt_ctx* ctx, void* device_ptr, size_t n_polys, int in_ntt,
@@ -2192,7 +2247,7 @@ extern "C" int rnt_profile_read(const rnt_ctx* ctx, const char* kernel, uint64_t
       t->prof->launches[r.id] += 1;
       t->prof->ms[r.id] += ms;
     } else {
-      cleanup(e, "hipEventElapsedTime(profile)");
+      prof_fail(t->prof, e, "hipEventElapsedTime(profile)");
     }
     t->prof->pool.push_back(r.a);
     t->prof->pool.push_back(r.b);
@@ -2200,5 +2255,12 @@ extern "C" int rnt_profile_read(const rnt_ctx* ctx, const char* kernel, uint64_t
   t->prof->pending.clear();
   *launches = t->prof->launches[id];
   *total_ms = t->prof->ms[id];
-  return take_deferred();
+  if (t->prof->err != hipSuccess) {
+    const hipError_t e = t->prof->err;
+    const char* where = t->prof->err_where;
+    t->prof->err = hipSuccess;
+    return fail(RNT_ERR_DEVICE, "%s failed: %s (profiling was turned off; the launches ran)", where,
+                hipGetErrorString(e));
+  }
+  return RNT_OK;
 }

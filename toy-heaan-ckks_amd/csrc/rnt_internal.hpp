@@ -134,6 +134,11 @@ struct Prof {
   std::vector<hipEvent_t> pool;
   uint64_t launches[K_COUNT] = {};
   double ms[K_COUNT] = {};
+  // the first failure of a profiling call (event create / record / elapsed
+  // time): profiling turns itself off and rnt_profile_read reports it; it
+  // never aborts or fails a launch
+  hipError_t err = hipSuccess;
+  const char* err_where = nullptr;
 };
 
 }  // namespace rnt

@@ -210,6 +210,10 @@ __device__ __forceinline__ int32_t recomb(int32_t c0, int32_t c1, int32_t c2, in
 // |a|, |b| < q < 2^31: |a b + m q| < q^2 + 2^31 q < 2^63 and the result lies
 // in (-q, q); the bias K only adds to the high word (its low word is 0), so
 // a wrap of the 64-bit sum does not change the returned word mod 2^32.
+// Where the result is handed on in the packed byte form (k_mf_mul's
+// product), the operands are pass outputs, |a|, |b| < q/2 + 2^14, so
+// |v| < (q/2 + 2^14)^2 / 2^32 + q/2 + 1 < 5q/8 + 1 < 0x7F7F7F7F, inside the
+// packed range [-0x80808080, 0x7F7F7F7F] (mf_build checks it per prime).
 template <bool WK>
 __device__ __forceinline__ int32_t mont(int32_t a, int32_t b, const Mc& m) {
   // one v_mad_i64_i32 (left to itself hipcc widens a -- the high word of
@@ -1141,7 +1145,7 @@ static_assert(kMulLdsBase * 4 + (size_t)kMulLdsTiles * 16 * 1024 <= mf::kLdsByte
 // be a or b: every wave has read its words of both before the exchange
 // barriers that precede the inverse's stores.
 __global__ void __launch_bounds__(mf::kT, 1)
-k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_t ls, uint32_t* __restrict__ scratch,
+k_mf_mul(uint32_t* c, const uint32_t* a, const uint32_t* b, uint64_t ls, uint32_t* __restrict__ scratch,
          uint32_t slots, const void* __restrict__ mft, const LimbConst<uint32_t>* __restrict__ lcs) {
   using namespace mf;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1184,10 +1188,11 @@ k_mf_mul(uint32_t* __restrict__ c, const uint32_t* a, const uint32_t* b, uint64_
     const v4i ah = cc >= 16 - kMulLdsTiles ? hat(cc - (16 - kMulLdsTiles)) : bld(RS, p4_lane(h), p4_soff(h, cc));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      // (a^ 2^32) b^ 2^-32, a signed Montgomery product of two signed
-      // representatives (|a^|, |b^| < q < 2^31: |a b| + |m q| < 2^63, the
-      // result in (-q, q)): the exact product, in the packed signed form
-      // the inverse's first pass takes as it is (inv_x<false, true>)
+      // (a^ 2^32) b^ 2^-32, a signed Montgomery product of two pass
+      // outputs (|a^|, |b^| < q/2 + 2^14, so |v| < 5q/8 + 1, inside the
+      // packed range; mont() and mf_build): the exact product, in the
+      // packed signed form the inverse's first pass takes as it is
+      // (inv_x<false, true>)
       xx[p3(cc, i)] = (uint32_t)mont<true>(ah[i], r[i], T.m) ^ K32;
     }
     // computed here: left free, hipcc sinks each reduction to the inverse's
@@ -1261,6 +1266,17 @@ int mf_build(Tables* t, std::string* err) {
       itw[g] = ipw[brv(g, 16)];
     }
     const uint64_t R = (uint64_t)(((host::u128)1 << 32) % q);
+    // k_mf_mul hands its product to the inverse in the packed byte form:
+    // with pass outputs |r| < q/2 + 2^14 the Montgomery product's bound
+    // (q/2 + 2^14)^2 / 2^32 + q/2 + 1 must stay inside [-0x80808080,
+    // 0x7F7F7F7F] (mont(); holds for every q < 2^31)
+    {
+      const double rb = (double)q / 2 + 16384.0;
+      if (rb * rb / 4294967296.0 + (double)q / 2 + 1 >= (double)0x7F7F7F7Fu) {
+        *err = "MFMA tables: the product bound exceeds the packed digit range for this prime";
+        return -1;
+      }
+    }
     // pass 0's matrix by running its four CT stages on unit vectors
     uint64_t M0[16][16];
     for (int k = 0; k < 16; ++k) {

@@ -92,6 +92,7 @@ SIGNATURES = {
     "rnt_device_count": (c_int, [POINTER(c_int)]),
     "rnt_profile_enable": (c_int, [_P, c_int]),
     "rnt_profile_read": (c_int, [_P, c_char_p, POINTER(c_uint64), POINTER(ctypes.c_double)]),
+    "rnt_debug_defer": (c_int, [c_int]),
     "rnt_is_ntt_friendly_prime": (c_int, [c_uint64, c_uint64, POINTER(c_int)]),
     "rnt_generate_primes": (c_int, [c_uint32, c_size_t, c_uint64, _U64P]),
     "rnt_find_psi": (c_int, [c_uint64, c_uint64, _U64P]),
