@@ -76,6 +76,37 @@ def test_config4_ct_mul_relin_rescale_two_chunks(gpu):
     assert np.array_equal(o0[tile[0]], o0[tile[-1]]) and np.array_equal(o1[tile[0]], o1[tile[-1]])
 
 
+def test_config4_full_1024_ct_batch(gpu):
+    """BASELINE config 4 at its stated batch: 1024 ciphertext pairs through
+    mul_ciphertexts_gadget (engine.rs:473-539) + rescale_ciphertext
+    (engine.rs:263-282) in one call, i.e. 16 key-switch chunks of 64.  The
+    operands are drawn on the device (Philox, rnt_sample_uniform: 32 GiB of
+    host data otherwise); the chunk-boundary ciphertexts 0, 63, 64 and the
+    last, 1023, are read back with their inputs and checked against the
+    oracle."""
+    rn = gpu
+    n, L, B = 1 << 16, 16, 1024
+    mod = rn.generate_primes(31, L, n)
+    Bd, Bo = rn.RnsBasis(mod, n), orc.Basis(mod, n)
+    drng = rn.DeviceRng(1024)
+    c0, c1, c0p, c1p = (rn.RnsPoly.sample_uniform(Bd, drng, B) for _ in range(4))
+    rng = np.random.default_rng(1025)
+    ka, kb = _rand(rng, mod, n, L), _rand(rng, mod, n, L)
+    rlk = rn.RnsGadgetKey.from_channels(ka, kb, Bd)
+    ct1 = rn.Ciphertext(c0, c1, 31, Bd.total_bits())
+    ct2 = rn.Ciphertext(c0p, c1p, 31, Bd.total_bits())
+    out = rn.mul_ciphertexts_gadget(ct1, ct2, rlk)
+    res = rn.rescale_ciphertext(out)
+    assert res.c0.basis.channel_count() == L - 1
+    for p in (0, 63, 64, B - 1):
+        x0, x1, y0, y1 = (t.channels_of(p)[0] for t in (c0, c1, c0p, c1p))
+        w0, w1 = orc.mul_ciphertexts_gadget(Bo, x0, x1, y0, y1, ka, kb, threads=T)
+        assert np.array_equal(out.c0.channels_of(p)[0], w0), p
+        assert np.array_equal(out.c1.channels_of(p)[0], w1), p
+        assert np.array_equal(res.c0.channels_of(p)[0], orc.rescale(Bo, w0)), p
+        assert np.array_equal(res.c1.channels_of(p)[0], orc.rescale(Bo, w1)), p
+
+
 @pytest.mark.parametrize("k", [1, -3, 1 << 15])
 def test_config5_rotation_full_32_limbs(gpu, k):
     rn = gpu
