@@ -175,6 +175,10 @@ int rnt_graph_workspace(const rnt_graph* graph, size_t* blocks, size_t* bytes);
  * another stream (e.g. through rnt_buf_device_ptr) must order itself after
  * that stream or call rnt_sync first. */
 int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out);
+/* The same buffer with unspecified contents: for an op's output, which the
+ * op overwrites entirely (no zero fill queued; the reference has no such
+ * constructor -- RnsPoly::zero is rnt_buf_alloc). */
+int rnt_buf_alloc_uninit(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out);
 /* Frees without waiting for the device: the buffer's device blocks go to a
  * per-device cache behind an event on the context stream, and a later
  * allocation's stream waits on that event before reusing them. */

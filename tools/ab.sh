@@ -31,7 +31,7 @@ for i in $(seq 1 $REPS); do
     libname=${parts[0]}
     if [ "$libname" = base ]; then lib=toy-heaan-ckks_amd/lib/librnsntt.so; else lib=toy-heaan-ckks_amd/lib/variants/librnsntt_$libname.so; fi
     tag=$(echo "${AB_TAG:-}$v" | tr '+=' '__')
-    env RNSNTT_LIB=$lib "${parts[@]:1}" timeout -k 10 300 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline $POWER_ARG $BENCH_ARGS > gpurun_out/ab_${tag}_$i.json 2> gpurun_out/ab_${tag}_$i.err || exit $?
+    env RNSNTT_LIB=$lib "${parts[@]:1}" timeout -k 10 300 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-live-pmc $POWER_ARG $BENCH_ARGS > gpurun_out/ab_${tag}_$i.json 2> gpurun_out/ab_${tag}_$i.err || exit $?
   done
 done
 for v in $VARS; do tag=$(echo "${AB_TAG:-}$v" | tr '+=' '__'); echo "== $v" >&2; python3 tools/ab_summary.py gpurun_out/ab_${tag}_[0-9]*.json >&2; done

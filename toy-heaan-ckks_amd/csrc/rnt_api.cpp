@@ -750,7 +750,7 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
   // the Python/C++ mirrors raise it before calling.
   if (log_n >= 63) return fail(RNT_ERR_BAD_ARGUMENT, "log_n %u out of range", log_n);
   const uint64_t n = 1ull << log_n;
-  bool wide = false, lazy30 = true;
+  bool wide = false, lazy30 = true, lazy62 = true;
   for (size_t i = 0; i < count; ++i) {
     if (!rnt::host::is_ntt_friendly(moduli[i], n))
       return fail_fields(RNT_ERR_NON_NTT_FRIENDLY, moduli[i], n,
@@ -760,6 +760,7 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
                   "modulus %" PRIu64 " >= 2^63 (the reference's add_mod overflows)", moduli[i]);
     if (moduli[i] >= (1ull << 31)) wide = true;
     if (moduli[i] >= (1ull << 30)) lazy30 = false;
+    if (moduli[i] >= (1ull << 62)) lazy62 = false;
   }
   // a valid basis the reference would accept, beyond this backend's tables
   // and grids: its own capacity status, not the reference's InvalidDegree
@@ -779,6 +780,9 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     t->wide = wide ? 1 : 0;
     // RNT_LAZY30=0 keeps the canonical product path for 30-bit bases (A/B)
     t->lazy30 = !wide && lazy30 && env_long("RNT_LAZY30", 1) != 0;
+    // the same Harvey-lazy product path for u64 bases of primes < 2^62 (the
+    // reference's 40/61/62-bit tests); RNT_LAZY62=0 keeps the canonical one
+    t->lazy62 = wide && lazy62 && env_long("RNT_LAZY62", 1) != 0;
     // the whole-plane product and MFMA transforms are the default where they
     // apply (N = 2^16, u32); RNT_PLANE=0 keeps the four-step kernels
     t->plane = env_long("RNT_PLANE", 1) != 0 ? 1 : 0;
@@ -1037,7 +1041,20 @@ extern "C" int rnt_sync(const rnt_ctx* ctx) {
 // ---------------------------------------------------------------------------
 // buffers
 // ---------------------------------------------------------------------------
+static int buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out, bool zero);
+
 extern "C" int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out) {
+  return buf_alloc(ctx, n_polys, out, true);
+}
+
+// An op's output buffer: the op overwrites every word, so the zero fill
+// (a fill kernel of the whole buffer on the stream: 33 us per 16 MiB, two
+// per ct-mul chunk for the tensor's d0^/d1^) is skipped.
+extern "C" int rnt_buf_alloc_uninit(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out) {
+  return buf_alloc(ctx, n_polys, out, false);
+}
+
+static int buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out, bool zero) {
   if (!ctx || !out) return fail(RNT_ERR_BAD_ARGUMENT, "null argument");
   *out = nullptr;
   if (n_polys == 0) return fail(RNT_ERR_BAD_ARGUMENT, "n_polys must be positive");
@@ -1060,7 +1077,7 @@ extern "C" int rnt_buf_alloc(const rnt_ctx* ctx, size_t n_polys, rnt_buf** out) 
     return hip_fail(e, "hipMalloc(buffer)");
   }
   // zero (RnsPoly::zero), queued on the context stream like every op
-  e = hipMemsetAsync(b->data, 0, bytes, s);
+  if (zero) e = hipMemsetAsync(b->data, 0, bytes, s);
   if (e != hipSuccess) {
     pool_give(ctx->t->device, b->data, b->data_bytes, s);
     ctx_release(ctx);
@@ -1331,7 +1348,8 @@ extern "C" int rnt_mul(rnt_buf* out, const rnt_buf* a, const rnt_buf* b) {
     return RNT_OK;
   }
   if (int rc = ensure_ws(out, poly_words(out) * word_bytes(k.t))) return rc;
-  // lazy: the Harvey 30-bit variant when every q < 2^30 (Tables::lazy30)
+  // lazy: the Harvey variant when every q < 2^30 (u32, Tables::lazy30) or
+  // every q < 2^62 (u64, Tables::lazy62)
   LAUNCH(k.t, rnt::K_COL_FWD, rnt::launch_col_fwd(k, out->data, a->data, out->ws, b->data, ls, ls, true),
          "column forward");
   LAUNCH(k.t, rnt::K_ROW_MUL, rnt::launch_row(k, 2, out->data, out->ws, ls, true), "row mul");

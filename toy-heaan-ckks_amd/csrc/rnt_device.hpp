@@ -37,14 +37,16 @@ __device__ __forceinline__ Mod<W> mod_of(const LimbConst<W>& lc) {
   return Mod<W>{lc.q, (W)(W(0) - lc.q)};
 }
 
-// The product path's modulus bundle: LZ = Harvey-lazy 30-bit arithmetic
-// (rnt_modarith.hpp Mod30; u32 words and q < 2^30 only).
+// The product path's modulus bundle: LZ = Harvey-lazy arithmetic
+// (rnt_modarith.hpp Mod30: u32 words, q < 2^30; Mod62: u64 words, q < 2^62).
 template <class W, bool LZ>
 __device__ __forceinline__ auto mod_for(const LimbConst<W>& lc) {
-  static_assert(!LZ || sizeof(W) == 4, "lazy 30-bit arithmetic needs 32-bit words");
-  if constexpr (LZ) {
+  if constexpr (LZ && sizeof(W) == 4) {
     const uint32_t q = (uint32_t)lc.q;
     return Mod30{q, 0u - q, 2u * q};
+  } else if constexpr (LZ) {
+    const uint64_t q = (uint64_t)lc.q;
+    return Mod62{q, 2ull * q};
   } else {
     return mod_of(lc);
   }

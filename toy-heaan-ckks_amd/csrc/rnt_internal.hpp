@@ -80,7 +80,8 @@ struct CrtDev {
 struct Tables {
   int device = 0;
   int wide = 0;            // 0: W = u32, 1: W = u64
-  bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path
+  bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path (u32)
+  bool lazy62 = false;     // u64 words, every modulus < 2^62: the same for u64
   int plane = 0;           // the whole-plane kernels where they apply (plane_ok, mf_ok);
   int mf_mul = 1;          // rnt_mul at N = 2^16 on the matrix-core transforms (RNT_MF_MUL=0: k_plane_fused)
                            // RNT_PLANE=0: the four-step kernels everywhere
@@ -191,9 +192,9 @@ struct Launch {
 // k.B polys (a batch or a chunk of one) and k.L limbs are processed.
 // Forward column pass on up to two operands (in0->out0, in1->out1).
 // lazy (all three): the product path's Harvey-lazy 30-bit variant (q < 2^30,
-// see rnt_modarith.hpp Mod30) where lazy30_ok(); the intermediates between
+// see rnt_modarith.hpp Mod30) where lazy_ok(); the intermediates between
 // the three launches are then unreduced, the product's output canonical.
-bool lazy30_ok(const Tables* t);
+bool lazy_ok(const Tables* t);
 hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* out1,
                           const void* in1, uint64_t in_ls, uint64_t out_ls, bool lazy = false);
 // Row pass.  mode 0: forward rows (in place on x); 1: inverse rows (in place

@@ -369,6 +369,10 @@ constexpr int kRowMinWaves = 6;
 // ... and for the whole-plane u32 rows (two operand planes of 16 registers,
 // no spills at 128 VGPRs; the u64 rows are left unconstrained)
 constexpr int kWholeMinWaves = 4;
+// (RNT_KS_ROWS_WAVES: A/B builds of the four-step key-switch rows' bound)
+#ifndef RNT_KS_ROWS_WAVES
+#define RNT_KS_ROWS_WAVES 4
+#endif
 constexpr int kKsMinWaves = 4;
 // Key rows of the key-switch rows kernel go global -> LDS directly
 // (global_load_lds, no registers) for u32 rows of >= 64 words, except in the
@@ -667,11 +671,11 @@ constexpr bool trunc_mul() {
   return sizeof(W) == 4 && !LZ && Trunc<LOG_C>::on;
 }
 
-// rnt_mul runs the Harvey-lazy kernels exactly when lazy30_ok(); otherwise
+// rnt_mul runs the Harvey-lazy kernels exactly when lazy_ok(); otherwise
 // its u32 row kernel truncates when the row length allows (Trunc<LOG_C>).
-bool lazy30_ok(const Tables* t);
+bool lazy_ok(const Tables* t);
 bool mul_truncated(const Tables* t) {
-  if (t->wide || lazy30_ok(t)) return false;
+  if (t->wide || lazy_ok(t)) return false;
   const Geom g = geom_for(t->log_n);
   return g.log_c >= 4 && g.log_c % 4 == 0;
 }
@@ -685,9 +689,18 @@ bool mul_truncated(const Tables* t) {
 // after a truncated one) that the inverse column pass applies otherwise:
 // the product is one launch moving 3 planes per (poly, limb), a transform
 // one launch moving 2.
+// Minimum waves per SIMD of the u64 lazy (q < 2^62) product rows: 3 lets
+// them take up to 168 VGPRs; at 4 (128 VGPRs, 60 bytes a lane of spills at
+// 2^8-word rows) 2^16 x 16 x 62-bit ran 1.6% slower (41.10k against 41.75k
+// poly-muls/s, row kernel 2.99 against 2.92 ms, profiles/r06/ab_u64_waves.txt)
+#ifndef RNT_U64_LZ_WAVES
+#define RNT_U64_LZ_WAVES 3
+#endif
 template <class W, int MODE, int LOG_C, bool LZ = false, bool WHOLE = false>
 __global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? (WHOLE ? kWholeMinWaves : kRowMinWaves)
-                                                                 : (MODE == 2 && LOG_C >= (WHOLE ? 13 : 7) ? 4 : 1))
+                                                                 : (MODE == 2 && LOG_C >= (WHOLE ? 13 : 7)
+                                                                        ? (LZ && !WHOLE ? RNT_U64_LZ_WAVES : 4)
+                                                                        : 1))
 k_row(W* __restrict__ xg, const W* __restrict__ yg, W* __restrict__ outg, TabPtrs<W> tp, uint32_t log_n,
       uint32_t B, uint64_t ls, uint64_t rows_total) {
   using G = RowGeo<LOG_C>;
@@ -742,7 +755,7 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, W* __restrict__ outg, TabPtr
       if constexpr (G::P > 1) inv_pass<G, W, 1, 0, WHOLE>(z, rp.xp, lds, itw, mo, ft);
     } else {
     xf_fwd<G, W, 2>(v, rp.xp, lds, tw, mo);
-    if constexpr (LZ) {
+    if constexpr (LZ && sizeof(W) == 4) {
       // [0, 4q) inputs -> [0, 2q); a b < 4q^2 < q 2^32, so the Montgomery
       // quotient leaves (ab + mq) / 2^32 < 2q: the GS passes' input range
 #pragma unroll
@@ -752,6 +765,13 @@ k_row(W* __restrict__ xg, const W* __restrict__ yg, W* __restrict__ outg, TabPtr
         const uint32_t mm = (uint32_t)t * (0u - (uint32_t)lc.qinv);
         z[0][i] = (uint32_t)(mad64(mm, (uint32_t)lc.q, t) >> 32);
       }
+    } else if constexpr (LZ) {
+      // u64, q < 2^62: [0, 4q) -> [0, 2q) inputs; hi(a b) < 4q^2 / 2^64 < q
+      // and hi(m q) < q, so mont_mul's final sub_mod gives the canonical
+      // product (the GS passes take [0, 2q))
+#pragma unroll
+      for (int i = 0; i < E; ++i)
+        z[0][i] = mont_mul<W>(csub<W>(v[0][i], mo.q2), csub<W>(v[1][i], mo.q2), lc.q, lc.qinv);
     } else {
 #pragma unroll
       for (int i = 0; i < E; ++i) z[0][i] = mont_mul<W>(v[0][i], v[1][i], lc.q, lc.qinv);
@@ -872,7 +892,7 @@ __device__ __forceinline__ uint32_t mac_lazy(uint32_t acc, uint32_t x, uint32_t 
 // per source limb instead of three (S, then key_b, then key_a), and 2 key
 // words per thread instead of 2E (A/B: profiles/r02_ab_ks_rows.txt).
 template <class W, int LOG_C, int NP>
-__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kKsMinWaves : 1)
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? RNT_KS_ROWS_WAVES : 1)
 k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
           const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
           const W* __restrict__ init0, const W* __restrict__ init1, uint64_t init_ls,
@@ -1663,9 +1683,7 @@ static hipError_t whole_t(const Launch& k, int mode, void* out, void* x, const v
   case C:                                                                                             \
     if (mode == 0) return row_launch<W, 0, C, false, true>(k, x, nullptr, ls);                        \
     if (mode == 1) return row_launch<W, 1, C, false, true>(k, x, nullptr, ls);                        \
-    if constexpr (sizeof(W) == 4) {                                                                   \
-      if (lz) return row_launch<W, 2, C, true, true>(k, x, y, ls, out);                               \
-    }                                                                                                 \
+    if (lz) return row_launch<W, 2, C, true, true>(k, x, y, ls, out);                                 \
     return row_launch<W, 2, C, false, true>(k, x, y, ls, out);
   switch (k.t->log_n) {
     RNT_W(10)
@@ -1685,10 +1703,8 @@ static hipError_t row_t(const Launch& k, int mode, void* x, const void* y, uint6
 #define RNT_L1(C) return row_launch<W, 1, C>(k, x, y, ls)
 #define RNT_L2(C) return row_launch<W, 2, C>(k, x, y, ls)
 #define RNT_L2Z(C) return row_launch<W, 2, C, true>(k, x, y, ls)
-  if constexpr (sizeof(W) == 4) {
-    if (mode == 2 && lz) {
-      RNT_DISPATCH_LOGC(g.log_c, RNT_L2Z)
-    }
+  if (mode == 2 && lz) {
+    RNT_DISPATCH_LOGC(g.log_c, RNT_L2Z)
   }
   if (mode == 0) {
     RNT_DISPATCH_LOGC(g.log_c, RNT_L0)
@@ -2030,31 +2046,42 @@ static hipError_t tensor_rows_t(const Launch& k, void* d0hat, void* d1hat, void*
 // W dispatch -----------------------------------------------------------------
 #define RNT_WIDE(CALL32, CALL64) return k.t->wide ? (CALL64) : (CALL32)
 
-bool lazy30_ok(const Tables* t) {
-  return !t->wide && t->lazy30 && geom_for(t->log_n).log_r >= 5;
+// The Harvey-lazy product path: u32 words with every q < 2^30 (lazy30) or
+// u64 words with every q < 2^62 (lazy62), on the tiled column grids.
+bool lazy_ok(const Tables* t) {
+  return (t->wide ? t->lazy62 : t->lazy30) && geom_for(t->log_n).log_r >= 5;
 }
 hipError_t launch_col_fwd(const Launch& k, void* out0, const void* in0, void* out1,
                           const void* in1, uint64_t in_ls, uint64_t out_ls, bool lazy) {
-  if (lazy && lazy30_ok(k.t))
-    return col_fwd_t<uint32_t, true>(k, out0, in0, out1, in1, in_ls, out_ls);
-  RNT_WIDE((col_fwd_t<uint32_t, false>(k, out0, in0, out1, in1, in_ls, out_ls)),
-           (col_fwd_t<uint64_t, false>(k, out0, in0, out1, in1, in_ls, out_ls)));
+  const bool lz = lazy && lazy_ok(k.t);
+  if (k.t->wide)
+    return lz ? col_fwd_t<uint64_t, true>(k, out0, in0, out1, in1, in_ls, out_ls)
+              : col_fwd_t<uint64_t, false>(k, out0, in0, out1, in1, in_ls, out_ls);
+  return lz ? col_fwd_t<uint32_t, true>(k, out0, in0, out1, in1, in_ls, out_ls)
+            : col_fwd_t<uint32_t, false>(k, out0, in0, out1, in1, in_ls, out_ls);
 }
 hipError_t launch_row(const Launch& k, int mode, void* x, const void* y, uint64_t ls, bool lazy) {
-  const bool lz = lazy && lazy30_ok(k.t);
-  RNT_WIDE(row_t<uint32_t>(k, mode, x, y, ls, lz), row_t<uint64_t>(k, mode, x, y, ls, false));
+  const bool lz = lazy && lazy_ok(k.t);
+  RNT_WIDE(row_t<uint32_t>(k, mode, x, y, ls, lz), row_t<uint64_t>(k, mode, x, y, ls, lz));
 }
 hipError_t launch_whole(const Launch& k, int mode, void* out, void* x, const void* y, uint64_t ls) {
-  // the Harvey-lazy arithmetic where every modulus < 2^30 (as rnt_mul's four-step path)
-  const bool lz = !k.t->wide && k.t->lazy30;
-  RNT_WIDE(whole_t<uint32_t>(k, mode, out, x, y, ls, lz), whole_t<uint64_t>(k, mode, out, x, y, ls, false));
+  // the Harvey-lazy arithmetic where every modulus < 2^30 (u32 words), as
+  // rnt_mul's four-step path.  The u64 whole-plane product stays canonical:
+  // capped at 128 VGPRs its lazy form spills 240 bytes a lane at 2^13 (92
+  // canonical) and measured 6.3% slower at the horner_chain.rs shape,
+  // 2^13 x 7 x 61-bit (0.792M against 0.845M poly-muls/s, same box,
+  // profiles/r06/ab_lazy62.txt); the u64 four-step product takes it (+7.9%)
+  const bool lz = !k.t->wide && k.t->lazy30 != 0;
+  RNT_WIDE(whole_t<uint32_t>(k, mode, out, x, y, ls, lz), whole_t<uint64_t>(k, mode, out, x, y, ls, lz));
 }
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
                           uint64_t in_ls, int rfold, const void* addend, bool lazy) {
-  if (lazy && lazy30_ok(k.t))
-    return col_inv_t<uint32_t, true>(k, out, out_ls, in, in_ls, rfold, addend);
-  RNT_WIDE((col_inv_t<uint32_t, false>(k, out, out_ls, in, in_ls, rfold, addend)),
-           (col_inv_t<uint64_t, false>(k, out, out_ls, in, in_ls, rfold, addend)));
+  const bool lz = lazy && lazy_ok(k.t);
+  if (k.t->wide)
+    return lz ? col_inv_t<uint64_t, true>(k, out, out_ls, in, in_ls, rfold, addend)
+              : col_inv_t<uint64_t, false>(k, out, out_ls, in, in_ls, rfold, addend);
+  return lz ? col_inv_t<uint32_t, true>(k, out, out_ls, in, in_ls, rfold, addend)
+            : col_inv_t<uint32_t, false>(k, out, out_ls, in, in_ls, rfold, addend);
 }
 hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a, const void* b) {
   RNT_WIDE(elementwise_t<uint32_t>(k, op, out, a, b), elementwise_t<uint64_t>(k, op, out, a, b));

@@ -527,6 +527,9 @@ __device__ __forceinline__ void swap_q3p2(uint32_t (&x)[64]) {
 #ifndef RNT_MF_TENSOR_PARK
 #define RNT_MF_TENSOR_PARK 0
 #endif
+#ifndef RNT_MF_TENSOR_MEAS
+#define RNT_MF_TENSOR_MEAS 0
+#endif
 #ifndef RNT_MF_TENSOR_PARK4
 #define RNT_MF_TENSOR_PARK4 0
 #endif
@@ -1081,14 +1084,22 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
   // off by default
   constexpr int NP = SX ? RNT_MF_TENSOR_PARK : 0;
   constexpr uint32_t PB = 128u * 1024u, PS = 2048u;
+  // RNT_MF_TENSOR_MEAS (measurement builds only, wrong results by design;
+  // profiles/r06/tensor_traffic.json): 1 drops c1^'s round trip through the
+  // scratch slot (its store and both reads), 2 drops t's (its store into
+  // d2's plane and its read), 3 drops c0^'s (its store into d1's plane and
+  // both reads); the PMC bytes each build saves say whether that temporary
+  // leaves the L2
+  constexpr int MEAS = RNT_MF_TENSOR_MEAS;
   fwd<false, S_F4, false, SX, NP, PB, PS>(x, rsrc(c0 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
-    bst(canon4(r), R1, pl, p4_soff(h, cc));
+    if constexpr (MEAS != 3) bst(canon4(r), R1, pl, p4_soff(h, cc));
   });
   fwd<!SX, S_F4, false, SX, NP, PB, PS>(x, rsrc(c1 + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
-    bst(canon4(r), RS, pl, p4_soff(h, cc));
+    if constexpr (MEAS != 1) bst(canon4(r), RS, pl, p4_soff(h, cc));
   });
   fwd<!SX, S_F4, false, SX, NP, PB, PS>(x, rsrc(c0p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
-    const v4i a0 = bld(R1, pl, p4_soff(h, cc)), a1 = bld(RS, pl, p4_soff(h, cc));
+    const v4i a0 = MEAS == 3 ? canon4(r) : bld(R1, pl, p4_soff(h, cc));
+    const v4i a1 = MEAS == 1 ? canon4(r) : bld(RS, pl, p4_soff(h, cc));
     const v4i b = canon4(r);
     v4i o0, t;
 #pragma unroll
@@ -1097,12 +1108,13 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
       t[i] = (int)mmul((uint32_t)a1[i], (uint32_t)b[i]);
     }
     bst<kLastAux>(o0, R0, pl, p4_soff(h, cc));
-    bst(t, R2, pl, p4_soff(h, cc));
+    if constexpr (MEAS != 2) bst(t, R2, pl, p4_soff(h, cc));
   });
   fwd<!SX, S_F4, false, RNT_MF_TENSOR_PARK4 && SX, RNT_MF_TENSOR_PARK4 ? NP : 0, PB, PS>(x, rsrc(c1p + io, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
-    const v4i a0 = bld<kLastAux>(R1, pl, p4_soff(h, cc)), a1 = bld<kLastAux>(RS, pl, p4_soff(h, cc));
-    const v4i t = bld<kLastAux>(R2, pl, p4_soff(h, cc));
     const v4i b = canon4(r);
+    const v4i a0 = MEAS == 3 ? b : bld<kLastAux>(R1, pl, p4_soff(h, cc));
+    const v4i a1 = MEAS == 1 ? b : bld<kLastAux>(RS, pl, p4_soff(h, cc));
+    const v4i t = MEAS == 2 ? b : bld<kLastAux>(R2, pl, p4_soff(h, cc));
     v4i o1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

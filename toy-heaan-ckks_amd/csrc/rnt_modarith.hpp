@@ -231,10 +231,47 @@ __device__ __forceinline__ void gs_bfly(uint32_t& x, uint32_t& y, uint32_t w, ui
 __device__ __forceinline__ uint32_t shoup_mul(uint32_t x, uint32_t w, uint32_t wp, const Mod30& m) {
   return csub<uint32_t>(shoup_lazy(x, w, wp, Mod<uint32_t>{m.q, m.nq}), m.q);
 }
+// ---- 62-bit moduli in 64-bit words: the same Harvey-lazy butterflies -------
+// With q < 2^62, 4q < 2^64 gives the u64 path the two bits of headroom the
+// 30-bit u32 bases have, so the product path runs the same lazy ranges
+// (forward CT values in [0, 4q), inverse GS values in [0, 2q)): one 64-bit
+// conditional subtraction per CT butterfly instead of three (the Shoup
+// product's, add_mod's, sub_mod's), and one per GS butterfly instead of two.
+// A 64-bit reduction is a two-word subtract, a 64-bit compare and two
+// selects, so each one saved is five VALU ops on the VALU-bound u64 path
+// ("The u64 path").  The reference's 40-, 61- and 62-bit
+// primes all qualify; a 63-bit prime keeps the canonical kernels.
+struct Mod62 {
+  uint64_t q;   // modulus, < 2^62
+  uint64_t q2;  // 2q
+};
+__device__ __forceinline__ uint64_t shoup_lazy(uint64_t x, uint64_t w, uint64_t wp, const Mod62& m) {
+  return x * w - mulhi(x, wp) * m.q;  // [0, 2q) for any x < 2^64
+}
+__device__ __forceinline__ void ct_bfly(uint64_t& x, uint64_t& y, uint64_t w, uint64_t wp, const Mod62& m) {
+  const uint64_t t = shoup_lazy(y, w, wp, m);                          // [0, 2q)
+  const uint64_t u = csub<uint64_t>(x, m.q2);                          // [0, 2q)
+  x = u + t;
+  y = u + (m.q2 - t);
+}
+__device__ __forceinline__ void ct_bfly_lazy(uint64_t& x, uint64_t& y, uint64_t w, uint64_t wp,
+                                             const Mod62& m) {
+  ct_bfly(x, y, w, wp, m);
+}
+__device__ __forceinline__ void gs_bfly(uint64_t& x, uint64_t& y, uint64_t w, uint64_t wp, const Mod62& m) {
+  const uint64_t u = x, v = y;
+  x = csub<uint64_t>(u + v, m.q2);
+  y = shoup_lazy(u - v + m.q2, w, wp, m);
+}
+__device__ __forceinline__ uint64_t shoup_mul(uint64_t x, uint64_t w, uint64_t wp, const Mod62& m) {
+  return csub<uint64_t>(shoup_lazy(x, w, wp, m), m.q);
+}
+
 // What the GS difference u - v is biased by to stay non-negative.
 template <class W>
 __device__ __forceinline__ W gs_bias(const Mod<W>& m) { return m.q; }   // u, v in [0, q)
 __device__ __forceinline__ uint32_t gs_bias(const Mod30& m) { return m.q2; }  // u, v in [0, 2q)
+__device__ __forceinline__ uint64_t gs_bias(const Mod62& m) { return m.q2; }  // u, v in [0, 2q)
 
 // m mod q for a 64-bit magnitude m, canonical.  The 32-bit path splits m
 // into halves, hi * (2^32 mod q) + lo, each reduced by a Shoup product, so

@@ -307,19 +307,22 @@ class RnsPoly:
     ``channels_batch()`` is always [B][L][N].
     """
 
-    def __init__(self, basis: RnsBasis, n_polys: Optional[int] = None):
+    def __init__(self, basis: RnsBasis, n_polys: Optional[int] = None, _uninit: bool = False):
         lib = load()
         h = ctypes.c_void_p()
         count = 1 if n_polys is None else int(n_polys)
-        check(lib.rnt_buf_alloc(basis.handle, count, ctypes.byref(h)))
+        alloc = lib.rnt_buf_alloc_uninit if _uninit else lib.rnt_buf_alloc
+        check(alloc(basis.handle, count, ctypes.byref(h)))
         self._h = h
         self.basis = basis
         self.n_polys = count
         self.batched = n_polys is not None
 
     def _like(self, basis: Optional[RnsBasis] = None) -> "RnsPoly":
-        """A zero output of this object's kind and batch on ``basis``."""
-        return RnsPoly(basis or self.basis, self.n_polys if self.batched else None)
+        """An op output of this object's kind and batch on ``basis``: its
+        contents are unspecified until the op (which writes every word)
+        fills it, so no zero fill is queued (rnt_buf_alloc_uninit)."""
+        return RnsPoly(basis or self.basis, self.n_polys if self.batched else None, _uninit=True)
 
     # -- constructors (poly.rs:34-114) --------------------------------------
     @classmethod

@@ -113,6 +113,7 @@ SIGNATURES = {
     "rnt_graph_destroy": (c_int, [_P]),
     "rnt_graph_workspace": (c_int, [_P, POINTER(c_size_t), POINTER(c_size_t)]),
     "rnt_buf_alloc": (c_int, [_P, c_size_t, POINTER(_P)]),
+    "rnt_buf_alloc_uninit": (c_int, [_P, c_size_t, POINTER(_P)]),
     "rnt_buf_free": (c_int, [_P]),
     "rnt_buf_n_polys": (c_int, [_P, POINTER(c_size_t)]),
     "rnt_buf_is_ntt": (c_int, [_P, POINTER(c_int)]),
