@@ -777,8 +777,9 @@ def run_ctmul(args, comm, world, rank, local_rank):
         pipe.basis, pipe.moduli, counts, pipe.limbs, pipe.owner_last = state0
         pipe.counts = list(counts)
         with torch.cuda.stream(lib_stream):  # torch ops share the library's stream
-            m0, m1 = pipe.mul_relin(c[0], c[1], c[2], c[3], key)
-            return pipe.rescale(m0, m1)
+            # (a world of one: the fused rnt_ct_mul_relin_rescale per chunk;
+            # limb-sharded: mul_relin, then rescale, with their RCCL joins)
+            return pipe.mul_relin_rescale(c[0], c[1], c[2], c[3], key)
 
     for _ in range(args.warmup):
         step()
@@ -883,7 +884,9 @@ def run_ctmul(args, comm, world, rank, local_rank):
             "workload": f"ct x ct + gadget relin + rescale, N=2^{args.log_n}, L={L} x {args.prime_bits}-bit primes",
             "ct_pairs_per_gpu_per_step": args.ct_batch,
             "global_batch": B_global,
-            "parallelism": (f"batch-sharded x{world}: no collective, full key per GPU" if batch_shard else
+            "parallelism": (f"batch-sharded x{world}: no collective, full key per GPU, fused "
+                            f"rnt_ct_mul_relin_rescale per chunk" if batch_shard else
+                            "single GPU: fused rnt_ct_mul_relin_rescale per chunk (no join)" if world == 1 else
                             f"limb-sharded x{world}: RCCL all-gather of d2, broadcast of q_L limb"),
             "parity_spot_check": parity_ok,
             "parity_pairs": check_pairs,

@@ -308,6 +308,16 @@ int rnt_keyswitch(rnt_buf* acc0, rnt_buf* acc1, const rnt_buf* d,
 int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
                      const rnt_buf* c1, const rnt_buf* c0p, const rnt_buf* c1p,
                      const rnt_buf* key_a, const rnt_buf* key_b);
+/* mul_ciphertexts_gadget followed by rescale_ciphertext (engine.rs:473-539,
+ * then :263-282), the engine's ct-mul call pair, as one op: out0/out1 are on
+ * drop_last(1) of the inputs' basis (one shared context, as rnt_ct_rescale);
+ * the result equals rnt_ct_mul_relin + rnt_ct_rescale word for word.  The
+ * rescale runs as the key-switch inverse's epilogue, so the un-rescaled
+ * product never reaches memory (N >= 2^14 with the four-step key-switch;
+ * smaller rings run the two ops). */
+int rnt_ct_mul_relin_rescale(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
+                             const rnt_buf* c1, const rnt_buf* c0p, const rnt_buf* c1p,
+                             const rnt_buf* key_a, const rnt_buf* key_b);
 /* rotate_ciphertext (engine.rs:412-463). */
 int rnt_ct_rotate(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
                   const rnt_buf* c1, int32_t k, const rnt_buf* key_a,

@@ -346,3 +346,50 @@ def test_keyswitch_row_grids(gpu, log_n, B, np_):
         w0, w1 = orc.keyswitch(Bo, d[p], ka, kb, threads=T)
         assert np.array_equal(a0.channels_of(p)[0], w0), (log_n, B, p)
         assert np.array_equal(a1.channels_of(p)[0], w1), (log_n, B, p)
+
+
+@pytest.mark.parametrize("log_n,L,B,bits", [(16, 16, 66, 31), (14, 8, 5, 31), (12, 4, 3, 31), (14, 3, 3, 61)])
+def test_fused_mul_relin_rescale_equals_two_calls(gpu, log_n, L, B, bits):
+    """rnt_ct_mul_relin_rescale (the rescale fused into the key-switch
+    inverse) equals mul_ciphertexts_gadget + rescale_ciphertext word for word
+    -- at config 4's ring over two key-switch chunks (66 pairs), config 3's,
+    a whole-plane ring (2^12, the two-op fallback) and a 61-bit u64 basis --
+    and the oracle on the first and last pair."""
+    rn = gpu
+    n = 1 << log_n
+    mod = rn.generate_primes(bits, L, n)
+    Bd, Bo = rn.RnsBasis(mod, n), orc.Basis(mod, n)
+    rng = np.random.default_rng(700 + log_n)
+    c0, c1, c0p, c1p = (_ct_batch(rng, mod, n, B, (0, B - 1)) for _ in range(4))
+    ka, kb = _rand(rng, mod, n, L), _rand(rng, mod, n, L)
+    rlk = rn.RnsGadgetKey.from_channels(ka, kb, Bd)
+    up = lambda x: rn.RnsPoly.from_channels(x, Bd)  # noqa: E731
+    ct1 = rn.Ciphertext(up(c0), up(c1), 31, Bd.total_bits())
+    ct2 = rn.Ciphertext(up(c0p), up(c1p), 31, Bd.total_bits())
+    fused = rn.mul_ciphertexts_gadget_rescale(ct1, ct2, rlk)
+    two = rn.rescale_ciphertext(rn.mul_ciphertexts_gadget(ct1, ct2, rlk))
+    assert fused.c0.basis.channel_count() == L - 1 and (fused.logp, fused.logq) == (two.logp, two.logq)
+    f0, f1 = fused.c0.channels(), fused.c1.channels()
+    assert np.array_equal(f0, two.c0.channels()) and np.array_equal(f1, two.c1.channels())
+    for p in (0, B - 1):
+        w0, w1 = orc.mul_ciphertexts_gadget(Bo, c0[p], c1[p], c0p[p], c1p[p], ka, kb, threads=T)
+        assert np.array_equal(f0[p], orc.rescale(Bo, w0)), p
+        assert np.array_equal(f1[p], orc.rescale(Bo, w1)), p
+
+
+def test_fused_mul_relin_rescale_errors(gpu):
+    """The fused op checks the output basis as rnt_ct_rescale does."""
+    rn = gpu
+    n = 1 << 14
+    mod = rn.generate_primes(31, 4, n)
+    Bd = rn.RnsBasis(mod, n)
+    rng = np.random.default_rng(9)
+    x = rn.RnsPoly.from_channels(_rand(rng, mod, n, 2), Bd)
+    ka, kb = _rand(rng, mod, n, 4), _rand(rng, mod, n, 4)
+    rlk = rn.RnsGadgetKey.from_channels(ka, kb, Bd)
+    lib = rn.load()
+    same = rn.RnsPoly(Bd, 2)  # full basis: not drop_last(1)
+    with pytest.raises(rn.RnsNttError) as e:
+        rn.check(lib.rnt_ct_mul_relin_rescale(same.handle, rn.RnsPoly(Bd, 2).handle, x.handle, x.handle,
+                                              x.handle, x.handle, rlk.a.handle, rlk.b.handle))
+    assert e.value.kind == "BasisMismatch"

@@ -2074,30 +2074,27 @@ extern "C" int rnt_ct_tensor(rnt_buf* d0, rnt_buf* d1, rnt_buf* d2, const rnt_bu
   return RNT_OK;
 }
 
-extern "C" int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
-                                const rnt_buf* c1, const rnt_buf* c0p, const rnt_buf* c1p,
-                                const rnt_buf* key_a, const rnt_buf* key_b) {
-  const rnt_buf* all[6] = {out0, out1, c0, c1, c0p, c1p};
-  for (const rnt_buf* b : all)
-    if (int rc = check_buf(b, "rnt_ct_mul_relin")) return rc;
-  for (int i = 1; i < 6; ++i)
-    if (int rc = check_same(all[0], all[i], "rnt_ct_mul_relin")) return rc;
-  if (int rc = check_key(c0, key_a, key_b)) return rc;
-  if (c0->in_ntt || c1->in_ntt || c0p->in_ntt || c1p->in_ntt)
-    return fail(RNT_ERR_DOMAIN_MISMATCH, "mul_ciphertexts_gadget: inputs must be in coefficient domain");
-  if (out0 == out1) return fail(RNT_ERR_BAD_ARGUMENT, "rnt_ct_mul_relin: out0 aliases out1");
+// The ct-mul body; with `resc` the outputs are on drop_last(1) and each
+// chunk's key-switch inverse applies the rescale as its epilogue
+// (rnt_ct_mul_relin_rescale: the dropped limb's inverse runs first, into a
+// chunk plane the other limbs' inverse reads), so the un-rescaled product
+// never goes through HBM.
+static int ct_mul_relin_body(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, const rnt_buf* c1,
+                             const rnt_buf* c0p, const rnt_buf* c1p, const rnt_buf* key_a,
+                             const rnt_buf* key_b, bool resc) {
   if (int rc = set_device(c0->ctx)) return rc;
   rnt::Launch k = launch_for(c0);
   const size_t L = k.L, n = k.t->n, wb = word_bytes(k.t), B = c0->n_polys;
   const size_t bc = ks_chunk(k.t, L, B);
   // ws: [T0..T3 (column outputs, chunk-local)] | D0 | D1 | D2 | key-switch (S|U0|U1)
+  // [| LAST0 | LAST1 with resc]
   // (the whole-plane tensor reads the ciphertexts directly: no T)
   const bool whole = rnt::tensor_whole_ok(k.t);
   const bool mf = !whole && use_mf(k);
   const size_t chunk_words = L * bc * n;
   // (the matrix-core tensor's scratch: plane_scratch_planes(L bc) <= L bc planes)
   const size_t nt = whole ? 0 : mf ? 1 : 4;
-  const size_t need = ((nt + 3) * chunk_words + ks_scratch_words(k.t, L, bc)) * wb;
+  const size_t need = ((nt + 3) * chunk_words + ks_scratch_words(k.t, L, bc) + (resc ? 2 * bc * n : 0)) * wb;
   CallWs cws(out0);
   if (int rc = cws.get(need)) return rc;
   char* ws = (char*)cws.p;
@@ -2132,6 +2129,39 @@ extern "C" int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
     // d2 -> coefficient domain (engine.rs:493), in place in D2
     LAUNCH(kc.t, rnt::K_COL_INV, rnt::launch_col_inv(kc, D2, cls, D2, cls, 1, nullptr), "d2 inverse");
     }
+    if (resc) {
+      // gadget sum into the chunk's NTT-row accumulators, then the inverse
+      // with the rescale fused (engine.rs:263-282 after :530-531)
+      char* S = KS;
+      char* U0 = S + L * L * c * n * wb;
+      char* U1 = U0 + L * c * n * wb;
+      char* LAST0 = KS + ks_scratch_words(k.t, L, bc) * wb;
+      char* LAST1 = LAST0 + bc * n * wb;
+      if (int rc = ks_decompose_rows(kc, S, D2, cls, U0, U1, cls, key_a, key_b, D0, D1, cls)) return rc;
+      rnt::Launch kl = kc;  // the dropped limb: its coefficient plane only
+      kl.L = 1;
+      rnt::ColRescArgs la;
+      la.limb0 = (uint32_t)(L - 1);
+      rnt::Launch kr = kc;  // the kept limbs, rescaled by it
+      kr.L = L - 1;
+      const uint64_t rls = limb_stride(out0);
+      char* U[2] = {U0, U1};
+      char* LAST[2] = {LAST0, LAST1};
+      rnt_buf* O[2] = {out0, out1};
+      for (int o = 0; o < 2; ++o) {
+        LAUNCH(kl.t, rnt::K_COL_INV,
+               rnt::launch_col_inv(kl, LAST[o], cls, U[o] + (L - 1) * cls * wb, cls, 1, nullptr, false, la),
+               "ks inverse (dropped limb)");
+        rnt::ColRescArgs ra;
+        ra.last = LAST[o];
+        ra.inv = rnt::resc_inv_row(k.t, L - 1, 0);
+        ra.invp = rnt::resc_inv_row(k.t, L - 1, 1);
+        LAUNCH(kr.t, rnt::K_COL_INV,
+               rnt::launch_col_inv(kr, (char*)O[o]->data + p0 * n * wb, rls, U[o], cls, 1, nullptr, false, ra),
+               "ks inverse + rescale");
+      }
+      continue;
+    }
     // gadget sum with d0hat / d1hat as accumulator seeds (engine.rs:530-531)
     // d2 lives in a chunk-local buffer: present it as a full "buffer".
     rnt_buf d2view;
@@ -2145,6 +2175,59 @@ extern "C" int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
   }
   out0->in_ntt = out1->in_ntt = 0;
   return RNT_OK;
+}
+
+static int ct_mul_check(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, const rnt_buf* c1,
+                        const rnt_buf* c0p, const rnt_buf* c1p, const rnt_buf* key_a, const rnt_buf* key_b,
+                        const char* name) {
+  const rnt_buf* all[6] = {out0, out1, c0, c1, c0p, c1p};
+  for (const rnt_buf* b : all)
+    if (int rc = check_buf(b, name)) return rc;
+  for (int i = 3; i < 6; ++i)
+    if (int rc = check_same(c0, all[i], name)) return rc;
+  if (int rc = check_key(c0, key_a, key_b)) return rc;
+  if (c0->in_ntt || c1->in_ntt || c0p->in_ntt || c1p->in_ntt)
+    return fail(RNT_ERR_DOMAIN_MISMATCH, "mul_ciphertexts_gadget: inputs must be in coefficient domain");
+  if (out0 == out1) return fail(RNT_ERR_BAD_ARGUMENT, "%s: out0 aliases out1", name);
+  return RNT_OK;
+}
+
+extern "C" int rnt_ct_mul_relin(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
+                                const rnt_buf* c1, const rnt_buf* c0p, const rnt_buf* c1p,
+                                const rnt_buf* key_a, const rnt_buf* key_b) {
+  if (int rc = ct_mul_check(out0, out1, c0, c1, c0p, c1p, key_a, key_b, "rnt_ct_mul_relin")) return rc;
+  if (int rc = check_same(out0, c0, "rnt_ct_mul_relin")) return rc;
+  if (int rc = check_same(out1, c0, "rnt_ct_mul_relin")) return rc;
+  return ct_mul_relin_body(out0, out1, c0, c1, c0p, c1p, key_a, key_b, false);
+}
+
+extern "C" int rnt_ct_mul_relin_rescale(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0,
+                                        const rnt_buf* c1, const rnt_buf* c0p, const rnt_buf* c1p,
+                                        const rnt_buf* key_a, const rnt_buf* key_b) {
+  if (int rc = ct_mul_check(out0, out1, c0, c1, c0p, c1p, key_a, key_b, "rnt_ct_mul_relin_rescale")) return rc;
+  const size_t L = c0->ctx->L;
+  if (L < 2)  // poly.rs:191-197
+    return fail_fields(RNT_ERR_INVALID_MOD_DROP, 1, L, "invalid mod-drop count 1 for %zu channels", L);
+  for (const rnt_buf* o : {(const rnt_buf*)out0, (const rnt_buf*)out1}) {
+    if (o->ctx->t != c0->ctx->t || o->ctx->L != L - 1)
+      return fail(RNT_ERR_BASIS_MISMATCH, "rescale: output basis is not drop_last(1) of the input's");
+    if (o->n_polys != c0->n_polys) return fail(RNT_ERR_BAD_ARGUMENT, "rescale: batch sizes differ");
+  }
+  if (out0->ctx != out1->ctx)  // engine.rs:272-274: one shared new basis
+    return fail(RNT_ERR_BASIS_MISMATCH, "rescale_ciphertext: outputs must share one basis");
+  if (rnt::col_resc_ok(c0->ctx->t.get()) && !rnt::ks_whole_ok(c0->ctx->t.get()))
+    return ct_mul_relin_body(out0, out1, c0, c1, c0p, c1p, key_a, key_b, true);
+  // small rings (the whole-plane key-switch, no column inverse): the product,
+  // then the rescale, through two call-scoped temporaries
+  rnt_buf* t0 = nullptr;
+  rnt_buf* t1 = nullptr;
+  int rc = rnt_buf_alloc_uninit(c0->ctx, c0->n_polys, &t0);
+  if (rc == RNT_OK) rc = rnt_buf_alloc_uninit(c0->ctx, c0->n_polys, &t1);
+  if (rc == RNT_OK) rc = ct_mul_relin_body(t0, t1, c0, c1, c0p, c1p, key_a, key_b, false);
+  if (rc == RNT_OK) rc = rnt_ct_rescale(out0, out1, t0, t1);
+  rnt_buf_free(t0);
+  rnt_buf_free(t1);
+  return rc;
 }
 
 extern "C" int rnt_ct_rotate(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, const rnt_buf* c1,

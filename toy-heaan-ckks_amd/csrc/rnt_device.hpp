@@ -166,6 +166,15 @@ __device__ __forceinline__ auto col_twiddles(const Tw<W>* base, uint32_t n) {
   }
 }
 
+// k_colt_inv's optional limb offset and fused rescale (ColRescArgs).
+template <class W>
+struct ColResc {
+  const W* last = nullptr;
+  const W* inv = nullptr;
+  const W* invp = nullptr;
+  uint32_t limb0 = 0;
+};
+
 // Last-stage constants of the inverse network (n^-1 folded, optionally with
 // the Montgomery factor): x <- (u+v) c1, y <- (u-v) c2.
 template <class W>

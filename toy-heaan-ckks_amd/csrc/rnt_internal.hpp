@@ -243,8 +243,22 @@ bool whole_ok(const Tables* t, int mode);
 hipError_t launch_whole(const Launch& k, int mode, void* out, void* x, const void* y, uint64_t ls);
 // Inverse column pass with n^-1 folded into the last stage; rfold adds the
 // Montgomery factor 2^w.  addend (optional, coefficient domain, out layout).
+// ColRescArgs (tiled grids, log R >= 5, col_resc_ok): limb0 offsets the
+// launch's limbs in the basis' tables (in/out point at the first one); with
+// `last` ([B][N], the dropped limb's coefficient plane) the output is
+// rescaled: (c_l - (c_last mod q_l)) inv[l], inv/invp the rows
+// resc_inv_row(t, last limb, 0 / 1) of the rescale table.
+struct ColRescArgs {
+  const void* last = nullptr;
+  const void* inv = nullptr;
+  const void* invp = nullptr;
+  uint32_t limb0 = 0;
+};
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
-                          uint64_t in_ls, int rfold, const void* addend, bool lazy = false);
+                          uint64_t in_ls, int rfold, const void* addend, bool lazy = false,
+                          const ColRescArgs& ra = ColRescArgs{});
+bool col_resc_ok(const Tables* t);
+const void* resc_inv_row(const Tables* t, size_t last, int which);
 // Elementwise over k.L*k.B*N contiguous words: op 0 add, 1 sub, 2 neg,
 // 3 pointwise mul (canonical a*b mod q), 4 Montgomery product (a*b*2^-w).
 hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a,

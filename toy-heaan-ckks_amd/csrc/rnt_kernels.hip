@@ -565,7 +565,7 @@ k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t
 template <class W, int LOG_R, int LOG_TC, bool LZ = false>
 __global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, uint32_t log_c,
-           uint32_t B, uint64_t in_ls, uint64_t out_ls, int rfold) {
+           uint32_t B, uint64_t in_ls, uint64_t out_ls, int rfold, ColResc<W> rs) {
   using G = ColGeo<LOG_R, LOG_TC>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -576,8 +576,9 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
   const uint64_t op = (uint64_t)cp.l * out_ls + (uint64_t)cp.p * N;
   ColAddr<G, G::BB0> a0(cp, log_c);
   const ColAddr<G, G::BBL> al(cp, log_c);
-  const LimbConst<W> lc = tp.lc[cp.l];
-  const auto itw = col_twiddles<W, G::UNIFORM>(tp.itw + (uint64_t)cp.l * N, N);
+  const uint32_t tl = cp.l + rs.limb0;  // this launch's limb in the basis' tables
+  const LimbConst<W> lc = tp.lc[tl];
+  const auto itw = col_twiddles<W, G::UNIFORM>(tp.itw + (uint64_t)tl * N, N);
   const Fold<W> f = rfold == 2 ? Fold<W>{lc.c1t, lc.c1t_p, lc.c2t, lc.c2t_p}
                   : rfold ? Fold<W>{lc.c1r, lc.c1r_p, lc.c2r, lc.c2r_p}
                           : Fold<W>{lc.c1, lc.c1_p, lc.c2, lc.c2_p};
@@ -592,6 +593,19 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
     const BufView<W> ad(addend + op, N);
 #pragma unroll
     for (int i = 0; i < E; ++i) x[0][i] = add_mod<W>(x[0][i], ad.ld(a0.v, i * a0.s), lc.q);
+  }
+  if (rs.last != nullptr) {
+    // the fused rescale (rescale_ciphertext, engine.rs:263-282; poly.rs:187-228):
+    // (c_l - (c_last mod q_l)) (q_last mod q_l)^-1, c_last the dropped
+    // limb's plane of the same poly, written by this op's previous launch
+    a0.refresh();
+    const BufView<W> lp(rs.last + (uint64_t)cp.p * N, N);
+    const W inv = rs.inv[tl], invp = rs.invp[tl];
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      const W cl = shoup_mul<W>(lp.ld(a0.v, i * a0.s), (W)1, lc.one_p, lc.q);
+      x[0][i] = shoup_mul<W>(sub_mod<W>(x[0][i], cl, lc.q), inv, invp, lc.q);
+    }
   }
   a0.refresh();
 #pragma unroll
@@ -1607,7 +1621,12 @@ static hipError_t col_fwd_t(const Launch& k, void* out0, const void* in0, void* 
 
 template <class W, bool LZ>
 static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const void* in,
-                            uint64_t in_ls, int rfold, const void* addend) {
+                            uint64_t in_ls, int rfold, const void* addend, const ColRescArgs& ra) {
+  ColResc<W> rs;
+  rs.last = (const W*)ra.last;
+  rs.inv = (const W*)ra.inv;
+  rs.invp = (const W*)ra.invp;
+  rs.limb0 = ra.limb0;
   const Geom g = geom_for(k.t->log_n);
   const TabPtrs<W> tp = tab_ptrs<W>(k.t);
   if ((uint64_t)k.L * k.B == 0) return hipSuccess;
@@ -1620,7 +1639,7 @@ static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const v
   if (e != hipSuccess) return e;                                                             \
   hipLaunchKernelGGL((k_colt_inv<W, R, TC, LZ>), grid, dim3(ColGeo<R, TC>::THREADS),             \
                      (col_lds<W, R, TC>()), k.s, (W*)out, (const W*)in, (const W*)addend, tp, \
-                     g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls, rfold)
+                     g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls, rfold, rs)
 #define RNT_L(R)                          \
   if (col_log_tc(g) == 6) {               \
     RNT_L2(R, 6);                         \
@@ -1632,6 +1651,7 @@ static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const v
 #undef RNT_L2
     return hipGetLastError();
   }
+  if (ra.last != nullptr || ra.limb0 != 0) return hipErrorInvalidValue;  // tiled grids only (log R >= 5)
   const uint64_t total = (uint64_t)k.L * k.B * g.c;
 #define RNT_L(R)                                                                          \
   hipLaunchKernelGGL((k_col_inv<W, R>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,  \
@@ -2075,13 +2095,19 @@ hipError_t launch_whole(const Launch& k, int mode, void* out, void* x, const voi
   RNT_WIDE(whole_t<uint32_t>(k, mode, out, x, y, ls, lz), whole_t<uint64_t>(k, mode, out, x, y, ls, lz));
 }
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
-                          uint64_t in_ls, int rfold, const void* addend, bool lazy) {
+                          uint64_t in_ls, int rfold, const void* addend, bool lazy, const ColRescArgs& ra) {
   const bool lz = lazy && lazy_ok(k.t);
   if (k.t->wide)
-    return lz ? col_inv_t<uint64_t, true>(k, out, out_ls, in, in_ls, rfold, addend)
-              : col_inv_t<uint64_t, false>(k, out, out_ls, in, in_ls, rfold, addend);
-  return lz ? col_inv_t<uint32_t, true>(k, out, out_ls, in, in_ls, rfold, addend)
-            : col_inv_t<uint32_t, false>(k, out, out_ls, in, in_ls, rfold, addend);
+    return lz ? col_inv_t<uint64_t, true>(k, out, out_ls, in, in_ls, rfold, addend, ra)
+              : col_inv_t<uint64_t, false>(k, out, out_ls, in, in_ls, rfold, addend, ra);
+  return lz ? col_inv_t<uint32_t, true>(k, out, out_ls, in, in_ls, rfold, addend, ra)
+            : col_inv_t<uint32_t, false>(k, out, out_ls, in, in_ls, rfold, addend, ra);
+}
+bool col_resc_ok(const Tables* t) { return geom_for(t->log_n).log_r >= 5; }
+const void* resc_inv_row(const Tables* t, size_t last, int which) {
+  const size_t wb = t->wide ? 8 : 4;
+  const char* base = (const char*)(which ? t->resc_p : t->resc);
+  return base + last * t->L * wb;
 }
 hipError_t launch_elementwise(const Launch& k, int op, void* out, const void* a, const void* b) {
   RNT_WIDE(elementwise_t<uint32_t>(k, op, out, a, b), elementwise_t<uint64_t>(k, op, out, a, b));

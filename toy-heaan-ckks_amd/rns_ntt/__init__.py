@@ -39,6 +39,7 @@ __all__ = [
     "find_psi",
     "keyswitch",
     "mul_ciphertexts_gadget",
+    "mul_ciphertexts_gadget_rescale",
     "rotate_ciphertext",
     "rescale_ciphertext",
     "Plaintext",
@@ -606,6 +607,20 @@ def rotate_ciphertext(ct: Ciphertext, rotk: RnsGadgetKey) -> Ciphertext:
     check(load().rnt_ct_rotate(out0.handle, out1.handle, ct.c0.handle, ct.c1.handle,
                                int(rotk.rotation or 0), rotk.a.handle, rotk.b.handle))
     return Ciphertext(out0, out1, ct.logp, ct.logq)
+
+
+def mul_ciphertexts_gadget_rescale(ct1: Ciphertext, ct2: Ciphertext, rlk: RnsGadgetKey) -> Ciphertext:
+    """mul_ciphertexts_gadget then rescale_ciphertext (engine.rs:473-539,
+    :263-282) as one op (rnt_ct_mul_relin_rescale): equal word for word to
+    the two calls, with the rescale fused into the key-switch inverse."""
+    assert ct1.logq == ct2.logq, "logq mismatch in gadget multiplication"
+    q_last = ct1.c0.basis.moduli()[-1]
+    bits_dropped = q_last.bit_length()
+    new_basis = ct1.c0.basis.drop_last(1)
+    out0, out1 = ct1.c0._like(new_basis), ct1.c0._like(new_basis)
+    check(load().rnt_ct_mul_relin_rescale(out0.handle, out1.handle, ct1.c0.handle, ct1.c1.handle,
+                                          ct2.c0.handle, ct2.c1.handle, rlk.a.handle, rlk.b.handle))
+    return Ciphertext(out0, out1, ct1.logp + ct2.logp - bits_dropped, ct1.logq - bits_dropped)
 
 
 def rescale_ciphertext(ct: Ciphertext) -> Ciphertext:

@@ -142,6 +142,7 @@ SIGNATURES = {
     "rnt_key_prepare": (c_int, [_P, _P]),
     "rnt_keyswitch": (c_int, [_P, _P, _P, _P, _P]),
     "rnt_ct_mul_relin": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
+    "rnt_ct_mul_relin_rescale": (c_int, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "rnt_ct_rotate": (c_int, [_P, _P, _P, _P, c_int32, _P, _P]),
     "rnt_ct_rescale": (c_int, [_P, _P, _P, _P]),
     "rnt_encode": (c_int, [_P, c_void_p, c_size_t, c_uint32]),

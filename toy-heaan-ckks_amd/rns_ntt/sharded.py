@@ -436,6 +436,16 @@ class GpuBackend:
     def new_planes(self, basis, count: int, B: int):
         return self._empty(basis, (count, B, basis.degree))
 
+    def mul_relin_rescale(self, basis, out_basis, x0, x1, y0, y1, key):
+        """One rank holding every limb: ct-mul + relin + rescale of a chunk
+        as the library's fused op (rnt_ct_mul_relin_rescale)."""
+        from . import Ciphertext, mul_ciphertexts_gadget_rescale
+
+        self._sync_torch(basis)
+        r = mul_ciphertexts_gadget_rescale(Ciphertext(x0, x1), Ciphertext(y0, y1), key)
+        self._lib_done(basis)
+        return r.c0, r.c1
+
     def rescale(self, basis, out_basis, poly, last_plane, q_last: int):
         from . import rescale_ext
 
@@ -548,6 +558,26 @@ class LimbShardedPipeline:
             o0.append(a0)
             o1.append(a1)
         return Chunked(o0), Chunked(o1)
+
+    def mul_relin_rescale(self, c0: Chunked, c1: Chunked, c0p: Chunked, c1p: Chunked, key):
+        """ct x ct -> relin -> rescale (engine.rs:473-539 then :263-282).  A
+        world of one with a backend that has the fused op runs it per chunk
+        (the rescale inside the key-switch inverse, no join to wait for);
+        otherwise mul_relin, then rescale with its joins."""
+        if self.comm.world == 1 and hasattr(self.backend, "mul_relin_rescale"):
+            out_basis = self.backend.drop_last(self.basis)
+            r0, r1 = [], []
+            for x0, x1, y0, y1 in zip(c0, c1, c0p, c1p):
+                a0, a1 = self.backend.mul_relin_rescale(self.basis, out_basis, x0, x1, y0, y1, key)
+                r0.append(a0)
+                r1.append(a1)
+            self.moduli = self.moduli[:-1]
+            self.counts[self.owner_last] -= 1
+            self.limbs = range(self.limbs.start, self.limbs.stop - 1)
+            self.basis = out_basis
+            return Chunked(r0), Chunked(r1)
+        m0, m1 = self.mul_relin(c0, c1, c0p, c1p, key)
+        return self.rescale(m0, m1)
 
     # -- rotation (engine.rs:412-463) ---------------------------------------
     def rotate(self, c0: Chunked, c1: Chunked, k: int, key):
