@@ -72,6 +72,9 @@ def parse():
                    help="poly-mul operands: seeded uniform residues drawn on the device (Philox, "
                         "rnt_sample_uniform) or 16 seeded host pairs tiled to the batch and uploaded")
     p.add_argument("--ct-batch", type=int, default=128, help="ciphertext pairs per GPU per step (ctmul)")
+    p.add_argument("--chunk", type=int, default=None,
+                   help="ctmul: ciphertexts per pipeline chunk (default 64, the library's key-switch "
+                        "chunk at N=2^16 under the default 4 GiB RNT_KS_WS_MB)")
     p.add_argument("--rot-batch", type=int, default=8, help="ciphertexts per rotation (rotate)")
     p.add_argument("--enc-batch", type=int, default=64, help="plaintexts per step (encode)")
     p.add_argument("--log-n", type=int, default=16)
@@ -755,7 +758,7 @@ def run_ctmul(args, comm, world, rank, local_rank):
         data_comm = SingleComm()
     B_global = args.ct_batch * world  # weak scaling
     B = args.ct_batch if batch_shard else B_global  # ciphertexts this rank's pipeline holds
-    pipe = LimbShardedPipeline(mod, n, data_comm, GpuBackend(local_rank))
+    pipe = LimbShardedPipeline(mod, n, data_comm, GpuBackend(local_rank), chunk=args.chunk)
     rng = np.random.default_rng(77)
     uniq = min(4, B)
     reps = (B + uniq - 1) // uniq

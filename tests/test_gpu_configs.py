@@ -3,8 +3,9 @@ oracle (VERDICT r01 "what's weak" #1).
 
 * Config 4 (N=2^16, 16 x 31-bit primes): mul_ciphertexts_gadget
   (engine.rs:473-539) + rescale_ciphertext (engine.rs:263-282) on a batch of
-  66 ciphertext pairs.  The key-switch workspace cap (4 GiB of S =
-  [L][L][Bc][N] words, rnt_api.cpp ks_chunk) gives chunks of 64 here, so the
+  66 ciphertext pairs.  With the key-switch workspace cap set to 4 GiB of S
+  (RNT_KS_WS_MB=4096; S = [L][L][Bc][N] words, rnt_api.cpp ks_chunk; the
+  default 16 GiB gives 256) the chunks are 64, so the
   batch runs as two chunks, [0, 64) and [64, 66); the checked pairs sit on
   both sides of the boundary and at the end.  The decomposition's target
   limb groups (auto: 16 for the first chunk, 2 for the 8-tile second) are
@@ -48,7 +49,8 @@ def _ct_batch(rng, mod, n, B, distinct_at):
     return out
 
 
-def test_config4_ct_mul_relin_rescale_two_chunks(gpu):
+def test_config4_ct_mul_relin_rescale_two_chunks(gpu, monkeypatch):
+    monkeypatch.setenv("RNT_KS_WS_MB", "4096")  # chunks of 64 (read at rnt_ctx_create)
     rn = gpu
     n, L, B = 1 << 16, 16, 66
     mod = rn.generate_primes(31, L, n)
@@ -79,9 +81,10 @@ def test_config4_ct_mul_relin_rescale_two_chunks(gpu):
 def test_config4_full_1024_ct_batch(gpu):
     """BASELINE config 4 at its stated batch: 1024 ciphertext pairs through
     mul_ciphertexts_gadget (engine.rs:473-539) + rescale_ciphertext
-    (engine.rs:263-282) in one call, i.e. 16 key-switch chunks of 64.  The
+    (engine.rs:263-282) in one call, i.e. 4 key-switch chunks of 256 (the
+    default 16 GiB S cap).  The
     operands are drawn on the device (Philox, rnt_sample_uniform: 32 GiB of
-    host data otherwise); the chunk-boundary ciphertexts 0, 63, 64 and the
+    host data otherwise); the chunk-boundary ciphertexts 0, 255, 256 and the
     last, 1023, are read back with their inputs and checked against the
     oracle."""
     rn = gpu
@@ -98,7 +101,7 @@ def test_config4_full_1024_ct_batch(gpu):
     out = rn.mul_ciphertexts_gadget(ct1, ct2, rlk)
     res = rn.rescale_ciphertext(out)
     assert res.c0.basis.channel_count() == L - 1
-    for p in (0, 63, 64, B - 1):
+    for p in (0, 255, 256, B - 1):
         x0, x1, y0, y1 = (t.channels_of(p)[0] for t in (c0, c1, c0p, c1p))
         w0, w1 = orc.mul_ciphertexts_gadget(Bo, x0, x1, y0, y1, ka, kb, threads=T)
         assert np.array_equal(out.c0.channels_of(p)[0], w0), p
@@ -349,12 +352,13 @@ def test_keyswitch_row_grids(gpu, log_n, B, np_):
 
 
 @pytest.mark.parametrize("log_n,L,B,bits", [(16, 16, 66, 31), (14, 8, 5, 31), (12, 4, 3, 31), (14, 3, 3, 61)])
-def test_fused_mul_relin_rescale_equals_two_calls(gpu, log_n, L, B, bits):
+def test_fused_mul_relin_rescale_equals_two_calls(gpu, monkeypatch, log_n, L, B, bits):
     """rnt_ct_mul_relin_rescale (the rescale fused into the key-switch
     inverse) equals mul_ciphertexts_gadget + rescale_ciphertext word for word
     -- at config 4's ring over two key-switch chunks (66 pairs), config 3's,
     a whole-plane ring (2^12, the two-op fallback) and a 61-bit u64 basis --
     and the oracle on the first and last pair."""
+    monkeypatch.setenv("RNT_KS_WS_MB", "4096")  # config 4: chunks of 64, so 66 pairs are two
     rn = gpu
     n = 1 << log_n
     mod = rn.generate_primes(bits, L, n)

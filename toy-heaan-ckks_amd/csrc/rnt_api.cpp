@@ -792,9 +792,13 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     {
       const long jg = env_long("RNT_DEC_JG", 0);  // A/B knob: 0 = auto, else 1..1024
       t->dec_jg = (uint32_t)(jg < 0 ? 0 : jg > 1024 ? 1024 : jg);
-      // key-switch scratch cap (S = [L][L][Bc][N] words per chunk), MiB
-      const long mb = env_long("RNT_KS_WS_MB", 4096);
-      t->ks_ws_bytes = (size_t)(mb > 0 ? mb : 4096) << 20;
+      // key-switch scratch cap (S = [L][L][Bc][N] words per chunk), MiB.
+      // 16 GiB: 256-ct chunks at config 4 (N = 2^16, L = 16) ran the fused
+      // ct-mul 2.5% faster than 64-ct ones (4 GiB), the tensor and rows
+      // kernels' last-round tails amortised over 4x the grid; 32 GiB chunks
+      // fell off the workspace pool (profiles/r06/ab_ks_chunk.txt)
+      const long mb = env_long("RNT_KS_WS_MB", 16384);
+      t->ks_ws_bytes = (size_t)(mb > 0 ? mb : 16384) << 20;
     }
     t->log_n = log_n;
     t->n = (size_t)n;

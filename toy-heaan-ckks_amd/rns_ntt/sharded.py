@@ -498,8 +498,11 @@ class LimbShardedPipeline:
         self.backend = backend
         self.degree = degree
         self.moduli = list(moduli)
-        # default: the library's key-switch chunk at N = 2^16 (64 ciphertexts)
-        self.chunk = int(chunk) if chunk else 64
+        # default: 64 ciphertexts with limb-sharded joins (each chunk's join
+        # overlaps its neighbours' compute); 256, the library's key-switch
+        # chunk at N = 2^16 under its 16 GiB cap, for a rank holding every
+        # limb (the fused ct-mul + rescale per chunk, no join to overlap)
+        self.chunk = int(chunk) if chunk else (256 if comm.world == 1 else 64)
         if comm.world > len(self.moduli):
             raise ValueError(f"{comm.world} ranks for {len(self.moduli)} limbs")
         self._layout()
