@@ -37,7 +37,7 @@ PKG = os.path.join(REPO, "toy-heaan-ckks_amd")
 sys.path.insert(0, PKG)
 
 METRIC = "RNS-NTT poly-muls/sec (N=2^16, 16 primes) at 1/2/4/8 GPUs; % HBM roofline"
-CT_METRIC = "ct x ct -> relin -> rescale ciphertexts/sec (N=2^16, 16 primes, limb-sharded)"
+CT_METRIC = "ct x ct -> relin -> rescale ciphertexts/sec (N=2^{log_n}, {L} primes)"
 ROT_METRIC = "rotation key-switches/sec (N=2^17, 32 primes, power-of-two Galois offsets)"
 ENC_METRIC = "CKKS encode+decode round trips/sec (N=2^16, 16 primes, N/2 complex slots)"
 NTT_METRIC = "RNS-NTT forward+inverse transform pairs/sec (N=2^16, 16 primes)"
@@ -704,7 +704,7 @@ def run_ctmul_graph(args, comm, world, rank, local_rank):
         roof.update(kernel="ks_whole", achieved=ach, frac=ach / VALU_PEAK_BFLY,
                     bfly_per_launch=bfly / kernels["ks_whole"]["launches"])
     return {
-        "metric": CT_METRIC,
+        "metric": CT_METRIC.format(log_n=args.log_n, L=args.limbs),
         "value": value,
         "unit": "ct-muls/s",
         "n_gpus": world,
@@ -816,7 +816,9 @@ def run_ctmul(args, comm, world, rank, local_rank):
     # the second pipeline chunk and the batch's last pair.  Limb-sharded:
     # every rank sends its limbs of those pairs (after the rescale) to rank
     # 0 over the gloo control plane, which assembles the full ciphertexts.
-    check_pairs = sorted({0, min(pipe.chunk, B - 1), B - 1})
+    # the first pair, the first of the second pipeline chunk (or, one chunk,
+    # of the library's second key-switch chunk at N = 2^16: 256), the last
+    check_pairs = sorted({0, min(pipe.chunk, 256, B - 1), B - 1})
     mine = {pi: pipe.download(r[0], first=pi, count=1)[0] for pi in check_pairs}
     if world > 1 and not batch_shard:
         parts = comm.gather((rank, pipe.limbs.start, mine))
@@ -871,7 +873,7 @@ def run_ctmul(args, comm, world, rank, local_rank):
         roof.update(kernel="ks_whole", achieved=ach, frac=ach / VALU_PEAK_BFLY,
                     bfly_per_launch=bfly / kernels["ks_whole"]["launches"])
     return {
-        "metric": CT_METRIC,
+        "metric": CT_METRIC.format(log_n=args.log_n, L=args.limbs),
         "value": value,
         "unit": "ct-muls/s",
         "n_gpus": world,

@@ -499,10 +499,12 @@ class LimbShardedPipeline:
         self.degree = degree
         self.moduli = list(moduli)
         # default: 64 ciphertexts with limb-sharded joins (each chunk's join
-        # overlaps its neighbours' compute); 256, the library's key-switch
-        # chunk at N = 2^16 under its 16 GiB cap, for a rank holding every
-        # limb (the fused ct-mul + rescale per chunk, no join to overlap)
-        self.chunk = int(chunk) if chunk else (256 if comm.world == 1 else 64)
+        # overlaps its neighbours' compute); a rank holding every limb has no
+        # join to overlap, so its batch is one chunk and the library chunks
+        # it by its own key-switch cap (256 cts at N = 2^16, 16 limbs): config
+        # 3 at 1024 cts 141.8k -> 148.1k ct-muls/s against 256-ct pipeline
+        # chunks, config 4 flat (profiles/r06/ab_ks_chunk.txt)
+        self.chunk = int(chunk) if chunk else (1 << 30 if comm.world == 1 else 64)
         if comm.world > len(self.moduli):
             raise ValueError(f"{comm.world} ranks for {len(self.moduli)} limbs")
         self._layout()
