@@ -341,7 +341,7 @@ def live_pmc(args, kernel_re):
     try:
         for name, ctrs in (("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE", "GRBM_GUI_ACTIVE"])):
             out = os.path.join(tmp, name)
-            cmd = ["timeout", "-s", "KILL", "240", prof, "--pmc", *ctrs, "--output-format", "csv", "-d", out,
+            cmd = ["timeout", "-s", "KILL", "120", prof, "--pmc", *ctrs, "--output-format", "csv", "-d", out,
                    "-o", "run", "--", *child]
             t0 = time.perf_counter()
             r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
