@@ -13,10 +13,10 @@
 # preloaded into python.  One runtime for both libraries (clang's), so the
 # oracle is built with the ROCm clang rather than gcc here.
 #
-# Usage: tools/sanitize.sh [log]   (default log: profiles/r05_sanitizer_cpu.log)
+# Usage: tools/sanitize.sh [log]   (default log: profiles/r06_sanitizer_cpu.log)
 set -euo pipefail
 cd "$(dirname "$0")/.."
-LOG=${1:-profiles/r05_sanitizer_cpu.log}
+LOG=${1:-profiles/r06_sanitizer_cpu.log}
 LLVM=/opt/rocm/lib/llvm/bin
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 OUT=build/asan
