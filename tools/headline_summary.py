@@ -45,9 +45,26 @@ def main():
     }
     rk = kern.get(dom)
     if rk:
+        # the dominant kernel's dispatches in the trace run's timed region:
+        # after its `warmup` launches, the next `steps` (the power probe's
+        # launches follow them and enter rocprof's all-dispatch average)
+        trows = []
+        for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if pmc_summary.short(r["Kernel_Name"]) == dom:
+                    trows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        trows.sort()
+        w, st = tline["warmup"], tline["steps"]
+        timed = trows[w:w + st]
+        timed_ms = sum(e - b for b, e in timed) / len(timed) / 1e6 if timed else None
         out["reconcile"] = {
-            "rocprof_avg_ms": rk["avg_ms"], "bench_ms_per_step": line["ms_per_step"],
-            "rocprof_over_bench": rk["avg_ms"] / line["ms_per_step"],
+            "rocprof_avg_ms_all_dispatches": rk["avg_ms"], "rocprof_dispatches": rk["calls"],
+            "rocprof_timed_avg_ms": timed_ms, "rocprof_timed_dispatches": len(timed),
+            "trace_run_ms_per_step": tline["ms_per_step"],
+            "rocprof_timed_over_trace_step": timed_ms / tline["ms_per_step"] if timed_ms else None,
+            "bench_ms_per_step": line["ms_per_step"],
+            "bench_kernel_avg_ms_hip_events": roof["kernels"][dom]["avg_ms"],
+            "rocprof_timed_over_bench_step": timed_ms / line["ms_per_step"] if timed_ms else None,
             "sclk_bench_mhz": (line.get("power") or {}).get("sclk_mhz_median"),
             "sclk_trace_mhz": (tline.get("power") or {}).get("sclk_mhz_median"),
         }
