@@ -397,3 +397,30 @@ def test_fused_mul_relin_rescale_errors(gpu):
         rn.check(lib.rnt_ct_mul_relin_rescale(same.handle, rn.RnsPoly(Bd, 2).handle, x.handle, x.handle,
                                               x.handle, x.handle, rlk.a.handle, rlk.b.handle))
     assert e.value.kind == "BasisMismatch"
+
+
+@pytest.mark.parametrize("log_n,L,B,bits", [(16, 16, 3, 31), (14, 8, 5, 31), (14, 3, 3, 61), (15, 4, 3, 31)])
+def test_keyswitch_diagonal_from_tensor(gpu, monkeypatch, log_n, L, B, bits):
+    """The ct-mul key-switch takes its diagonal (source limb i of target limb
+    i) from the tensor's exact d2^ instead of transforming S (the matrix-core
+    tensor at 2^16, the four-step tensor rows elsewhere, u32 and u64): the
+    relinearised product equals the RNT_KS_DIAG=0 path, which transforms
+    every (i, j), word for word, and the oracle on the first pair."""
+    rn = gpu
+    n = 1 << log_n
+    mod = rn.generate_primes(bits, L, n)
+    Bo = orc.Basis(mod, n)
+    rng = np.random.default_rng(900 + log_n)
+    c0, c1, c0p, c1p = (_rand(rng, mod, n, B) for _ in range(4))
+    ka, kb = _rand(rng, mod, n, L), _rand(rng, mod, n, L)
+    outs = []
+    for diag in ("1", "0"):
+        monkeypatch.setenv("RNT_KS_DIAG", diag)  # read at rnt_ctx_create
+        Bd = rn.RnsBasis(mod, n)
+        rlk = rn.RnsGadgetKey.from_channels(ka, kb, Bd)
+        up = lambda x: rn.RnsPoly.from_channels(x, Bd)  # noqa: E731
+        r = rn.mul_ciphertexts_gadget(rn.Ciphertext(up(c0), up(c1)), rn.Ciphertext(up(c0p), up(c1p)), rlk)
+        outs.append((r.c0.channels(), r.c1.channels()))
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    w0, w1 = orc.mul_ciphertexts_gadget(Bo, c0[0], c1[0], c0p[0], c1p[0], ka, kb, threads=T)
+    assert np.array_equal(outs[0][0][0], w0) and np.array_equal(outs[0][1][0], w1)

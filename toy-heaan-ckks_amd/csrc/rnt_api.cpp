@@ -783,6 +783,10 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     // the same Harvey-lazy product path for u64 bases of primes < 2^62 (the
     // reference's 40/61/62-bit tests); RNT_LAZY62=0 keeps the canonical one
     t->lazy62 = wide && lazy62 && env_long("RNT_LAZY62", 1) != 0;
+    // the ct-mul's key-switch takes its diagonal (source limb i of target
+    // limb i) from the tensor's exact d2^ instead of transforming it;
+    // RNT_KS_DIAG=0 transforms every (i, j) (A/B)
+    t->ks_diag = env_long("RNT_KS_DIAG", 1) != 0;
     // the whole-plane product and MFMA transforms are the default where they
     // apply (N = 2^16, u32); RNT_PLANE=0 keeps the four-step kernels
     t->plane = env_long("RNT_PLANE", 1) != 0 ? 1 : 0;
@@ -2098,7 +2102,11 @@ static int ct_mul_relin_body(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, co
   const size_t chunk_words = L * bc * n;
   // (the matrix-core tensor's scratch: plane_scratch_planes(L bc) <= L bc planes)
   const size_t nt = whole ? 0 : mf ? 1 : 4;
-  const size_t need = ((nt + 3) * chunk_words + ks_scratch_words(k.t, L, bc) + (resc ? 2 * bc * n : 0)) * wb;
+  // the key-switch's diagonal from the tensor's d2^ (one more chunk plane
+  // set, D2H): the four-step key-switch on tiled grids, whose tensor writes it
+  const bool diag = k.t->ks_diag && !whole && !rnt::ks_whole_ok(k.t) && rnt::col_resc_ok(k.t);
+  const size_t need = ((nt + 3 + (diag ? 1 : 0)) * chunk_words + ks_scratch_words(k.t, L, bc) +
+                       (resc ? 2 * bc * n : 0)) * wb;
   CallWs cws(out0);
   if (int rc = cws.get(need)) return rc;
   char* ws = (char*)cws.p;
@@ -2108,12 +2116,20 @@ static int ct_mul_relin_body(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, co
   char* D1 = D0 + chunk_words * wb;
   char* D2 = D1 + chunk_words * wb;
   char* KS = D2 + chunk_words * wb;
+  char* D2H = nullptr;
+  if (diag) {
+    D2H = KS + ks_scratch_words(k.t, L, bc) * wb + (resc ? 2 * bc * n * wb : 0);
+  }
   const uint64_t full_ls = limb_stride(c0);
   for (size_t p0 = 0; p0 < B; p0 += bc) {
     const size_t c = std::min(bc, B - p0);
     rnt::Launch kc = k;
     kc.B = c;
     const uint64_t cls = (uint64_t)c * n;
+    if (diag) {
+      kc.d2hat = D2H;  // written by the tensor, read by the key-switch rows
+      kc.d2hat_ls = cls;
+    }
     auto off = [&](const rnt_buf* b) { return (const char*)b->data + p0 * n * wb; };
     if (whole) {
       // d0^, d1^ NTT-resident and d2 in coefficient domain (engine.rs:486-493), one
@@ -2172,7 +2188,7 @@ static int ct_mul_relin_body(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, co
     d2view.ctx = c0->ctx;
     d2view.n_polys = c;
     d2view.data = D2;
-    if (int rc = ks_chunk_run(k, KS, &d2view, 0, c, key_a, key_b, (char*)out0->data + p0 * n * wb,
+    if (int rc = ks_chunk_run(kc, KS, &d2view, 0, c, key_a, key_b, (char*)out0->data + p0 * n * wb,
                               (char*)out1->data + p0 * n * wb, full_ls, D0, D1, cls, nullptr, 1))
       return rc;
     d2view.data = nullptr;  // not owned

@@ -82,6 +82,7 @@ struct Tables {
   int wide = 0;            // 0: W = u32, 1: W = u64
   bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path (u32)
   bool lazy62 = false;     // u64 words, every modulus < 2^62: the same for u64
+  bool ks_diag = true;     // ct-mul key-switch diagonal from the tensor's d2^ (RNT_KS_DIAG)
   int plane = 0;           // the whole-plane kernels where they apply (plane_ok, mf_ok);
   int mf_mul = 1;          // rnt_mul at N = 2^16 on the matrix-core transforms (RNT_MF_MUL=0: k_plane_fused)
                            // RNT_PLANE=0: the four-step kernels everywhere
@@ -184,6 +185,12 @@ struct Launch {
   size_t B;            // polys per buffer
   hipStream_t s;
   size_t Ls = 0;       // key-switch source limbs (0: same as L)
+  // The ct-mul key-switch's diagonal (source limb i == target limb i, the
+  // same basis): the tensor launches write the exact d2^ here ([L][B][N],
+  // limb stride d2hat_ls), the decomposition skips those planes and the
+  // key-switch rows read them instead of transforming S (nullptr: off)
+  void* d2hat = nullptr;
+  uint64_t d2hat_ls = 0;
   size_t src_limbs() const { return Ls ? Ls : L; }
 };
 

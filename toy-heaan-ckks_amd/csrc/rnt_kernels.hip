@@ -620,7 +620,7 @@ template <class W, int LOG_R, int LOG_TC>
 __global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint32_t log_n,
                  uint32_t log_c, uint32_t L, uint32_t B, uint64_t d_ls, uint32_t Lt,
-                 uint32_t jg, uint32_t lift_csub) {
+                 uint32_t jg, uint32_t lift_csub, uint32_t skip_diag) {
   using G = ColGeo<LOG_R, LOG_TC>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -646,6 +646,9 @@ k_colt_decompose(W* __restrict__ S, const W* __restrict__ d, TabPtrs<W> tp, uint
   for (int e = 0; e < E; ++e) raw[e] = src.ld(a0.v, e * a0.s);
 #pragma unroll 1
   for (uint32_t j = j0; j < j1; ++j) {
+    // the diagonal (target j == source i) is the tensor's own d2^ (k_ks_rows
+    // reads it there): no transform, no S plane
+    if (skip_diag && j == i) continue;
     const BufView<W> dst(S + (((uint64_t)j * L + i) * B + p) * N, N);
     const LimbConst<W> lc = tp.lc[j];
     W x[1][E];
@@ -911,7 +914,7 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
           const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
           const W* __restrict__ init0, const W* __restrict__ init1, uint64_t init_ls,
           TabPtrs<W> tp, uint32_t log_n, uint32_t L, uint32_t B, uint64_t ls, uint32_t pgroups,
-          uint32_t nblocks) {
+          uint32_t nblocks, const W* __restrict__ d2hat, uint64_t d2hat_ls) {
   using G = RowGeo<LOG_C>;
   constexpr int E = G::E;
   constexpr int C = G::C;
@@ -993,6 +996,13 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     const uint64_t sbase = (((uint64_t)j * L + i) * B + rp.p) * N + rowoff;
     const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + (WIDE ? (uint64_t)rbase * G::C : rowoff);
     W x[1][E];
+    // the diagonal (source limb i == target limb j): x is the tensor's exact
+    // d2^ row, already in the last pass's layout -- no S row, no transform.
+    // Without the transform's exchange barriers, one barrier before the key
+    // loads (every read of the earlier limbs' key rows, and of key_a's in
+    // the exchange region, is done) and one after them publish the rows
+    const bool diag = d2hat != nullptr && i == j;
+    if (diag) __syncthreads();
     // one key buffer: every thread's reads of the previous limb's keys
     // finish before it is rewritten
     if constexpr (!KDOUBLE) __syncthreads();
@@ -1020,8 +1030,14 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
       // (in-order) vmcnt wait for x below also covers them; the exchange
       // barriers after it then publish kb to the other waves
       __builtin_amdgcn_sched_barrier(0);
+      if (diag) {
+        const uint64_t hb = (uint64_t)j * d2hat_ls + (uint64_t)rp.p * N + rowoff + bl;
 #pragma unroll
-      for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
+        for (int e = 0; e < E; ++e) x[0][e] = d2hat[hb + (uint32_t)e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
+      }
       if constexpr (G::P < 2) {
         // no exchange barrier follows: wait for this wave's DMA explicitly
         // before the barrier below publishes kb
@@ -1034,8 +1050,14 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
         const uint32_t w = threadIdx.x + (uint32_t)m * G::THREADS;
         if (w < 2u * KW) kr[m] = w < KW ? key_b[kbase + w] : key_a[kbase + w - KW];
       }
+      if (diag) {
+        const uint64_t hb = (uint64_t)j * d2hat_ls + (uint64_t)rp.p * N + rowoff + bl;
 #pragma unroll
-      for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
+        for (int e = 0; e < E; ++e) x[0][e] = d2hat[hb + (uint32_t)e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[0][e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
+      }
 #pragma unroll
       for (int m = 0; m < KPT; ++m) {
         const uint32_t w = threadIdx.x + (uint32_t)m * G::THREADS;
@@ -1048,8 +1070,13 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     // the transform's LDS exchange ends in barriers that publish kb (and
     // order the reads of this slot two limbs ago before this write); a
     // single-pass row has none, so it gets one here
-    if constexpr (G::P < 2) __syncthreads();
-    xf_fwd<G, W, 1>(x, rp.xp, lds, tw, mod_of(lc));
+    if (diag) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's key DMA has landed
+      __syncthreads();
+    } else {
+      if constexpr (G::P < 2) __syncthreads();
+      xf_fwd<G, W, 1>(x, rp.xp, lds, tw, mod_of(lc));
+    }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (KSPLIT) {
       // the transform's last exchange has ended in a barrier: the exchange
@@ -1255,7 +1282,7 @@ __global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? kTens
 k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2row,
               const W* __restrict__ c0, const W* __restrict__ c1, const W* __restrict__ c0p,
               const W* __restrict__ c1p, TabPtrs<W> tp, uint32_t log_n, uint32_t B, uint64_t ls,
-              uint64_t rows_total, uint64_t in_ls) {
+              uint64_t rows_total, uint64_t in_ls, W* __restrict__ d2hat) {
   using G = RowGeo<LOG_C>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -1286,6 +1313,7 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
   }
   xf_fwd<G, W, 2>(b, rp.xp, lds, tw, mod_of(lc));
   W d2[1][E];
+  W o0[E], o1[E];
   W nqi = (W)0 - lc.qinv;
   asm volatile("" : "+v"(nqi));  // one multiply per REDC (see mont_mul_nq)
 #pragma unroll
@@ -1305,10 +1333,39 @@ k_tensor_rows(W* __restrict__ d0hat, W* __restrict__ d1hat, W* __restrict__ d2ro
       d1 = add_mod<W>(mont_mul<W>(a[0][i], b[1][i], q, qi), mont_mul<W>(a[1][i], b[0][i], q, qi), q);
       d2[0][i] = mont_mul<W>(a[1][i], b[1][i], q, qi);
     }
-    if (rp.active) {
-      const uint32_t pos = bl + ((uint32_t)i << G::BBL);
-      d0hat[base + pos] = d0;
-      d1hat[base + pos] = d1;
+    o0[i] = d0;
+    o1[i] = d1;
+  }
+  // the last pass leaves a thread's E words consecutive (G::BBL == 0): the
+  // outputs go as 16-byte stores (four 4-byte stores 64 bytes apart per lane
+  // before: the exact d2^ as a third such stream cost the config-3 tensor
+  // 44%, profiles/r06/ab_ks_diag.txt)
+  static_assert(G::BBL == 0, "consecutive output words");
+  if (rp.active && (E * sizeof(W)) % 16 != 0) {  // rows shorter than 16 bytes a thread
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      d0hat[base + bl + i] = o0[i];
+      d1hat[base + bl + i] = o1[i];
+      if (d2hat != nullptr) d2hat[base + bl + i] = shoup_mul<W>(d2[0][i], lc.rmod, lc.rmod_p, lc.q);
+    }
+  } else if (rp.active) {
+    constexpr int V = 16 / sizeof(W) < E ? 16 / sizeof(W) : E;
+    uint4* p0 = (uint4*)(d0hat + base + bl);
+    uint4* p1 = (uint4*)(d1hat + base + bl);
+#pragma unroll
+    for (int t = 0; t < E / V; ++t) {
+      p0[t] = *(const uint4*)&o0[t * V];
+      p1[t] = *(const uint4*)&o1[t * V];
+    }
+    if (d2hat != nullptr) {
+      // the exact d2^ (times 2^w by a Shoup product): the key-switch's own
+      // source-limb-i transform of target limb i (its diagonal, k_ks_rows)
+      W h[E];
+#pragma unroll
+      for (int i = 0; i < E; ++i) h[i] = shoup_mul<W>(d2[0][i], lc.rmod, lc.rmod_p, lc.q);
+      uint4* ph = (uint4*)(d2hat + base + bl);
+#pragma unroll
+      for (int t = 0; t < E / V; ++t) ph[t] = *(const uint4*)&h[t * V];
     }
   }
   xf_inv<G, W, 1, WHOLE>(d2, rp.xp, lds, itw, mod_of(lc),
@@ -1913,13 +1970,15 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
     uint64_t qmin = ~0ull;
     for (uint64_t q : k.t->moduli) qmin = q < qmin ? q : qmin;
     const uint32_t lift_csub = sizeof(W) == 4 && qmin >= (1ull << 30) ? 1u : 0u;
+    if (k.d2hat != nullptr && Ls != (uint32_t)k.L) return hipErrorInvalidValue;  // the diagonal needs one basis
+    const uint32_t skip_diag = k.d2hat != nullptr ? 1u : 0u;
     hipError_t e = hipSuccess;
 #define RNT_L2(R, TC)                                                                         \
   e = allow_lds(k_colt_decompose<W, R, TC>, col_lds<W, R, TC>());                             \
   if (e != hipSuccess) return e;                                                              \
   hipLaunchKernelGGL((k_colt_decompose<W, R, TC>), grid, dim3(ColGeo<R, TC>::THREADS),        \
                      (col_lds<W, R, TC>()), k.s, (W*)S, (const W*)d, tp, g.log_n, g.log_c,      \
-                     Ls, (uint32_t)k.B, d_ls, (uint32_t)k.L, jg, lift_csub)
+                     Ls, (uint32_t)k.B, d_ls, (uint32_t)k.L, jg, lift_csub, skip_diag)
 #define RNT_L(R)                          \
   if (col_log_tc(g) == 6) {               \
     RNT_L2(R, 6);                         \
@@ -1931,6 +1990,7 @@ static hipError_t ks_decompose_t(const Launch& k, void* S, const void* d, uint64
 #undef RNT_L2
     return hipGetLastError();
   }
+  if (k.d2hat != nullptr) return hipErrorInvalidValue;  // the diagonal skip: tiled grids only
   const uint64_t total = (uint64_t)k.L * Ls * k.B * g.c;
 #define RNT_L(R)                                                                               \
   hipLaunchKernelGGL((k_ks_decompose<W, R>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,  \
@@ -1965,7 +2025,7 @@ static hipError_t ks_rows_launch(const Launch& k, void* u0, void* u1, uint64_t l
                      (W*)u0, (W*)u1, (const W*)S, (const W*)key_a, (const W*)key_b, key_ls,
                      (const W*)init0, (const W*)init1, init_ls, tab_ptrs<W>(k.t), g.log_n,
                      (uint32_t)k.src_limbs(), (uint32_t)k.B, ls, (uint32_t)pgroups,
-                     (uint32_t)blocks);
+                     (uint32_t)blocks, (const W*)k.d2hat, k.d2hat_ls);
   return hipGetLastError();
 }
 
@@ -2048,7 +2108,8 @@ static hipError_t tensor_rows_launch(const Launch& k, void* d0hat, void* d1hat, 
   hipLaunchKernelGGL((k_tensor_rows<W, LOG_C, WHOLE>), dim3(blocks), dim3(G::THREADS), lds, k.s,
                      (W*)d0hat, (W*)d1hat, (W*)d2row, (const W*)c0, (const W*)c1,
                      (const W*)c0p, (const W*)c1p, tab_ptrs<W>(k.t),
-                     WHOLE ? (uint32_t)LOG_C : g.log_n, (uint32_t)k.B, ls, rows, in_ls);
+                     WHOLE ? (uint32_t)LOG_C : g.log_n, (uint32_t)k.B, ls, rows, in_ls,
+                     (W*)(WHOLE ? nullptr : k.d2hat));  // (its stride is the outputs' ls)
   return hipGetLastError();
 }
 

@@ -1038,7 +1038,8 @@ __global__ void __launch_bounds__(mf::kT, 1)
 k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __restrict__ d2, uint64_t ols,
             const uint32_t* __restrict__ c0, const uint32_t* __restrict__ c1, const uint32_t* __restrict__ c0p,
             const uint32_t* __restrict__ c1p, uint64_t ils, uint32_t* __restrict__ scratch, uint32_t slots,
-            const void* __restrict__ mft, const LimbConst<uint32_t>* __restrict__ lcs) {
+            const void* __restrict__ mft, const LimbConst<uint32_t>* __restrict__ lcs,
+            uint32_t* __restrict__ d2hat) {
   using namespace mf;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   uint32_t* lds = (uint32_t*)smem_raw;
@@ -1058,6 +1059,10 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
   }
   const Rsrc R0 = rsrc(d0 + oo, kN * 4u), R1 = rsrc(d1 + oo, kN * 4u), R2 = rsrc(d2 + oo, kN * 4u);
   const Rsrc RS = rsrc(scratch + so, kN * 4u);
+  // the exact d2^ (c1^ c1'^, canonical, device order): the key-switch's
+  // diagonal source row (k_ks_rows), when asked for
+  const bool want_hat = d2hat != nullptr;
+  const Rsrc RH = rsrc(want_hat ? d2hat + oo : d2 + oo, kN * 4u);
   // The lane offset is computed once per kernel, and the epilogues'
   // products are plain C++.
   const uint32_t pl = p4_lane(h);
@@ -1128,6 +1133,9 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
     }
     pin4(xx[p3(cc, 0)], xx[p3(cc, 1)], xx[p3(cc, 2)], xx[p3(cc, 3)]);  // (as in k_mf_mul)
     bst<kLastAux>(o1, R1, pl, p4_soff(h, cc));
+    if (want_hat)
+      bst<kLastAux>(v4i{(int)xx[p3(cc, 0)], (int)xx[p3(cc, 1)], (int)xx[p3(cc, 2)], (int)xx[p3(cc, 3)]}, RH, pl,
+                    p4_soff(h, cc));
   });
   inv_x<false>(x, R2, lds, h, T);
 }
@@ -1437,7 +1445,8 @@ hipError_t launch_mf_tensor(const Launch& k, void* d0, void* d1, void* d2, uint6
   uint32_t slots = (uint64_t)k.B * k.L >= kPlaneSlots ? 1u : 0u;  // plane_scratch_planes
   const void* mft = k.t->mf;
   const LimbConst<uint32_t>* lcs = (const LimbConst<uint32_t>*)k.t->lconst;
-  void* args[] = {&d0, &d1, &d2, &ols, &c0, &c1, &c0p, &c1p, &ils, &scratch, &slots, &mft, &lcs};
+  void* d2hat = k.d2hat;  // the exact d2^ for the key-switch's diagonal (its stride is ols)
+  void* args[] = {&d0, &d1, &d2, &ols, &c0, &c1, &c0p, &c1p, &ils, &scratch, &slots, &mft, &lcs, &d2hat};
   return hipLaunchKernel(fn, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), args, mf::kLdsBytes, k.s);
 }
 
