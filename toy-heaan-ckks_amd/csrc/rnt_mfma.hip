@@ -1154,6 +1154,12 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
 #ifndef RNT_MF_MUL_PARK
 #define RNT_MF_MUL_PARK 4
 #endif
+// RNT_MF_MUL_MEAS (measurement build only, wrong results by design): the
+// a^ tiles that go through memory are neither stored nor read back -- the
+// rate a design keeping all of a^ on the CU could reach at best
+#ifndef RNT_MF_MUL_MEAS
+#define RNT_MF_MUL_MEAS 0
+#endif
 constexpr int kMulLdsTiles = RNT_MF_MUL_Q4 ? 6 : 2;  // a^ tiles per wave kept in the LDS (k_mf_mul)
 constexpr uint32_t kMulLdsBase = RNT_MF_MUL_Q4 ? (1u << 14) : (1u << 15);  // words
 static_assert(kMulLdsBase * 4 + (size_t)kMulLdsTiles * 16 * 1024 <= mf::kLdsBytes, "in the LDS");
@@ -1198,14 +1204,15 @@ k_mf_mul(uint32_t* c, const uint32_t* a, const uint32_t* b, uint64_t ls, uint32_
   fwd<false, S_F4S, false, RNT_MF_MUL_Q4 != 0, NP, kMulLdsBase * 4, kMulLdsTiles * 1024>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     if (cc >= 16 - kMulLdsTiles)
       hat(cc - (16 - kMulLdsTiles)) = v4i{r[0], r[1], r[2], r[3]};
-    else
+    else if (!RNT_MF_MUL_MEAS)
       bst(v4i{r[0], r[1], r[2], r[3]}, RS, p4_lane(h), p4_soff(h, cc));
   });
   // fwd(b) needs no barrier before its first exchange write with Q4: every
   // wave passed fwd(a)'s SYNCX after its last read of fwd(a)'s exchange,
   // and fwd(b)'s quarter rounds stay below the a^ tiles
   fwd<!(RNT_MF_MUL_Q4 && RNT_MF_MUL_NOSYNC1), S_F4, RNT_MF_MUL_Q4 != 0, (NP > 0), NP, 0, 4096>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
-    const v4i ah = cc >= 16 - kMulLdsTiles ? hat(cc - (16 - kMulLdsTiles)) : bld(RS, p4_lane(h), p4_soff(h, cc));
+    const v4i ah = cc >= 16 - kMulLdsTiles ? hat(cc - (16 - kMulLdsTiles))
+                   : RNT_MF_MUL_MEAS ? v4i{r[0], r[1], r[2], r[3]} : bld(RS, p4_lane(h), p4_soff(h, cc));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       // (a^ 2^32) b^ 2^-32, a signed Montgomery product of two pass
