@@ -849,19 +849,41 @@ __device__ __forceinline__ uint32_t ks_pad(uint32_t w) { return w + ((w >> 6) <<
 //    the exchange region once the transform's last exchange is done, so
 //    four workgroups fit a CU (three left a 1024-workgroup grid 1.33
 //    rounds long).
+//  * KREG: the one-poly grid (NP = 1) of u32 rows of >= 64 words shares no
+//    key word between threads, so each thread loads its own E words of both
+//    keys straight into registers, issued with the S row and landing while
+//    the row transform runs; no key LDS, no key barriers.  With KSPLIT the
+//    one-ciphertext rotation waited twice a source limb (S + key_b, then
+//    key_a after the transform).  RNT_KS_SPRE: the S row of the next source
+//    limb also loads one limb ahead (16 registers).  Off: parity-green, but
+//    the 32 key registers live across the transform spill (176 bytes a lane
+//    without SPRE, 352 with it, against 104) and the rows kernel measured
+//    0.4749 / 0.6573 ms against 0.4513 ms a one-ciphertext rotation at config
+//    5 (profiles/r06/ab_ks_kreg.txt); with the loads after the transform
+//    (RNT_KS_KLATE) hipcc still spills 272 bytes.
+#ifndef RNT_KS_KREG
+#define RNT_KS_KREG 0
+#endif
+#ifndef RNT_KS_SPRE
+#define RNT_KS_SPRE 1
+#endif
+#ifndef RNT_KS_KLATE
+#define RNT_KS_KLATE 0
+#endif
 template <class W, int LOG_C, int NP>
 struct KsCfg {
   using G = RowGeo<LOG_C>;
   static constexpr int KROWS = G::RPW / NP;
   static constexpr int KPAD = ks_kpad_words<W>(G::C);
+  static constexpr bool KREG = RNT_KS_KREG && sizeof(W) == 4 && G::C >= 64 && NP == 1 && G::RPW > 1;
   static constexpr bool KDOUBLE =
-      (size_t)(G::REGION + 4 * KROWS * KPAD) * sizeof(W) <= 40u * 1024u || KROWS == 1;
-  static constexpr bool KSPLIT = sizeof(W) == 4 && G::C >= 64 && !KDOUBLE && G::P >= 2 &&
+      !KREG && ((size_t)(G::REGION + 4 * KROWS * KPAD) * sizeof(W) <= 40u * 1024u || KROWS == 1);
+  static constexpr bool KSPLIT = !KREG && sizeof(W) == 4 && G::C >= 64 && !KDOUBLE && G::P >= 2 &&
                                  (size_t)(G::REGION + 2 * KROWS * KPAD) * sizeof(W) > 40u * 1024u &&
                                  KROWS * KPAD <= G::REGION;
   static constexpr bool KEYGLDS =
-      sizeof(W) == 4 && G::C >= 64 && (NP > 1 || LOG_C >= kKsGldsWideMinLogC || KSPLIT);
-  static constexpr int KWORDS = (KDOUBLE ? 4 : KSPLIT ? 1 : 2) * KROWS * KPAD;
+      !KREG && sizeof(W) == 4 && G::C >= 64 && (NP > 1 || LOG_C >= kKsGldsWideMinLogC || KSPLIT);
+  static constexpr int KWORDS = KREG ? 0 : (KDOUBLE ? 4 : KSPLIT ? 1 : 2) * KROWS * KPAD;
   static constexpr size_t LDS_BYTES = (size_t)(G::REGION + KWORDS) * sizeof(W);
 };
 
@@ -989,6 +1011,60 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     acc[1][e] = init1 ? init1[ibase + pos] : (W)0;
   }
   constexpr uint32_t KW = (uint32_t)(KROWS * C);  // words per key
+  if constexpr (K::KREG) {
+    // the source row of limb i: S[j][i][p] in the first pass's layout, or on
+    // the diagonal the tensor's exact d2^ row in the last pass's (no
+    // transform, so no LDS and no barrier that iteration: every wave passes
+    // the same barriers, diag being uniform over the workgroup)
+    auto src_row = [&](uint32_t i, W (&v)[E]) {
+      if (d2hat != nullptr && i == j) {
+        const uint64_t hb = (uint64_t)j * d2hat_ls + (uint64_t)rp.p * N + rowoff + bl;
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = d2hat[hb + (uint32_t)e];
+      } else {
+        const uint64_t sbase = (((uint64_t)j * L + i) * B + rp.p) * N + rowoff;
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
+      }
+    };
+    W xn[E];
+    if constexpr (RNT_KS_SPRE) src_row(0, xn);
+#pragma unroll 1
+    for (uint32_t i = 0; i < L; ++i) {
+      W x[1][E];
+      if constexpr (RNT_KS_SPRE) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) x[0][e] = xn[e];
+        if (i + 1 < L) src_row(i + 1, xn);
+      } else {
+        src_row(i, x[0]);
+      }
+      // this thread's E consecutive words (the last pass's layout, bl + e)
+      // of both keys' row: 16-byte loads, consecutive across the row's threads
+      W kv[2][E];
+      const uint64_t kt = (uint64_t)j * key_ls + (uint64_t)i * N + rowoff + bl;
+      auto load_keys = [&]() {
+#pragma unroll
+        for (int e = 0; e < E; e += 4) {
+          const uint4 b4 = *(const uint4*)(key_b + kt + e);
+          const uint4 a4 = *(const uint4*)(key_a + kt + e);
+          kv[0][e] = b4.x; kv[0][e + 1] = b4.y; kv[0][e + 2] = b4.z; kv[0][e + 3] = b4.w;
+          kv[1][e] = a4.x; kv[1][e + 1] = a4.y; kv[1][e + 2] = a4.z; kv[1][e + 3] = a4.w;
+        }
+      };
+      // RNT_KS_KLATE: the key loads after the transform (32 registers fewer
+      // live across it, their latency exposed)
+      if constexpr (!RNT_KS_KLATE) load_keys();
+      if (!(d2hat != nullptr && i == j)) xf_fwd<G, W, 1>(x, rp.xp, lds, tw, mod_of(lc));
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (RNT_KS_KLATE) load_keys();
+#pragma unroll
+      for (int o = 0; o < 2; ++o)
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[o][e] = mac_lazy(acc[o][e], x[0][e], kv[o][e], lc.q, q2, nqinv);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
 #pragma unroll 1
   for (uint32_t i = 0; i < L; ++i) {
     // this limb's key rows (key poly i, limb j, rows rbase ..; limb stride
@@ -1131,6 +1207,7 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+  }
   }
   // (KSPLIT: every thread's reads of the last key_a rows end before the
   // inverse's exchanges write that region)
@@ -2010,6 +2087,9 @@ static hipError_t ks_rows_launch(const Launch& k, void* u0, void* u1, uint64_t l
   const Geom g = geom_for(k.t->log_n);
   if (k.L == 0 || k.B == 0) return hipSuccess;
   if (g.r % KROWS) return hipErrorInvalidValue;
+  // KREG's 16-byte key loads: key planes on 16-byte boundaries
+  if (KsCfg<W, LOG_C, NP>::KREG && ((((uintptr_t)key_a | (uintptr_t)key_b) & 15u) || (key_ls & 3u)))
+    return hipErrorInvalidValue;
   // one workgroup per (target limb, group of KROWS rows, group of NP polys)
   const uint64_t pgroups = (k.B + NP - 1) / NP;
   const uint64_t blocks = (uint64_t)k.L * (g.r / KROWS) * pgroups;

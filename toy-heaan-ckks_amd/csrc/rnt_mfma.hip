@@ -983,6 +983,156 @@ __device__ __forceinline__ void inv(Rsrc pr, uint32_t* lds, const Th& h, const T
   inv_x<true>(x2, pr, lds, h, T);
 }
 
+// ---- two virtual waves a wave (k_mf_mul2) -----------------------------------
+// fwd and inv_x for a 512-thread workgroup whose wave p carries the sixteen-
+// wave layout's waves 2p (ha, xa) and 2p + 1 (hb, xb): every pass runs once
+// for each, the barriers once for both.  The per-wave state of the 1024-thread
+// layout (x, a^, the VGPRs of the working set) is then held by half as many
+// threads, and the register file left over keeps a^ tiles on the CU.
+template <bool SYNC1, int F4, bool Q4, bool SYNCX, int NPARK, uint32_t PBASE, uint32_t PSTRIDE, class EA, class EB>
+__device__ __forceinline__ void fwd2(uint32_t (&xa)[64], uint32_t (&xb)[64], Rsrc src, uint32_t* lds, const Th& ha,
+                                     const Th& hb, const Tabs& T, const EA& epa, const EB& epb) {
+  const Mc& m = T.m;
+  const uint32_t lo = ha.lam() * 16u;
+  v4i M[4];
+  load_mat(M, T.tab, S_F1, lo);
+  const v4i comp = bld(T.tab, lo, (uint32_t)kCompF1 * 16u);
+  uint32_t x1a[64], x1b[64];
+  load_p1(x1a, src, ha);
+  load_p1(x1b, src, hb);
+  pass_p1<0, true>(x1a, M, comp, m);
+  pass_p1<0, true>(x1b, M, comp, m);
+  if constexpr (SYNC1) __syncthreads();
+  uint32_t wb[4], rb[4];
+  const uint32_t t3v = ha.g() * 256u;
+  auto t3s = [](const Th& h) { return (uint32_t)(kTw3f + h.w * 64) * 16u; };
+  if constexpr (Q4) {
+    p1_bases4(wb, ha); x_write_p1q<0>(x1a, lds, wb);
+    p1_bases4(wb, hb); x_write_p1q<0>(x1b, lds, wb);
+    pass_p1<8, true>(x1a, M, comp, m);
+    pass_p1<8, true>(x1b, M, comp, m);
+    __syncthreads();
+    p2_bases4(rb, ha); x_read_p2q<0>(xa, lds, rb);
+    p2_bases4(rb, hb); x_read_p2q<0>(xb, lds, rb);
+    __syncthreads();
+    p1_bases4(wb, ha); x_write_p1q<1>(x1a, lds, wb);
+    p1_bases4(wb, hb); x_write_p1q<1>(x1b, lds, wb);
+    __syncthreads();
+    p2_bases4(rb, ha); x_read_p2q<1>(xa, lds, rb);
+    p2_bases4(rb, hb); x_read_p2q<1>(xb, lds, rb);
+    __syncthreads();
+    p1_bases4(wb, ha); x_write_p1q<2>(x1a, lds, wb);
+    p1_bases4(wb, hb); x_write_p1q<2>(x1b, lds, wb);
+    load_mat(M, T.tab, S_F2 + ha.w, lo);
+    pass_p2<0>(xa, M, T.tab, t3v, t3s(ha), m);
+    load_mat(M, T.tab, S_F2 + hb.w, lo);
+    pass_p2<0>(xb, M, T.tab, t3v, t3s(hb), m);
+    __syncthreads();
+    p2_bases4(rb, ha); x_read_p2q<2>(xa, lds, rb);
+    p2_bases4(rb, hb); x_read_p2q<2>(xb, lds, rb);
+    __syncthreads();
+    p1_bases4(wb, ha); x_write_p1q<3>(x1a, lds, wb);
+    p1_bases4(wb, hb); x_write_p1q<3>(x1b, lds, wb);
+    __syncthreads();
+    p2_bases4(rb, ha); x_read_p2q<3>(xa, lds, rb);
+    p2_bases4(rb, hb); x_read_p2q<3>(xb, lds, rb);
+  } else {
+    p1_bases(wb, ha); x_write_p1<0>(x1a, lds, wb);
+    p1_bases(wb, hb); x_write_p1<0>(x1b, lds, wb);
+    pass_p1<8, true>(x1a, M, comp, m);
+    pass_p1<8, true>(x1b, M, comp, m);
+    __syncthreads();
+    p2_bases(rb, ha); x_read_p2<0>(xa, lds, rb);
+    p2_bases(rb, hb); x_read_p2<0>(xb, lds, rb);
+    __syncthreads();
+    p1_bases(wb, ha); x_write_p1<1>(x1a, lds, wb);
+    p1_bases(wb, hb); x_write_p1<1>(x1b, lds, wb);
+    load_mat(M, T.tab, S_F2 + ha.w, lo);
+    pass_p2<0>(xa, M, T.tab, t3v, t3s(ha), m);
+    load_mat(M, T.tab, S_F2 + hb.w, lo);
+    pass_p2<0>(xb, M, T.tab, t3v, t3s(hb), m);
+    __syncthreads();
+    p2_bases(rb, ha); x_read_p2<1>(xa, lds, rb);
+    p2_bases(rb, hb); x_read_p2<1>(xb, lds, rb);
+  }
+  if constexpr (SYNCX) __syncthreads();
+  static_assert(NPARK == 0 || SYNCX, "the park area is free only past SYNCX");
+#pragma unroll
+  for (int c = 0; c < NPARK; ++c) {
+    stash_put(park_addr<NPARK, PBASE, PSTRIDE>(lds, ha), c, xa[4 * c], xa[4 * c + 1], xa[4 * c + 2], xa[4 * c + 3]);
+    stash_put(park_addr<NPARK, PBASE, PSTRIDE>(lds, hb), c, xb[4 * c], xb[4 * c + 1], xb[4 * c + 2], xb[4 * c + 3]);
+  }
+  load_mat(M, T.tab, S_F2 + ha.w, lo);
+  pass_p2<8>(xa, M, T.tab, t3v, t3s(ha), m);
+  load_mat(M, T.tab, S_F2 + hb.w, lo);
+  pass_p2<8>(xb, M, T.tab, t3v, t3s(hb), m);
+#pragma unroll
+  for (int c = 0; c < NPARK; ++c) {
+    const v4i va = stash_get(park_addr<NPARK, PBASE, PSTRIDE>(lds, ha), c);
+    const v4i vb = stash_get(park_addr<NPARK, PBASE, PSTRIDE>(lds, hb), c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xa[4 * c + i] = (uint32_t)va[i];
+      xb[4 * c + i] = (uint32_t)vb[i];
+    }
+  }
+  swap_p2p3(xa);
+  swap_p2p3(xb);
+  load_mat(M, T.tab, S_F3, lo);
+  pass_p3(xa, M, T.tab, lo, (uint32_t)(kTw4f + ha.w * 1024) * 16u, m);
+  pass_p3(xb, M, T.tab, lo, (uint32_t)(kTw4f + hb.w * 1024) * 16u, m);
+  load_mat(M, T.tab, F4, lo);
+  pass_p4(xa, M, m, epa);
+  pass_p4(xb, M, m, epb);
+}
+
+// inv_x<false, true> for two virtual waves: the product (packed signed form,
+// P4 positions) in xa / xb to the canonical coefficients stored at pr.
+__device__ __forceinline__ void inv2(uint32_t (&xa)[64], uint32_t (&xb)[64], Rsrc pr, uint32_t* lds, const Th& ha,
+                                     const Th& hb, const Tabs& T) {
+  const Mc& m = T.m;
+  const uint32_t lo = ha.lam() * 16u;
+  v4i M[4];
+  load_mat(M, T.tab, S_I4, lo);
+  const v4i comp = {0, 0, 0, 0};  // (PK: no input bias)
+  auto t4s = [](const Th& h) { return (uint32_t)(kTw4i + h.w * 1024) * 16u; };
+  __syncthreads();  // ipass_p4's stash reuses the LDS of the last exchange and the a^ tiles
+  ipass_p4<true>(xa, M, comp, bld(T.tab, lo, t4s(ha)), T.tab, lo, t4s(ha), m, lds, ha);
+  ipass_p4<true>(xb, M, comp, bld(T.tab, lo, t4s(hb)), T.tab, lo, t4s(hb), m, lds, hb);
+  load_mat(M, T.tab, S_I3, lo);
+  ipass_p3(xa, M, T.tab, ha.g() * 16u, (uint32_t)(kTw3i + ha.w * 64) * 16u, m, lds, ha);
+  ipass_p3(xb, M, T.tab, hb.g() * 16u, (uint32_t)(kTw3i + hb.w * 64) * 16u, m, lds, hb);
+  swap_q3p2(xa);
+  swap_q3p2(xb);
+  uint32_t wb[4], rb[4];
+  uint32_t x1a[64], x1b[64];
+  load_mat(M, T.tab, S_I2 + ha.w, lo);
+  ipass_p2<0>(xa, M, m);
+  load_mat(M, T.tab, S_I2 + hb.w, lo);
+  ipass_p2<0>(xb, M, m);
+  __syncthreads();  // every wave's stash reads are done
+  p2_bases(rb, ha); x_write_p2<0>(xa, lds, rb);
+  p2_bases(rb, hb); x_write_p2<0>(xb, lds, rb);
+  load_mat(M, T.tab, S_I2 + ha.w, lo);
+  ipass_p2<8>(xa, M, m);
+  load_mat(M, T.tab, S_I2 + hb.w, lo);
+  ipass_p2<8>(xb, M, m);
+  __syncthreads();
+  p1_bases(wb, ha); x_read_p1<0>(x1a, lds, wb);
+  p1_bases(wb, hb); x_read_p1<0>(x1b, lds, wb);
+  __syncthreads();
+  p2_bases(rb, ha); x_write_p2<1>(xa, lds, rb);
+  p2_bases(rb, hb); x_write_p2<1>(xb, lds, rb);
+  load_mat(M, T.tab, S_I1, lo);
+  ipass_p1<0>(x1a, M, m, pr, ha);
+  ipass_p1<0>(x1b, M, m, pr, hb);
+  __syncthreads();
+  p1_bases(wb, ha); x_read_p1<1>(x1a, lds, wb);
+  p1_bases(wb, hb); x_read_p1<1>(x1b, lds, wb);
+  ipass_p1<8>(x1a, M, m, pr, ha);
+  ipass_p1<8>(x1b, M, m, pr, hb);
+}
+
 }  // namespace mf
 
 // Standalone transforms in place (rnt_ntt_fwd / rnt_ntt_inv at N = 2^16),
@@ -1160,6 +1310,15 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
 #ifndef RNT_MF_MUL_MEAS
 #define RNT_MF_MUL_MEAS 0
 #endif
+// RNT_MF_MUL_V2: rnt_mul at 2^16 runs k_mf_mul2 (512 threads, two virtual
+// waves a wave) instead of k_mf_mul.  Off: bit-identical, but two waves a
+// SIMD measured 11% slower at the same power (7.08 against 6.27 ms, the clock
+// 17% higher: issue-bound, not power-bound), and the registers it frees hold
+// about one a^ tile a virtual wave (+1.5%), not the ten that cost k_mf_mul
+// 7.8% (profiles/r06/ab_mf_mul2.txt, ab_mf_mul_ahat_ceiling.txt)
+#ifndef RNT_MF_MUL_V2
+#define RNT_MF_MUL_V2 0
+#endif
 constexpr int kMulLdsTiles = RNT_MF_MUL_Q4 ? 6 : 2;  // a^ tiles per wave kept in the LDS (k_mf_mul)
 constexpr uint32_t kMulLdsBase = RNT_MF_MUL_Q4 ? (1u << 14) : (1u << 15);  // words
 static_assert(kMulLdsBase * 4 + (size_t)kMulLdsTiles * 16 * 1024 <= mf::kLdsBytes, "in the LDS");
@@ -1228,6 +1387,80 @@ k_mf_mul(uint32_t* c, const uint32_t* a, const uint32_t* b, uint64_t ls, uint32_
     pin4(xx[p3(cc, 0)], xx[p3(cc, 1)], xx[p3(cc, 2)], xx[p3(cc, 3)]);
   });
   inv_x<false, true>(x, rsrc(c + o, kN * 4u), lds, h, T);
+}
+
+// RNT_MF_MUL2_REG: a^ tiles a virtual wave keeps in registers (k_mf_mul2):
+// tiles 10 - REG .. 9 (10 .. 15 stay in the LDS as in k_mf_mul; the first
+// 10 - REG go through the scratch slot)
+#ifndef RNT_MF_MUL2_REG
+#define RNT_MF_MUL2_REG 6
+#endif
+#ifndef RNT_MF_MUL2_PARK
+#define RNT_MF_MUL2_PARK 0
+#endif
+// k_mf_mul with 512 threads, each wave the two virtual waves 2p, 2p + 1 of
+// k_mf_mul's sixteen-wave layout (mf::fwd2 / inv2): the same plane
+// positions, LDS layout, tables and scratch slot indexing, so the same words
+// out; RNT_MF_MUL2_REG of the ten a^ tiles a virtual wave sent through the
+// scratch slot stay in registers instead.
+__global__ void __launch_bounds__(mf::kT / 2, 1)
+k_mf_mul2(uint32_t* c, const uint32_t* a, const uint32_t* b, uint64_t ls, uint32_t* __restrict__ scratch,
+          uint32_t slots, const void* __restrict__ mft, const LimbConst<uint32_t>* __restrict__ lcs) {
+  using namespace mf;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  uint32_t* lds = (uint32_t*)smem_raw;
+  // virtual thread ids: wave p's lane l is thread 128p + l of wave 2p and
+  // 128p + 64 + l of wave 2p + 1
+  const uint32_t tv = 2u * threadIdx.x - (threadIdx.x & 63u);
+  const Th ha(tv), hb(tv + 64u);
+  const uint32_t poly = blockIdx.x, l = blockIdx.y;
+  const uint64_t o = (uint64_t)l * ls + (uint64_t)poly * kN;
+  const LimbConst<uint32_t> lc = lcs[l];
+  const Tabs T = tabs_of(mft, lc, l);
+  uint64_t so;
+  if (slots) {
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;          // hwreg(HW_REG_XCC_ID)
+    const uint32_t cu = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 8) & 0xffu;  // hwreg(HW_REG_HW_ID)[15:8]
+    so = (uint64_t)((xcc << 8) | cu) << 16;
+  } else {
+    so = (uint64_t)(poly + l * gridDim.x) << 16;
+  }
+  const Rsrc RS = rsrc(scratch + so, kN * 4u);
+  constexpr int R = RNT_MF_MUL2_REG;
+  static_assert(R >= 0 && R <= 16 - kMulLdsTiles, "a^ register tiles");
+  constexpr int MEM = 16 - kMulLdsTiles - R;  // tiles 0 .. MEM-1 through the slot
+  v4i ra[R > 0 ? R : 1], rbv[R > 0 ? R : 1];
+  auto hat = [&](const Th& h, int t) -> v4i& {
+    return ((v4i*)(lds + kMulLdsBase) + h.w * (kMulLdsTiles * 64) + h.lam())[t * 64];
+  };
+  uint32_t xa[64], xb[64];
+  auto put = [&](const Th& h, v4i (&reg)[R > 0 ? R : 1], int cc, const int32_t (&r)[4]) {
+    const v4i v = {r[0], r[1], r[2], r[3]};
+    if (cc >= 16 - kMulLdsTiles)
+      hat(h, cc - (16 - kMulLdsTiles)) = v;
+    else if (cc >= MEM)
+      reg[cc - MEM] = v;
+    else
+      bst(v, RS, p4_lane(h), p4_soff(h, cc));
+  };
+  constexpr int NP = RNT_MF_MUL2_PARK;
+  fwd2<false, S_F4S, false, true, NP, kMulLdsBase * 4, kMulLdsTiles * 1024>(
+      xa, xb, rsrc(a + o, kN * 4u), lds, ha, hb, T,
+      [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) { put(ha, ra, cc, r); },
+      [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) { put(hb, rbv, cc, r); });
+  auto mul = [&](const Th& h, v4i (&reg)[R > 0 ? R : 1], int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
+    const v4i ah = cc >= 16 - kMulLdsTiles ? hat(h, cc - (16 - kMulLdsTiles))
+                   : cc >= MEM             ? reg[cc - MEM]
+                                           : bld(RS, p4_lane(h), p4_soff(h, cc));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xx[p3(cc, i)] = (uint32_t)mont<true>(ah[i], r[i], T.m) ^ K32;  // (as k_mf_mul)
+    pin4(xx[p3(cc, 0)], xx[p3(cc, 1)], xx[p3(cc, 2)], xx[p3(cc, 3)]);
+  };
+  fwd2<false, S_F4, true, (NP > 0), NP, 0, 4096>(
+      xa, xb, rsrc(b + o, kN * 4u), lds, ha, hb, T,
+      [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) { mul(ha, ra, cc, r, xx); },
+      [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) { mul(hb, rbv, cc, r, xx); });
+  inv2(xa, xb, rsrc(c + o, kN * 4u), lds, ha, hb, T);
 }
 
 // ---------------------------------------------------------------------------
@@ -1460,14 +1693,15 @@ hipError_t launch_mf_tensor(const Launch& k, void* d0, void* d1, void* d2, uint6
 hipError_t launch_mf_mul(const Launch& k, void* c, const void* a, const void* b, uint64_t ls, void* scratch) {
   if (k.B == 0 || k.L == 0) return hipSuccess;
   if (k.B > 0x7fffffffull || k.L > 65535) return hipErrorInvalidConfiguration;
-  const void* fn = (const void*)k_mf_mul;
+  const void* fn = RNT_MF_MUL_V2 ? (const void*)k_mf_mul2 : (const void*)k_mf_mul;
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mf::kLdsBytes);
   if (e != hipSuccess) return e;
   uint32_t slots = (uint64_t)k.B * k.L >= kPlaneSlots ? 1u : 0u;  // plane_scratch_planes
   const void* mft = k.t->mf;
   const LimbConst<uint32_t>* lcs = (const LimbConst<uint32_t>*)k.t->lconst;
   void* args[] = {&c, &a, &b, &ls, &scratch, &slots, &mft, &lcs};
-  return hipLaunchKernel(fn, dim3((unsigned)k.B, (unsigned)k.L), dim3(mf::kT), args, mf::kLdsBytes, k.s);
+  return hipLaunchKernel(fn, dim3((unsigned)k.B, (unsigned)k.L), dim3(RNT_MF_MUL_V2 ? mf::kT / 2 : mf::kT), args,
+                         mf::kLdsBytes, k.s);
 }
 
 #ifdef RNT_MF_TRACE
