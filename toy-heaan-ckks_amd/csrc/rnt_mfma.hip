@@ -1310,6 +1310,12 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
 #ifndef RNT_MF_MUL_MEAS
 #define RNT_MF_MUL_MEAS 0
 #endif
+// RNT_MF_MUL_MEAS_SKIP: the same for the first SKIP slot tiles only (the
+// slot's footprint per XCD shrinks from 32 x 160 KiB: does the rest then stay
+// in the L2?)
+#ifndef RNT_MF_MUL_MEAS_SKIP
+#define RNT_MF_MUL_MEAS_SKIP (RNT_MF_MUL_MEAS ? 16 - kMulLdsTiles : 0)
+#endif
 // RNT_MF_MUL_V2: rnt_mul at 2^16 runs k_mf_mul2 (512 threads, two virtual
 // waves a wave) instead of k_mf_mul.  Off: bit-identical, but two waves a
 // SIMD measured 11% slower at the same power (7.08 against 6.27 ms, the clock
@@ -1363,7 +1369,7 @@ k_mf_mul(uint32_t* c, const uint32_t* a, const uint32_t* b, uint64_t ls, uint32_
   fwd<false, S_F4S, false, RNT_MF_MUL_Q4 != 0, NP, kMulLdsBase * 4, kMulLdsTiles * 1024>(x, rsrc(a + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&)[64]) {
     if (cc >= 16 - kMulLdsTiles)
       hat(cc - (16 - kMulLdsTiles)) = v4i{r[0], r[1], r[2], r[3]};
-    else if (!RNT_MF_MUL_MEAS)
+    else if (cc >= RNT_MF_MUL_MEAS_SKIP)
       bst(v4i{r[0], r[1], r[2], r[3]}, RS, p4_lane(h), p4_soff(h, cc));
   });
   // fwd(b) needs no barrier before its first exchange write with Q4: every
@@ -1371,7 +1377,7 @@ k_mf_mul(uint32_t* c, const uint32_t* a, const uint32_t* b, uint64_t ls, uint32_
   // and fwd(b)'s quarter rounds stay below the a^ tiles
   fwd<!(RNT_MF_MUL_Q4 && RNT_MF_MUL_NOSYNC1), S_F4, RNT_MF_MUL_Q4 != 0, (NP > 0), NP, 0, 4096>(x, rsrc(b + o, kN * 4u), lds, h, T, [&](int cc, const int32_t (&r)[4], uint32_t (&xx)[64]) {
     const v4i ah = cc >= 16 - kMulLdsTiles ? hat(cc - (16 - kMulLdsTiles))
-                   : RNT_MF_MUL_MEAS ? v4i{r[0], r[1], r[2], r[3]} : bld(RS, p4_lane(h), p4_soff(h, cc));
+                   : cc < RNT_MF_MUL_MEAS_SKIP ? v4i{r[0], r[1], r[2], r[3]} : bld(RS, p4_lane(h), p4_soff(h, cc));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       // (a^ 2^32) b^ 2^-32, a signed Montgomery product of two pass
