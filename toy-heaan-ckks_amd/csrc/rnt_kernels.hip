@@ -870,6 +870,13 @@ __device__ __forceinline__ uint32_t ks_pad(uint32_t w) { return w + ((w >> 6) <<
 #ifndef RNT_KS_KLATE
 #define RNT_KS_KLATE 0
 #endif
+// RNT_KS_PAIR (below, KsCfg::PAIR): off -- parity-green (the whole GPU
+// suite), but the second row's 16 registers spill (k_ks_rows<u32, 8, 8>
+// 92 -> 228 bytes a lane): config-4 ct-mul -1.5%, config 3 +1%, the
+// 8-ciphertext rotation -4.3% (profiles/r06/ab_ks_pair.txt)
+#ifndef RNT_KS_PAIR
+#define RNT_KS_PAIR 0
+#endif
 template <class W, int LOG_C, int NP>
 struct KsCfg {
   using G = RowGeo<LOG_C>;
@@ -883,7 +890,13 @@ struct KsCfg {
                                  KROWS * KPAD <= G::REGION;
   static constexpr bool KEYGLDS =
       !KREG && sizeof(W) == 4 && G::C >= 64 && (NP > 1 || LOG_C >= kKsGldsWideMinLogC || KSPLIT);
-  static constexpr int KWORDS = KREG ? 0 : (KDOUBLE ? 4 : KSPLIT ? 1 : 2) * KROWS * KPAD;
+  // PAIR: two source limbs a step (RNT_KS_PAIR): both rows transform
+  // together (NOPS = 2, one twiddle fetch for both) and their two products
+  // share one Montgomery reduction (mac2_lazy); four key-row slots (two
+  // steps in flight x two limbs) beside the exchange region
+  static constexpr bool PAIR = RNT_KS_PAIR && sizeof(W) == 4 && !KREG && KEYGLDS && KDOUBLE && !KSPLIT &&
+                               G::P >= 2 && (size_t)(G::REGION + 8 * KROWS * KPAD) * sizeof(W) <= 40u * 1024u;
+  static constexpr int KWORDS = KREG ? 0 : PAIR ? 8 * KROWS * KPAD : (KDOUBLE ? 4 : KSPLIT ? 1 : 2) * KROWS * KPAD;
   static constexpr size_t LDS_BYTES = (size_t)(G::REGION + KWORDS) * sizeof(W);
 };
 
@@ -909,10 +922,32 @@ __device__ __forceinline__ void ks_lds_read16(W (&o)[16 / sizeof(W)], const W* p
 // half-rate products plus add, subtract and select, where mont_mul + add_mod
 // took two more full-rate ops.  The sum is made canonical once, after the
 // source-limb loop.
+#ifndef RNT_KS_MAC_MEAS
+#define RNT_KS_MAC_MEAS 0
+#endif
 __device__ __forceinline__ uint32_t mac_lazy(uint32_t acc, uint32_t x, uint32_t k, uint32_t q,
                                              uint32_t q2, uint32_t nqinv) {
+  // (RNT_KS_MAC_MEAS: measurement builds only, wrong words by design -- the
+  // key-switch rows with a one-op stand-in for the product, to price it)
+  if constexpr (RNT_KS_MAC_MEAS) return acc + (x ^ k);
   const uint64_t T = mul64(x, k);
   const uint32_t m = (uint32_t)T * nqinv;  // -T q^-1 mod 2^32
+  const uint32_t t = (uint32_t)(mad64(m, q, T) >> 32);
+  uint32_t s, d;
+  const bool carry = __builtin_add_overflow(acc, t, &s);
+  const bool borrow = __builtin_sub_overflow(s, q2, &d);
+  return (carry || !borrow) ? d : s;
+}
+// Two terms, one reduction: canonical x0, x1, k0, k1 < q < 2^31 give
+// T = x0 k0 + x1 k1 < 2q^2 < 2^63 and T + m q < 2^64, so the shared
+// Montgomery term t = (T + m q) / 2^32 < 2q^2 / 2^32 + q < 2q: the same
+// [0, 2q) term mac_lazy adds, for two products (two multiply-adds, one
+// reduction) instead of one.
+__device__ __forceinline__ uint32_t mac2_lazy(uint32_t acc, uint32_t x0, uint32_t k0, uint32_t x1, uint32_t k1,
+                                              uint32_t q, uint32_t q2, uint32_t nqinv) {
+  if constexpr (RNT_KS_MAC_MEAS) return acc + (x0 ^ k0) + (x1 ^ k1);
+  const uint64_t T = mad64(x1, k1, mul64(x0, k0));
+  const uint32_t m = (uint32_t)T * nqinv;
   const uint32_t t = (uint32_t)(mad64(m, q, T) >> 32);
   uint32_t s, d;
   const bool carry = __builtin_add_overflow(acc, t, &s);
@@ -1011,7 +1046,111 @@ k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
     acc[1][e] = init1 ? init1[ibase + pos] : (W)0;
   }
   constexpr uint32_t KW = (uint32_t)(KROWS * C);  // words per key
-  if constexpr (K::KREG) {
+  if constexpr (K::PAIR) {
+    // the off-diagonal sources two a step (the last alone when their count
+    // is odd), then the diagonal alone (the tensor's d2^ row, no transform)
+    const bool dg = d2hat != nullptr && j < L;
+    const uint32_t n = dg ? L - 1 : L;
+    const uint32_t steps = (n + 1) / 2 + (dg ? 1u : 0u);
+    auto src_of = [&](uint32_t t) { return dg && t >= j ? t + 1 : t; };
+    constexpr uint32_t SEG = KW / 64;  // 64-word segments per key
+    constexpr int WAVES = G::THREADS / 64;
+    constexpr uint32_t SLOT = 2 * KROWS * KPAD;  // both keys' rows of one source limb
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    // both keys' rows of source limb i, global -> LDS (one segment per wave
+    // instruction, as the one-limb loop below)
+    auto keys_to = [&](uint32_t i, W* kb) {
+      const uint64_t kbase = (uint64_t)j * key_ls + (uint64_t)i * N + (WIDE ? (uint64_t)rbase * G::C : rowoff);
+#pragma unroll
+      for (int m = 0; m < (int)((2 * SEG + WAVES - 1) / WAVES); ++m) {
+        const uint32_t sg = wave + (uint32_t)m * WAVES;
+        if (sg < 2 * SEG) {
+          const uint32_t kk = sg >= SEG, rs = kk ? sg - SEG : sg;
+          const W* src = (kk ? key_a : key_b) + kbase + rs * 64u + lane;
+          W* dst = kb + kk * (KROWS * KPAD) + (rs / (C / 64)) * KPAD + ks_pad((rs % (C / 64)) * 64u);
+          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
+        }
+      }
+    };
+    auto s_row = [&](uint32_t i, W (&v)[E]) {
+      const uint64_t sbase = (((uint64_t)j * L + i) * B + rp.p) * N + rowoff;
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[e] = S[sbase + b0 + ((uint32_t)e << G::BB0)];
+    };
+    auto kptr = [&](const W* kb, int o) {
+      return kb + o * KROWS * KPAD + (WIDE ? (rp.xp.slot / NP) * KPAD : 0u) + ks_pad(bl);
+    };
+#pragma unroll 1
+    for (uint32_t st = 0; st < steps; ++st) {
+      // key slots: two steps in flight (the transform's exchange barriers of
+      // step st - 1 order every read of step st - 2's slot before this write)
+      W* kb = kbuf + (st & 1u) * 2 * SLOT;
+      const uint32_t t0 = 2 * st;
+      if (t0 + 1 < n) {
+        const uint32_t i0 = src_of(t0), i1 = src_of(t0 + 1);
+        keys_to(i0, kb);
+        keys_to(i1, kb + SLOT);
+        // the DMA issues before the S loads, so the transform's first vmcnt
+        // wait covers it and its exchange barriers publish the slot
+        __builtin_amdgcn_sched_barrier(0);
+        W x[2][E];
+        s_row(i0, x[0]);
+        s_row(i1, x[1]);
+        xf_fwd<G, W, 2>(x, rp.xp, lds, tw, mod_of(lc));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          const W* k0 = kptr(kb, o);
+          const W* k1 = kptr(kb + SLOT, o);
+#pragma unroll
+          for (int e0 = 0; e0 < E; e0 += 4) {
+            W kv0[4], kv1[4];
+            ks_lds_read16<W>(kv0, k0 + e0);
+            ks_lds_read16<W>(kv1, k1 + e0);
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              acc[o][e0 + v] = mac2_lazy(acc[o][e0 + v], x[0][e0 + v], kv0[v], x[1][e0 + v], kv1[v], lc.q, q2, nqinv);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        // one source: the odd one out, or the diagonal (the last step: no
+        // transform, so a barrier before its key write and one after)
+        const bool diag = t0 >= n;
+        const uint32_t i0 = diag ? j : src_of(t0);
+        if (diag) __syncthreads();
+        keys_to(i0, kb);
+        __builtin_amdgcn_sched_barrier(0);
+        W x[1][E];
+        if (diag) {
+          const uint64_t hb = (uint64_t)j * d2hat_ls + (uint64_t)rp.p * N + rowoff + bl;
+#pragma unroll
+          for (int e = 0; e < E; ++e) x[0][e] = d2hat[hb + (uint32_t)e];
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's key DMA has landed
+          __syncthreads();
+        } else {
+          s_row(i0, x[0]);
+          xf_fwd<G, W, 1>(x, rp.xp, lds, tw, mod_of(lc));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          const W* kk = kptr(kb, o);
+#pragma unroll
+          for (int e0 = 0; e0 < E; e0 += 4) {
+            W kv[4];
+            ks_lds_read16<W>(kv, kk + e0);
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+              acc[o][e0 + v] = mac_lazy(acc[o][e0 + v], x[0][e0 + v], kv[v], lc.q, q2, nqinv);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  } else if constexpr (K::KREG) {
     // the source row of limb i: S[j][i][p] in the first pass's layout, or on
     // the diagonal the tensor's exact d2^ row in the last pass's (no
     // transform, so no LDS and no barrier that iteration: every wave passes
