@@ -870,6 +870,12 @@ __device__ __forceinline__ uint32_t ks_pad(uint32_t w) { return w + ((w >> 6) <<
 #ifndef RNT_KS_KLATE
 #define RNT_KS_KLATE 0
 #endif
+// RNT_KS_KREG_WAVES: the KREG grid's occupancy bound (workgroups a CU the
+// launch bounds promise): 2 gives its registers room (256 VGPRs: the keys and
+// the next S row in flight without spills) at half the resident waves
+#ifndef RNT_KS_KREG_WAVES
+#define RNT_KS_KREG_WAVES 4
+#endif
 // RNT_KS_PAIR (below, KsCfg::PAIR): off -- parity-green (the whole GPU
 // suite), but the second row's 16 registers spill (k_ks_rows<u32, 8, 8>
 // 92 -> 228 bytes a lane): config-4 ct-mul -1.5%, config 3 +1%, the
@@ -966,7 +972,7 @@ __device__ __forceinline__ uint32_t mac2_lazy(uint32_t acc, uint32_t x0, uint32_
 // per source limb instead of three (S, then key_b, then key_a), and 2 key
 // words per thread instead of 2E (A/B: profiles/r02_ab_ks_rows.txt).
 template <class W, int LOG_C, int NP>
-__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? RNT_KS_ROWS_WAVES : 1)
+__global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, (KsCfg<W, LOG_C, NP>::KREG ? RNT_KS_KREG_WAVES : sizeof(W) == 4 ? RNT_KS_ROWS_WAVES : 1))
 k_ks_rows(W* __restrict__ u0, W* __restrict__ u1, const W* __restrict__ S,
           const W* __restrict__ key_a, const W* __restrict__ key_b, uint64_t key_ls,
           const W* __restrict__ init0, const W* __restrict__ init1, uint64_t init_ls,
