@@ -713,10 +713,20 @@ bool mul_truncated(const Tables* t) {
 #ifndef RNT_U64_LZ_WAVES
 #define RNT_U64_LZ_WAVES 3
 #endif
+// RNT_U64_WHOLE_WAVES / RNT_U64_WHOLE_LZ: the u64 whole-plane product's
+// occupancy bound (4: two 512-thread workgroups a CU at 128 VGPRs; 2: one
+// at 256) and its arithmetic (1: Harvey-lazy where every q < 2^62)
+#ifndef RNT_U64_WHOLE_WAVES
+#define RNT_U64_WHOLE_WAVES 4
+#endif
+#ifndef RNT_U64_WHOLE_LZ
+#define RNT_U64_WHOLE_LZ 0
+#endif
 template <class W, int MODE, int LOG_C, bool LZ = false, bool WHOLE = false>
 __global__ void __launch_bounds__(RowGeo<LOG_C>::THREADS, sizeof(W) == 4 ? (WHOLE ? kWholeMinWaves : kRowMinWaves)
                                                                  : (MODE == 2 && LOG_C >= (WHOLE ? 13 : 7)
-                                                                        ? (LZ && !WHOLE ? RNT_U64_LZ_WAVES : 4)
+                                                                        ? (LZ && !WHOLE ? RNT_U64_LZ_WAVES
+                                                                                        : WHOLE ? RNT_U64_WHOLE_WAVES : 4)
                                                                         : 1))
 k_row(W* __restrict__ xg, const W* __restrict__ yg, W* __restrict__ outg, TabPtrs<W> tp, uint32_t log_n,
       uint32_t B, uint64_t ls, uint64_t rows_total) {
@@ -2377,7 +2387,7 @@ hipError_t launch_whole(const Launch& k, int mode, void* out, void* x, const voi
   // canonical) and measured 6.3% slower at the horner_chain.rs shape,
   // 2^13 x 7 x 61-bit (0.792M against 0.845M poly-muls/s, same box,
   // profiles/r06/ab_lazy62.txt); the u64 four-step product takes it (+7.9%)
-  const bool lz = !k.t->wide && k.t->lazy30 != 0;
+  const bool lz = k.t->wide ? (RNT_U64_WHOLE_LZ && k.t->lazy62 != 0) : k.t->lazy30 != 0;
   RNT_WIDE(whole_t<uint32_t>(k, mode, out, x, y, ls, lz), whole_t<uint64_t>(k, mode, out, x, y, ls, lz));
 }
 hipError_t launch_col_inv(const Launch& k, void* out, uint64_t out_ls, const void* in,
