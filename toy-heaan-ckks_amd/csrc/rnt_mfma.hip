@@ -1310,6 +1310,12 @@ k_mf_tensor(uint32_t* __restrict__ d0, uint32_t* __restrict__ d1, uint32_t* __re
 #ifndef RNT_MF_MUL_MEAS
 #define RNT_MF_MUL_MEAS 0
 #endif
+// RNT_MF_SLOT_ST_AUX: cache-policy bits of k_mf_mul's a^ slot stores (0:
+// default; 2: nt; 16: sc1, which drops the line from the L2 -- the slot is
+// read back from HBM in any case, profiles/r06/ab_mf_mul_slot_skip.txt)
+#ifndef RNT_MF_SLOT_ST_AUX
+#define RNT_MF_SLOT_ST_AUX 0
+#endif
 // RNT_MF_MUL_MEAS_SKIP: the same for the first SKIP slot tiles only (the
 // slot's footprint per XCD shrinks from 32 x 160 KiB: does the rest then stay
 // in the L2?)
@@ -1370,7 +1376,7 @@ k_mf_mul(uint32_t* c, const uint32_t* a, const uint32_t* b, uint64_t ls, uint32_
     if (cc >= 16 - kMulLdsTiles)
       hat(cc - (16 - kMulLdsTiles)) = v4i{r[0], r[1], r[2], r[3]};
     else if (cc >= RNT_MF_MUL_MEAS_SKIP)
-      bst(v4i{r[0], r[1], r[2], r[3]}, RS, p4_lane(h), p4_soff(h, cc));
+      bst<RNT_MF_SLOT_ST_AUX>(v4i{r[0], r[1], r[2], r[3]}, RS, p4_lane(h), p4_soff(h, cc));
   });
   // fwd(b) needs no barrier before its first exchange write with Q4: every
   // wave passed fwd(a)'s SYNCX after its last read of fwd(a)'s exchange,
