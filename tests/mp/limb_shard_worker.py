@@ -1,6 +1,7 @@
 """One rank of the multi-process limb-sharded pipeline test
 (tests/test_gpu_multiproc.py): launched by torch.distributed.run with
-world_size 2 on ONE GPU, gloo process group.  Each rank runs
+world_size 2 on ONE GPU, gloo process group (or world_size 1 over RCCL,
+--backend nccl).  Each rank runs
 LimbShardedPipeline with GpuBackend on device 0 -- its limbs in its own
 library context, the joins (all-gather of d2 / sigma(c1), broadcast of the
 last limb) as torch collectives between the processes over buffers the
@@ -26,6 +27,8 @@ def main():
     ap.add_argument("--shared", action="store_true",
                     help="queue torch's ops and the joins on the library's stream (GpuBackend.shared_stream)")
     ap.add_argument("--chunk", type=int, default=None)
+    ap.add_argument("--backend", default="gloo", choices=["gloo", "nccl"],
+                    help="the process group of the joins (nccl = RCCL: one GPU per rank)")
     args = ap.parse_args()
 
     import rns_ntt  # noqa: F401  (loads librnsntt before torch initialises HIP)
@@ -34,9 +37,9 @@ def main():
 
     from rns_ntt.sharded import GpuBackend, LimbShardedPipeline, TorchDistComm
 
-    dist.init_process_group("gloo")
-    rank = dist.get_rank()
     torch.cuda.set_device(0)
+    dist.init_process_group(args.backend)
+    rank = dist.get_rank()
     z = np.load(args.inputs)
     mod = [int(q) for q in z["moduli"]]
     n = int(z["n"])
