@@ -27,8 +27,9 @@ def main():
     ap.add_argument("--shared", action="store_true",
                     help="queue torch's ops and the joins on the library's stream (GpuBackend.shared_stream)")
     ap.add_argument("--chunk", type=int, default=None)
-    ap.add_argument("--backend", default="gloo", choices=["gloo", "nccl"],
-                    help="the process group of the joins (nccl = RCCL: one GPU per rank)")
+    ap.add_argument("--backend", default="gloo", choices=["gloo", "nccl", "gloo+nccl"],
+                    help="the process group of the joins (nccl = RCCL: one GPU per rank); gloo+nccl: "
+                         "bench.py's layout, a gloo default group and an nccl group for the joins")
     args = ap.parse_args()
 
     import rns_ntt  # noqa: F401  (loads librnsntt before torch initialises HIP)
@@ -38,15 +39,16 @@ def main():
     from rns_ntt.sharded import GpuBackend, LimbShardedPipeline, TorchDistComm
 
     torch.cuda.set_device(0)
-    dist.init_process_group(args.backend)
+    dist.init_process_group(args.backend.split("+")[0])
     rank = dist.get_rank()
+    data_group = dist.new_group(backend="nccl") if args.backend == "gloo+nccl" else None
     z = np.load(args.inputs)
     mod = [int(q) for q in z["moduli"]]
     n = int(z["n"])
     import contextlib
 
     be = GpuBackend(0)
-    pipe = LimbShardedPipeline(mod, n, TorchDistComm(), be, chunk=args.chunk)
+    pipe = LimbShardedPipeline(mod, n, TorchDistComm(data_group), be, chunk=args.chunk)
     scope = torch.cuda.stream(be.shared_stream(pipe.basis)) if args.shared else contextlib.nullcontext()
     scope.__enter__()
     c = [pipe.upload(z[k]) for k in ("c0", "c1", "c0p", "c1p")]

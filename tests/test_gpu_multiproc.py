@@ -68,13 +68,16 @@ def test_two_process_limb_sharded_pipeline(gpu, tmp_path, shared):
         assert np.array_equal(res0[p], orc.rescale(Bo, m0)) and np.array_equal(res1[p], orc.rescale(Bo, m1)), p
 
 
-def test_single_rank_rccl_limb_pipeline(gpu, tmp_path):
+@pytest.mark.parametrize("backend", ["nccl", "gloo+nccl"])
+def test_single_rank_rccl_limb_pipeline(gpu, tmp_path, backend):
     """The joins over RCCL itself (backend nccl, the driver's multi-GPU
     layout), at the one rank a one-GPU box allows: rotate_ciphertext's
     all-gather of sigma(c1), mul_ciphertexts_gadget's all-gather of d2 (both
     all_gather_into_tensor: equal limb counts) and rescale_ciphertext's
     broadcast of the last limb run as RCCL collectives on the library's
-    buffers (rnt_buf_wrap), bit-exact against the oracle."""
+    buffers (rnt_buf_wrap), bit-exact against the oracle.  gloo+nccl is
+    bench.py's layout: a gloo default group (control plane) and the joins on
+    dist.new_group(backend="nccl")."""
     rn = gpu
     n, L, B, k = 1 << 12, 4, 3, 5
     mod = rn.generate_primes(31, L, n)
@@ -87,9 +90,9 @@ def test_single_rank_rccl_limb_pipeline(gpu, tmp_path):
     out = str(tmp_path / "res")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0", NCCL_SOCKET_IFNAME="lo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr", "127.0.0.1", "--master-port", "29631",
+           "--master-addr", "127.0.0.1", "--master-port", str(29631 + (backend != "nccl")),
            os.path.join(REPO, "tests", "mp", "limb_shard_worker.py"), "--inputs", inp, "--out", out,
-           "--backend", "nccl"]
+           "--backend", backend]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     r = np.load(f"{out}.rank0.npz")
