@@ -424,3 +424,40 @@ def test_keyswitch_diagonal_from_tensor(gpu, monkeypatch, log_n, L, B, bits):
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     w0, w1 = orc.mul_ciphertexts_gadget(Bo, c0[0], c1[0], c0p[0], c1p[0], ka, kb, threads=T)
     assert np.array_equal(outs[0][0][0], w0) and np.array_equal(outs[0][1][0], w1)
+
+
+@pytest.mark.parametrize("log_n,L,B,k", [(14, 8, 5, 3), (16, 6, 3, -7), (17, 4, 2, 1 << 12)])
+def test_rotation_fused_sigma_c0(gpu, monkeypatch, log_n, L, B, k):
+    """rnt_ct_rotate gathers sigma(c0) inside the key-switch's inverse column
+    pass (k_colt_inv's addend with g^-1 mod 2N) instead of a launch of its
+    own: word for word the RNT_ROT_FUSE=0 path (k_automorph_odd into a
+    scratch plane), over several key-switch chunks (RNT_KS_WS_MB=1 at 2^14),
+    and the in-place call (out0 = c0, which keeps the separate launch), and
+    the oracle on the first and last ciphertext (engine.rs:412-463)."""
+    rn = gpu
+    n = 1 << log_n
+    mod = rn.generate_primes(31, L, n)
+    Bo = orc.Basis(mod, n)
+    rng = np.random.default_rng(1300 + log_n)
+    c0, c1 = _rand(rng, mod, n, B), _rand(rng, mod, n, B)
+    ka, kb = _rand(rng, mod, n, L), _rand(rng, mod, n, L)
+    if log_n == 14:
+        monkeypatch.setenv("RNT_KS_WS_MB", "1")  # one ciphertext a chunk: five chunks
+    outs = []
+    for fuse in ("2", "0"):
+        monkeypatch.setenv("RNT_ROT_FUSE", fuse)  # read at rnt_ctx_create (2: fused at any batch)
+        Bd = rn.RnsBasis(mod, n)
+        rotk = rn.RnsGadgetKey.from_channels(ka, kb, Bd, rotation=k)
+        x0, x1 = rn.RnsPoly.from_channels(c0, Bd), rn.RnsPoly.from_channels(c1, Bd)
+        r = rn.rotate_ciphertext(rn.Ciphertext(x0, x1), rotk)
+        outs.append((r.c0.channels(), r.c1.channels()))
+        if fuse == "2":
+            o1 = rn.RnsPoly(Bd, B)
+            rn.check(rn.load().rnt_ct_rotate(x0.handle, o1.handle, x0.handle, x1.handle, int(k),
+                                              rotk.a.handle, rotk.b.handle))
+            outs.append((x0.channels(), o1.channels()))
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1])
+    for p in (0, B - 1):
+        w0, w1 = orc.rotate_ciphertext(Bo, c0[p], c1[p], k, ka, kb, threads=T)
+        assert np.array_equal(outs[0][0][p], w0) and np.array_equal(outs[0][1][p], w1), p

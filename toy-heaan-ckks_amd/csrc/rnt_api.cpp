@@ -787,6 +787,7 @@ extern "C" int rnt_ctx_create(uint32_t log_n, const uint64_t* moduli, size_t cou
     // limb i) from the tensor's exact d2^ instead of transforming it;
     // RNT_KS_DIAG=0 transforms every (i, j) (A/B)
     t->ks_diag = env_long("RNT_KS_DIAG", 1) != 0;
+    t->rot_fuse = (int)env_long("RNT_ROT_FUSE", 1);
     // the whole-plane product and MFMA transforms are the default where they
     // apply (N = 2^16, u32); RNT_PLANE=0 keeps the four-step kernels
     t->plane = env_long("RNT_PLANE", 1) != 0 ? 1 : 0;
@@ -2267,6 +2268,16 @@ extern "C" int rnt_ct_rotate(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, co
   // ws: SIG0 | SIG1 | [TMP when an input is NTT-domain] | key-switch chunk space
   const size_t bc = ks_chunk(k.t, L, B);
   const bool any_ntt = c0->in_ntt || c1->in_ntt;
+  // sigma(c0) needs no launch of its own on the tiled four-step key-switch:
+  // its inverse column pass gathers it from c0 as it adds it (k_colt_inv's
+  // addend with g^-1 mod 2N).  Only for one ciphertext by default
+  // (RNT_ROT_FUSE=1; 2: any batch, 0: never): the scattered 4-byte gather
+  // costs the inverse about what the automorphism launch costs, which at one
+  // ciphertext is mostly launch and tail (config 5: +2.0% at one ciphertext,
+  // -0.5% at eight, profiles/r06/ab_rot_fuse.txt).  Not in place on out0: a
+  // workgroup's gather would race the stores of the others on the same plane
+  const bool fuse0 = (k.t->rot_fuse == 2 || (k.t->rot_fuse == 1 && B == 1)) && (g & 1) && !c0->in_ntt &&
+                     !rnt::ks_whole_ok(k.t) && rnt::col_resc_ok(k.t) && out0->data != c0->data;
   const size_t tmp_words = any_ntt ? words : 0;
   CallWs ws(out0);
   if (int rc = ws.get((2 * words + tmp_words + ks_scratch_words(k.t, L, bc)) * wb)) return rc;
@@ -2276,7 +2287,7 @@ extern "C" int rnt_ct_rotate(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, co
   char* KS = tmp + tmp_words * wb;
   // sigma(c0), sigma(c1) in coefficient domain (engine.rs:417-419; poly.rs:494-504
   // converts an NTT-domain input first)
-  for (int i = 0; i < 2; ++i) {
+  for (int i = fuse0 ? 1 : 0; i < 2; ++i) {
     const rnt_buf* src = i ? c1 : c0;
     char* dst = i ? sig1 : sig0;
     const void* s = src->data;
@@ -2291,10 +2302,17 @@ extern "C" int rnt_ct_rotate(rnt_buf* out0, rnt_buf* out1, const rnt_buf* c0, co
   sview.n_polys = B;
   sview.data = sig1;
   const uint64_t ls = limb_stride(c0);
+  rnt::Launch kr = k;
+  if (fuse0) {
+    // g^-1 mod 2N (g odd): Newton's iteration mod 2^64, then the mask
+    uint64_t x = g;
+    for (int it = 0; it < 6; ++it) x *= 2 - g * x;
+    kr.add_ginv = (uint32_t)(x & (2 * (uint64_t)n - 1));
+  }
   for (size_t p0 = 0; p0 < B; p0 += bc) {
     const size_t c = std::min(bc, B - p0);
-    if (int rc = ks_chunk_run(k, KS, &sview, p0, c, key_a, key_b, out0->data, out1->data, ls,
-                              nullptr, nullptr, 0, sig0, 0))
+    if (int rc = ks_chunk_run(kr, KS, &sview, p0, c, key_a, key_b, out0->data, out1->data, ls,
+                              nullptr, nullptr, 0, fuse0 ? c0->data : sig0, 0))
       return rc;
   }
   sview.data = nullptr;

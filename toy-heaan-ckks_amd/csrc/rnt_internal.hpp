@@ -83,6 +83,7 @@ struct Tables {
   bool lazy30 = false;     // every modulus < 2^30: Harvey-lazy product path (u32)
   bool lazy62 = false;     // u64 words, every modulus < 2^62: the same for u64
   bool ks_diag = true;     // ct-mul key-switch diagonal from the tensor's d2^ (RNT_KS_DIAG)
+  int rot_fuse = 1;        // rotation: sigma(c0) gathered by the key-switch inverse (RNT_ROT_FUSE: 1 one ct, 2 any, 0 off)
   int plane = 0;           // the whole-plane kernels where they apply (plane_ok, mf_ok);
   int mf_mul = 1;          // rnt_mul at N = 2^16 on the matrix-core transforms (RNT_MF_MUL=0: k_plane_fused)
                            // RNT_PLANE=0: the four-step kernels everywhere
@@ -191,6 +192,10 @@ struct Launch {
   // key-switch rows read them instead of transforming S (nullptr: off)
   void* d2hat = nullptr;
   uint64_t d2hat_ls = 0;
+  // The rotation's sigma_g(c0) read straight from c0 by the key-switch
+  // inverse's addend (g^-1 mod 2N, odd; 0: the addend as it is): no
+  // separate automorphism launch for c0 (tiled column grids only)
+  uint32_t add_ginv = 0;
   size_t src_limbs() const { return Ls ? Ls : L; }
 };
 

@@ -565,7 +565,7 @@ k_colt_fwd(W* out0, const W* in0, W* out1, const W* in1, TabPtrs<W> tp, uint32_t
 template <class W, int LOG_R, int LOG_TC, bool LZ = false>
 __global__ void __launch_bounds__((ColGeo<LOG_R, LOG_TC>::THREADS))
 k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, uint32_t log_c,
-           uint32_t B, uint64_t in_ls, uint64_t out_ls, int rfold, ColResc<W> rs) {
+           uint32_t B, uint64_t in_ls, uint64_t out_ls, int rfold, ColResc<W> rs, uint32_t aginv) {
   using G = ColGeo<LOG_R, LOG_TC>;
   constexpr int E = G::E;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -591,8 +591,21 @@ k_colt_inv(W* out, const W* in, const W* addend, TabPtrs<W> tp, uint32_t log_n, 
   a0.refresh();
   if (addend != nullptr) {
     const BufView<W> ad(addend + op, N);
+    if (aginv != 0) {
+      // the addend is sigma_g of the plane at `addend` (rnt_ct_rotate's
+      // sigma(c0)): position pos takes its word t mod N, negated mod q when
+      // t >= N, t = pos g^-1 mod 2N -- k_automorph_odd's gather (poly.rs:520-537)
 #pragma unroll
-    for (int i = 0; i < E; ++i) x[0][i] = add_mod<W>(x[0][i], ad.ld(a0.v, i * a0.s), lc.q);
+      for (int i = 0; i < E; ++i) {
+        const uint32_t pos = a0.v + (uint32_t)i * a0.s;
+        const uint32_t t = (pos * aginv) & (2u * N - 1u);
+        const W c = ad.ld(t & (N - 1u), 0u);
+        x[0][i] = add_mod<W>(x[0][i], (t >= N && c != 0) ? (W)(lc.q - c) : c, lc.q);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < E; ++i) x[0][i] = add_mod<W>(x[0][i], ad.ld(a0.v, i * a0.s), lc.q);
+    }
   }
   if (rs.last != nullptr) {
     // the fused rescale (rescale_ciphertext, engine.rs:263-282; poly.rs:187-228):
@@ -1928,7 +1941,7 @@ static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const v
   if (e != hipSuccess) return e;                                                             \
   hipLaunchKernelGGL((k_colt_inv<W, R, TC, LZ>), grid, dim3(ColGeo<R, TC>::THREADS),             \
                      (col_lds<W, R, TC>()), k.s, (W*)out, (const W*)in, (const W*)addend, tp, \
-                     g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls, rfold, rs)
+                     g.log_n, g.log_c, (uint32_t)k.B, in_ls, out_ls, rfold, rs, k.add_ginv)
 #define RNT_L(R)                          \
   if (col_log_tc(g) == 6) {               \
     RNT_L2(R, 6);                         \
@@ -1940,7 +1953,8 @@ static hipError_t col_inv_t(const Launch& k, void* out, uint64_t out_ls, const v
 #undef RNT_L2
     return hipGetLastError();
   }
-  if (ra.last != nullptr || ra.limb0 != 0) return hipErrorInvalidValue;  // tiled grids only (log R >= 5)
+  if (ra.last != nullptr || ra.limb0 != 0 || (addend != nullptr && k.add_ginv != 0))
+    return hipErrorInvalidValue;  // tiled grids only (log R >= 5)
   const uint64_t total = (uint64_t)k.L * k.B * g.c;
 #define RNT_L(R)                                                                          \
   hipLaunchKernelGGL((k_col_inv<W, R>), dim3(grid_for(total, 256)), dim3(256), 0, k.s,  \
